@@ -1,0 +1,78 @@
+"""ctypes binding of libdx.so (include/dx.h).
+
+The library is built in-tree (`dexterity_amd/libdx.so`, see `build.py`).  There is
+deliberately no fallback: if the HIP library is missing or cannot reach a GPU,
+every entry point raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libdx.so")
+
+# dx_field
+QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
+SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER = 6, 7, 8, 9, 10, 11, 12
+INT_FIELDS = (NCON, GROUND_CONTACT, NITER)
+
+EXPORTS = (
+    "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_field_width",
+    "dx_batch_create", "dx_batch_destroy", "dx_batch_nenv", "dx_reset",
+    "dx_set_field", "dx_get_field", "dx_field_ptr", "dx_set_xfrc", "dx_set_ground_geom",
+    "dx_set_watch", "dx_step", "dx_forward", "dx_stream", "dx_sync",
+    "dx_debug_enable", "dx_debug_get", "dx_last_error", "dx_abi_version",
+)
+
+_lib = None
+
+
+class DxError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise DxError(
+            f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    L = ctypes.CDLL(path)
+    vp, i32, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t
+    L.dx_model_load.restype = vp
+    L.dx_model_load.argtypes = [ctypes.c_char_p, sz]
+    L.dx_model_free.argtypes = [vp]
+    L.dx_model_sizes.argtypes = [vp, ctypes.POINTER(i32)]
+    L.dx_field_width.argtypes = [vp, ctypes.c_int]
+    L.dx_batch_create.restype = vp
+    L.dx_batch_create.argtypes = [vp, i32, i32]
+    L.dx_batch_destroy.argtypes = [vp]
+    L.dx_batch_nenv.argtypes = [vp]
+    L.dx_reset.argtypes = [vp, i32, i32]
+    L.dx_set_field.argtypes = [vp, ctypes.c_int, vp, i32, i32]
+    L.dx_get_field.argtypes = [vp, ctypes.c_int, vp, i32, i32]
+    L.dx_field_ptr.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.dx_set_xfrc.argtypes = [vp, vp, i32]
+    L.dx_set_ground_geom.argtypes = [vp, i32]
+    L.dx_set_watch.argtypes = [vp, i32, i32]
+    L.dx_step.argtypes = [vp, i32]
+    L.dx_forward.argtypes = [vp]
+    L.dx_stream.restype = vp
+    L.dx_stream.argtypes = [vp]
+    L.dx_sync.argtypes = [vp]
+    L.dx_debug_enable.argtypes = [vp, ctypes.c_int]
+    L.dx_debug_get.argtypes = [vp, ctypes.c_char_p, vp, sz]
+    L.dx_last_error.restype = ctypes.c_char_p
+    L.dx_abi_version.restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise DxError(f"libdx error {rc}: {load().dx_last_error().decode()}")
+    return rc

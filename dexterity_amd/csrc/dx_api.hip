@@ -1,0 +1,625 @@
+// dx_api.hip -- host implementation of include/dx.h.
+//
+// dx_model_load parses the compiled-model blob (fp64 arrays from the build-time
+// compiler), derives the tables the kernels index (tree levels, dof chain
+// bitmasks, friction/limit row maps, dense fixed-tendon Jacobians), converts to
+// fp32 and uploads one read-only copy per device.  dx_batch owns the per-env
+// state arrays ([nenv][width], fp32) and a HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/dx.h"
+#include "dx_internal.h"
+
+extern "C" __global__ void dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode);
+extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int n);
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess) return fail(DX_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" const char* dx_last_error(void) { return g_err.c_str(); }
+extern "C" int dx_abi_version(void) { return DX_ABI_VERSION; }
+
+// ------------------------------------------------------------------------ //
+// blob parsing
+// ------------------------------------------------------------------------ //
+struct BlobArr {
+  int dtype;
+  long n;
+  const void* p;
+};
+
+static bool parse_blob(const unsigned char* b, size_t nbytes, std::map<std::string, BlobArr>& out) {
+  if (nbytes < 16 || memcmp(b, "DXMBLOB1", 8) != 0) return false;
+  long n;
+  memcpy(&n, b + 8, 8);
+  if (n < 0 || 16 + n * 72 > (long)nbytes) return false;
+  for (long i = 0; i < n; i++) {
+    const unsigned char* e = b + 16 + i * 72;
+    char name[49];
+    memcpy(name, e, 48);
+    name[48] = 0;
+    int code;
+    long cnt, off;
+    memcpy(&code, e + 48, 4);
+    memcpy(&cnt, e + 56, 8);
+    memcpy(&off, e + 64, 8);
+    size_t esz = code == 0 ? 4 : 8;
+    if (off < 0 || cnt < 0 || (size_t)off + cnt * esz > nbytes) return false;
+    out[name] = BlobArr{code, cnt, b + off};
+  }
+  return true;
+}
+
+struct dx_model {
+  std::vector<unsigned char> blob;
+  std::map<std::string, BlobArr> arr;
+  // host copies (fp32 / int) of every device array, keyed by name
+  std::map<std::string, std::vector<float>> hf;
+  std::map<std::string, std::vector<int>> hi;
+  std::vector<uint64_t> body_chain;
+  DevModel dm;  // host-side scalars; pointers filled per device
+  std::map<int, std::vector<void*>> dev_allocs;
+  std::map<int, DevModel> dev_models;
+  Lds lds;
+  int ncon_max, nefc_max;
+};
+
+static int geti(const dx_model* m, const char* name, int def = -1) {
+  auto it = m->arr.find(name);
+  if (it == m->arr.end() || it->second.dtype != 0 || it->second.n < 1) return def;
+  return ((const int*)it->second.p)[0];
+}
+static double getd(const dx_model* m, const char* name, double def = 0) {
+  auto it = m->arr.find(name);
+  if (it == m->arr.end() || it->second.dtype != 1 || it->second.n < 1) return def;
+  return ((const double*)it->second.p)[0];
+}
+static bool load_f(dx_model* m, const char* name) {
+  auto it = m->arr.find(name);
+  if (it == m->arr.end() || it->second.dtype != 1) return false;
+  const double* p = (const double*)it->second.p;
+  m->hf[name].assign(p, p + it->second.n);
+  return true;
+}
+static bool load_i(dx_model* m, const char* name) {
+  auto it = m->arr.find(name);
+  if (it == m->arr.end() || it->second.dtype != 0) return false;
+  const int* p = (const int*)it->second.p;
+  m->hi[name].assign(p, p + it->second.n);
+  return true;
+}
+static void quat2mat_h(float* R, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+static const char* kFloatArrays[] = {
+    "body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia", "body_bsphere",
+    "body_invweight0", "jnt_pos", "jnt_axis", "jnt_range", "jnt_margin", "jnt_solref", "jnt_solimp",
+    "qpos0", "dof_armature", "dof_damping", "dof_frictionloss", "dof_solref", "dof_solimp",
+    "dof_invweight0", "geom_size", "geom_pos", "geom_quat", "geom_center", "geom_bsphere", "mesh_vert",
+    "site_pos", "site_quat", "tendon_range", "tendon_margin", "tendon_solref", "tendon_solimp",
+    "tendon_invweight0", "wrap_coef", "actuator_gear", "actuator_gainprm", "actuator_biasprm",
+    "actuator_ctrlrange", "actuator_forcerange", "gpair_friction", "gpair_solref", "gpair_solimp",
+    "gpair_margin", "gravity"};
+static const char* kIntArrays[] = {
+    "body_parent", "body_rootid", "body_jntnum", "body_jntadr", "body_dofnum", "body_dofadr",
+    "jnt_type", "jnt_bodyid", "jnt_qposadr", "jnt_dofadr", "jnt_limited", "dof_bodyid",
+    "dof_parentid", "dof_jntid", "geom_type", "geom_bodyid", "geom_dataid", "mesh_vertadr",
+    "mesh_vertnum", "site_bodyid", "tendon_adr", "tendon_num", "tendon_limited", "wrap_dof",
+    "actuator_trntype", "actuator_trnid", "actuator_biastype", "actuator_ctrllimited",
+    "actuator_forcelimited", "bpair_body", "bpair_adr", "bpair_num", "gpair_geom", "gpair_condim"};
+
+extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
+  if (!blob) { fail(DX_EINVAL, "null blob"); return nullptr; }
+  dx_model* m = new dx_model();
+  m->blob.assign((const unsigned char*)blob, (const unsigned char*)blob + nbytes);
+  if (!parse_blob(m->blob.data(), nbytes, m->arr)) {
+    fail(DX_EMODEL, "malformed model blob");
+    delete m;
+    return nullptr;
+  }
+  for (const char* n : kFloatArrays)
+    if (!load_f(m, n)) { fail(DX_EMODEL, std::string("blob missing float array ") + n); delete m; return nullptr; }
+  for (const char* n : kIntArrays)
+    if (!load_i(m, n)) { fail(DX_EMODEL, std::string("blob missing int array ") + n); delete m; return nullptr; }
+  DevModel& d = m->dm;
+  memset(&d, 0, sizeof(d));
+  d.nq = geti(m, "nq"); d.nv = geti(m, "nv"); d.nbody = geti(m, "nbody"); d.njnt = geti(m, "njnt");
+  d.ngeom = geti(m, "ngeom"); d.nsite = geti(m, "nsite"); d.nu = geti(m, "nu");
+  d.ntendon = geti(m, "ntendon"); d.nwrap = geti(m, "nwrap"); d.nbpair = geti(m, "nbpair");
+  d.ngpair = geti(m, "ngpair"); d.iterations = geti(m, "iterations");
+  d.disable_contact = geti(m, "disable_contact");
+  d.timestep = (float)getd(m, "timestep"); d.tolerance = (float)getd(m, "tolerance");
+  d.impratio = (float)getd(m, "impratio"); d.meaninertia = (float)getd(m, "meaninertia");
+  for (int k = 0; k < 3; k++) d.gravity[k] = m->hf["gravity"][k];
+  if (d.nv < 1 || d.nv > DX_MAX_NV || d.nbody < 1) {
+    fail(DX_ELIMIT, "nv must be in [1, 64]");
+    delete m;
+    return nullptr;
+  }
+  int nb = d.nbody, nv = d.nv;
+  auto& parent = m->hi["body_parent"];
+  auto& rootid = m->hi["body_rootid"];
+  // roots, levels
+  std::vector<int> rootidx(nb, 0), roots;
+  for (int b = 1; b < nb; b++) {
+    if (parent[b] == 0) { rootidx[b] = (int)roots.size(); roots.push_back(b); }
+  }
+  for (int b = 1; b < nb; b++) rootidx[b] = rootidx[rootid[b]];
+  std::vector<int> depth(nb, 0);
+  int maxd = 0;
+  for (int b = 1; b < nb; b++) { depth[b] = depth[parent[b]] + 1; maxd = std::max(maxd, depth[b]); }
+  std::vector<int> lvl_adr(maxd + 1, 0), lvl_body;
+  for (int lv = 1; lv <= maxd; lv++) {
+    lvl_adr[lv - 1] = (int)lvl_body.size();
+    for (int b = 1; b < nb; b++)
+      if (depth[b] == lv) lvl_body.push_back(b);
+  }
+  lvl_adr[maxd] = (int)lvl_body.size();
+  d.nlevel = maxd;
+  d.nroot = (int)roots.size();
+  m->hi["body_rootidx"] = rootidx;
+  m->hi["root_body"] = roots.empty() ? std::vector<int>{0} : roots;
+  m->hi["lvl_adr"] = lvl_adr;
+  m->hi["lvl_body"] = lvl_body.empty() ? std::vector<int>{0} : lvl_body;
+  // dof chain masks
+  m->body_chain.assign(nb, 0);
+  auto& dofadr = m->hi["body_dofadr"];
+  auto& dofnum = m->hi["body_dofnum"];
+  for (int b = 1; b < nb; b++) {
+    uint64_t c = m->body_chain[parent[b]];
+    for (int k = 0; k < dofnum[b]; k++) c |= 1ull << (dofadr[b] + k);
+    m->body_chain[b] = c;
+  }
+  // check contact jacobian support limit over all candidate body pairs
+  auto& bpair = m->hi["bpair_body"];
+  for (int k = 0; k < d.nbpair; k++) {
+    uint64_t s = m->body_chain[bpair[2 * k]] ^ m->body_chain[bpair[2 * k + 1]];
+    if (__builtin_popcountll(s) > DX_DOFMAX) {
+      fail(DX_ELIMIT, "contact jacobian support exceeds DX_DOFMAX");
+      delete m;
+      return nullptr;
+    }
+  }
+  // rotation matrices
+  auto mats = [&](const char* qname, const char* out, int n) {
+    std::vector<float> R(9 * std::max(n, 1), 0.f);
+    auto& q = m->hf[qname];
+    for (int i = 0; i < n; i++) quat2mat_h(R.data() + 9 * i, q.data() + 4 * i);
+    m->hf[out] = R;
+  };
+  mats("body_iquat", "body_imat", nb);
+  mats("geom_quat", "geom_mat", d.ngeom);
+  mats("site_quat", "site_mat", d.nsite);
+  // friction rows / limited joints / limited tendons
+  std::vector<int> fric_dof, dof_fricrow(nv, -1), limj, limt;
+  auto& floss = m->hf["dof_frictionloss"];
+  for (int i = 0; i < nv; i++)
+    if (floss[i] > 0) { dof_fricrow[i] = (int)fric_dof.size(); fric_dof.push_back(i); }
+  auto& jtype = m->hi["jnt_type"];
+  auto& jlim = m->hi["jnt_limited"];
+  for (int j = 0; j < d.njnt; j++)
+    if (jlim[j] && jtype[j] == DXJ_HINGE) limj.push_back(j);
+  auto& tlim = m->hi["tendon_limited"];
+  for (int t = 0; t < d.ntendon; t++)
+    if (tlim[t]) limt.push_back(t);
+  d.nfric = (int)fric_dof.size();
+  d.nlimj = (int)limj.size();
+  d.nlimt = (int)limt.size();
+  m->hi["fric_dof"] = fric_dof.empty() ? std::vector<int>{0} : fric_dof;
+  m->hi["dof_fricrow"] = dof_fricrow;
+  m->hi["limj_jnt"] = limj.empty() ? std::vector<int>{0} : limj;
+  m->hi["limt_ten"] = limt.empty() ? std::vector<int>{0} : limt;
+  // wraps: qpos address; dense tendon jacobian
+  auto& wdof = m->hi["wrap_dof"];
+  auto& dofj = m->hi["dof_jntid"];
+  auto& jqa = m->hi["jnt_qposadr"];
+  std::vector<int> wqadr(std::max(d.nwrap, 1), 0);
+  for (int w = 0; w < d.nwrap; w++) wqadr[w] = jqa[dofj[wdof[w]]];
+  m->hi["wrap_qadr"] = wqadr;
+  std::vector<float> tJ(std::max(d.ntendon, 1) * nv, 0.f);
+  auto& tadr = m->hi["tendon_adr"];
+  auto& tnum = m->hi["tendon_num"];
+  auto& wcoef = m->hf["wrap_coef"];
+  for (int t = 0; t < d.ntendon; t++)
+    for (int w = tadr[t]; w < tadr[t] + tnum[t]; w++) tJ[t * nv + wdof[w]] += wcoef[w];
+  m->hf["tendon_J"] = tJ;
+  auto& damp = m->hf["dof_damping"];
+  d.any_damping = 0;
+  for (int i = 0; i < nv; i++)
+    if (damp[i] > 0) d.any_damping = 1;
+  // LDS layout
+  Lds& L = m->lds;
+  int off = 0;
+  auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+  L.qpos = take(d.nq); L.qvel = take(nv); L.ctrl = take(std::max(d.nu, 1)); L.qacc = take(nv);
+  L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv); L.qfrc_con = take(nv);
+  L.v1 = take(nv); L.v2 = take(nv); L.v3 = take(nv); L.v4 = take(nv); L.v5 = take(nv);
+  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.xanchor = take(3 * std::max(d.njnt, 1)); L.xaxis = take(3 * std::max(d.njnt, 1));
+  L.rcom = take(3 * std::max(d.nroot, 1)); L.cinert = take(10 * nb); L.cdof = take(6 * nv);
+  L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.scr = take(12 * nb);
+  L.M = take(nv * nv);
+  L.cand_max = std::max(nv * nv, 512);
+  L.H = take(L.cand_max);
+  L.ten_len = take(std::max(d.ntendon, 1)); L.act_len = take(std::max(d.nu, 1));
+  L.act_force = take(std::max(d.nu, 1));
+  L.con = take(DX_NCON_MAX * DX_CON_STRIDE);
+  L.cj_idx = take(DX_NCON_MAX * DX_DOFMAX);
+  L.cj_val = take(DX_NCON_MAX * 3 * DX_DOFMAX);
+  L.cq = take(3 * DX_NCON_MAX);
+  L.cw = take(3 * DX_NCON_MAX);
+  L.nefc_max = d.nfric + 2 * d.nlimj + 2 * d.nlimt + 4 * DX_NCON_MAX;
+  L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
+  L.efc_fl = take(L.nefc_max); L.efc_Rf = take(L.nefc_max); L.efc_jar = take(L.nefc_max);
+  L.efc_jv = take(L.nefc_max);
+  L.ints = take(16);
+  L.total = off;
+  m->ncon_max = DX_NCON_MAX;
+  m->nefc_max = L.nefc_max;
+  if (L.total * 4 > 160 * 1024) {
+    fail(DX_ELIMIT, "per-env LDS footprint exceeds 160 KiB");
+    delete m;
+    return nullptr;
+  }
+  return m;
+}
+
+extern "C" void dx_model_free(dx_model* m) {
+  if (!m) return;
+  for (auto& kv : m->dev_allocs) {
+    int cur;
+    hipGetDevice(&cur);
+    hipSetDevice(kv.first);
+    for (void* p : kv.second) hipFree(p);
+    hipSetDevice(cur);
+  }
+  delete m;
+}
+
+extern "C" int dx_model_sizes(const dx_model* m, int32_t out[12]) {
+  if (!m || !out) return fail(DX_EINVAL, "null argument");
+  const DevModel& d = m->dm;
+  int v[12] = {d.nq, d.nv, d.nbody, d.njnt, d.ngeom, d.nsite, d.nu, d.ntendon, d.nbpair, d.ngpair,
+               m->ncon_max, m->nefc_max};
+  memcpy(out, v, sizeof(v));
+  return 0;
+}
+
+extern "C" int dx_field_width(const dx_model* m, int field) {
+  if (!m) return fail(DX_EINVAL, "null model");
+  const DevModel& d = m->dm;
+  switch (field) {
+    case DX_QPOS: return d.nq;
+    case DX_QVEL: case DX_QACC_WARMSTART: case DX_QACC: return d.nv;
+    case DX_CTRL: return d.nu;
+    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: return 1;
+    case DX_SITE_XPOS: return 3 * d.nsite;
+    case DX_SITE_VEL: return 6 * d.nsite;
+    case DX_XPOS: return 3 * d.nbody;
+    case DX_XQUAT: return 4 * d.nbody;
+  }
+  return fail(DX_EINVAL, "unknown field");
+}
+
+// Upload the model to `device` once; returns the DevModel with device pointers.
+static int device_model(dx_model* m, int device, DevModel* out) {
+  auto it = m->dev_models.find(device);
+  if (it != m->dev_models.end()) { *out = it->second; return 0; }
+  DevModel d = m->dm;
+  std::vector<void*>& allocs = m->dev_allocs[device];
+  auto upf = [&](const char* name, const float** dst) -> int {
+    auto& v = m->hf[name];
+    size_t n = std::max<size_t>(v.size(), 1);
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, n * 4));
+    allocs.push_back(p);
+    if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    *dst = (const float*)p;
+    return 0;
+  };
+  auto upi = [&](const char* name, const int** dst) -> int {
+    auto& v = m->hi[name];
+    size_t n = std::max<size_t>(v.size(), 1);
+    void* p = nullptr;
+    HIPCHK(hipMalloc(&p, n * 4));
+    allocs.push_back(p);
+    if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
+    *dst = (const int*)p;
+    return 0;
+  };
+#define UF(field) if (int rc = upf(#field, &d.field)) return rc
+#define UI(field) if (int rc = upi(#field, &d.field)) return rc
+  UI(body_parent); UI(body_rootidx); UI(body_jntnum); UI(body_jntadr); UI(body_dofnum); UI(body_dofadr);
+  UI(lvl_adr); UI(lvl_body); UI(root_body);
+  UF(body_pos); UF(body_quat); UF(body_ipos); UF(body_imat); UF(body_mass); UF(body_inertia);
+  UF(body_bsphere); UF(body_invweight0);
+  UI(jnt_type); UI(jnt_bodyid); UI(jnt_qposadr); UI(jnt_dofadr);
+  UF(jnt_pos); UF(jnt_axis); UF(jnt_range); UF(jnt_margin); UF(jnt_solref); UF(jnt_solimp); UF(qpos0);
+  UI(limj_jnt); UI(dof_bodyid); UI(dof_parentid); UI(dof_jntid); UI(fric_dof); UI(dof_fricrow);
+  UF(dof_armature); UF(dof_damping); UF(dof_frictionloss); UF(dof_solref); UF(dof_solimp); UF(dof_invweight0);
+  UI(geom_type); UI(geom_bodyid); UI(geom_dataid);
+  UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere);
+  UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert);
+  UI(site_bodyid); UF(site_pos); UF(site_mat);
+  UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
+  UF(tendon_range); UF(tendon_margin); UF(tendon_solref); UF(tendon_solimp); UF(tendon_invweight0);
+  UF(wrap_coef); UF(tendon_J);
+  UI(actuator_trntype); UI(actuator_trnid); UI(actuator_biastype); UI(actuator_ctrllimited);
+  UI(actuator_forcelimited);
+  UF(actuator_gear); UF(actuator_gainprm); UF(actuator_biasprm); UF(actuator_ctrlrange); UF(actuator_forcerange);
+  UI(bpair_body); UI(bpair_adr); UI(bpair_num); UI(gpair_geom); UI(gpair_condim);
+  UF(gpair_friction); UF(gpair_solref); UF(gpair_solimp); UF(gpair_margin);
+#undef UF
+#undef UI
+  void* p = nullptr;
+  HIPCHK(hipMalloc(&p, m->body_chain.size() * 8));
+  allocs.push_back(p);
+  HIPCHK(hipMemcpy(p, m->body_chain.data(), m->body_chain.size() * 8, hipMemcpyHostToDevice));
+  d.body_chain = (const uint64_t*)p;
+  m->dev_models[device] = d;
+  *out = d;
+  return 0;
+}
+
+// ------------------------------------------------------------------------ //
+// batch
+// ------------------------------------------------------------------------ //
+struct dx_batch {
+  dx_model* model;
+  int device, nenv;
+  hipStream_t stream;
+  DevModel dm;
+  DevBatch db;
+  float* xfrc;
+  std::vector<void*> allocs;
+  bool debug;
+};
+
+static int balloc(dx_batch* b, void** p, size_t bytes) {
+  HIPCHK(hipMalloc(p, std::max<size_t>(bytes, 4)));
+  HIPCHK(hipMemsetAsync(*p, 0, std::max<size_t>(bytes, 4), b->stream));
+  b->allocs.push_back(*p);
+  return 0;
+}
+
+extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t device) {
+  dx_model* m = const_cast<dx_model*>(mc);
+  if (!m || nenv < 1) { fail(DX_EINVAL, "bad model or nenv"); return nullptr; }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    fail(DX_EHIP, "invalid HIP device (is a GPU visible?)");
+    return nullptr;
+  }
+  if (hipSetDevice(device) != hipSuccess) { fail(DX_EHIP, "hipSetDevice failed"); return nullptr; }
+  dx_batch* b = new dx_batch();
+  b->model = m;
+  b->device = device;
+  b->nenv = nenv;
+  b->debug = false;
+  b->xfrc = nullptr;
+  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    fail(DX_EHIP, "hipStreamCreate failed");
+    delete b;
+    return nullptr;
+  }
+  if (device_model(m, device, &b->dm) != 0) { delete b; return nullptr; }
+  const DevModel& d = b->dm;
+  DevBatch& B = b->db;
+  memset(&B, 0, sizeof(B));
+  B.nenv = nenv;
+  size_t E = nenv;
+  int rc = 0;
+  rc |= balloc(b, (void**)&B.qpos, E * d.nq * 4);
+  rc |= balloc(b, (void**)&B.qvel, E * d.nv * 4);
+  rc |= balloc(b, (void**)&B.ctrl, E * std::max(d.nu, 1) * 4);
+  rc |= balloc(b, (void**)&B.qacc_ws, E * d.nv * 4);
+  rc |= balloc(b, (void**)&B.qacc, E * d.nv * 4);
+  rc |= balloc(b, (void**)&B.time, E * 4);
+  rc |= balloc(b, (void**)&B.site_xpos, E * 3 * std::max(d.nsite, 1) * 4);
+  rc |= balloc(b, (void**)&B.site_vel, E * 6 * std::max(d.nsite, 1) * 4);
+  rc |= balloc(b, (void**)&B.xpos, E * 3 * d.nbody * 4);
+  rc |= balloc(b, (void**)&B.xquat, E * 4 * d.nbody * 4);
+  rc |= balloc(b, (void**)&B.ncon, E * 4);
+  rc |= balloc(b, (void**)&B.watch, E * 4);
+  rc |= balloc(b, (void**)&B.niter, E * 4);
+  rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
+  if (rc) { dx_batch_destroy(b); return nullptr; }
+  B.xfrc = nullptr;  // enabled by dx_set_xfrc
+  B.watch_geom = -1;
+  B.watch_body = -1;
+  if (dx_reset(b, 0, nenv) != 0) { dx_batch_destroy(b); return nullptr; }
+  return b;
+}
+
+extern "C" void dx_batch_destroy(dx_batch* b) {
+  if (!b) return;
+  hipSetDevice(b->device);
+  hipStreamSynchronize(b->stream);
+  for (void* p : b->allocs) hipFree(p);
+  hipStreamDestroy(b->stream);
+  delete b;
+}
+
+extern "C" int dx_batch_nenv(const dx_batch* b) { return b ? b->nenv : fail(DX_EINVAL, "null batch"); }
+
+extern "C" int dx_reset(dx_batch* b, int32_t env0, int32_t n) {
+  if (!b || env0 < 0 || n < 0 || env0 + n > b->nenv) return fail(DX_EINVAL, "bad env range");
+  if (n == 0) return 0;
+  HIPCHK(hipSetDevice(b->device));
+  hipLaunchKernelGGL(dx_reset_kernel, dim3(n), dim3(64), 0, b->stream, b->dm, b->db, env0, n);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+static void* field_base(dx_batch* b, int field) {
+  DevBatch& B = b->db;
+  switch (field) {
+    case DX_QPOS: return B.qpos;
+    case DX_QVEL: return B.qvel;
+    case DX_CTRL: return B.ctrl;
+    case DX_QACC_WARMSTART: return B.qacc_ws;
+    case DX_QACC: return B.qacc;
+    case DX_TIME: return B.time;
+    case DX_SITE_XPOS: return B.site_xpos;
+    case DX_SITE_VEL: return B.site_vel;
+    case DX_XPOS: return B.xpos;
+    case DX_XQUAT: return B.xquat;
+    case DX_NCON: return B.ncon;
+    case DX_GROUND_CONTACT: return B.watch;
+    case DX_NITER: return B.niter;
+  }
+  return nullptr;
+}
+
+extern "C" int dx_field_ptr(dx_batch* b, int field, void** devptr) {
+  if (!b || !devptr) return fail(DX_EINVAL, "null argument");
+  void* p = field_base(b, field);
+  if (!p) return fail(DX_EINVAL, "unknown field");
+  *devptr = p;
+  return 0;
+}
+
+extern "C" int dx_set_field(dx_batch* b, int field, const void* src, int32_t env0, int32_t n) {
+  if (!b || !src) return fail(DX_EINVAL, "null argument");
+  if (env0 < 0 || n < 0 || env0 + n > b->nenv) return fail(DX_EINVAL, "bad env range");
+  if (field != DX_QPOS && field != DX_QVEL && field != DX_CTRL && field != DX_QACC_WARMSTART && field != DX_TIME)
+    return fail(DX_EINVAL, "field is read-only");
+  int w = dx_field_width(b->model, field);
+  if (w <= 0) return 0;
+  char* base = (char*)field_base(b, field);
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemcpyAsync(base + (size_t)env0 * w * 4, src, (size_t)n * w * 4, hipMemcpyDefault, b->stream));
+  return 0;
+}
+
+extern "C" int dx_get_field(dx_batch* b, int field, void* dst, int32_t env0, int32_t n) {
+  if (!b || !dst) return fail(DX_EINVAL, "null argument");
+  if (env0 < 0 || n < 0 || env0 + n > b->nenv) return fail(DX_EINVAL, "bad env range");
+  char* base = (char*)field_base(b, field);
+  if (!base) return fail(DX_EINVAL, "unknown field");
+  int w = dx_field_width(b->model, field);
+  if (w <= 0) return 0;
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemcpyAsync(dst, base + (size_t)env0 * w * 4, (size_t)n * w * 4, hipMemcpyDefault, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+extern "C" int dx_set_xfrc(dx_batch* b, const float* xfrc, int32_t nbody) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (!xfrc) { b->db.xfrc = nullptr; return 0; }
+  if (nbody != b->dm.nbody) return fail(DX_EINVAL, "xfrc must be [nbody][6]");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemcpyAsync(b->xfrc, xfrc, (size_t)nbody * 6 * 4, hipMemcpyDefault, b->stream));
+  b->db.xfrc = b->xfrc;
+  return 0;
+}
+
+extern "C" int dx_set_ground_geom(dx_batch* b, int32_t geom) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (geom >= b->dm.ngeom) return fail(DX_EINVAL, "geom out of range");
+  b->db.watch_geom = geom;
+  return 0;
+}
+
+extern "C" int dx_set_watch(dx_batch* b, int32_t geom, int32_t body) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (geom >= b->dm.ngeom || body >= b->dm.nbody) return fail(DX_EINVAL, "watch out of range");
+  b->db.watch_geom = geom;
+  b->db.watch_body = body;
+  return 0;
+}
+
+static int launch_step(dx_batch* b, int nsub, int mode) {
+  HIPCHK(hipSetDevice(b->device));
+  size_t lds = (size_t)b->model->lds.total * 4;
+  hipLaunchKernelGGL(dx_step_kernel, dim3(b->nenv), dim3(64), lds, b->stream, b->dm, b->db,
+                     b->model->lds, nsub, mode);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int dx_step(dx_batch* b, int32_t nsubstep) {
+  if (!b || nsubstep < 1) return fail(DX_EINVAL, "bad batch or nsubstep");
+  return launch_step(b, nsubstep, 0);
+}
+
+extern "C" int dx_forward(dx_batch* b) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  return launch_step(b, 1, 1);
+}
+
+extern "C" void* dx_stream(dx_batch* b) { return b ? (void*)b->stream : nullptr; }
+
+extern "C" int dx_sync(dx_batch* b) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+extern "C" int dx_debug_enable(dx_batch* b, int enable) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  DevBatch& B = b->db;
+  if (enable && !b->debug) {
+    size_t E = b->nenv;
+    int nv = b->dm.nv;
+    int rc = 0;
+    rc |= balloc(b, (void**)&B.dbg_qacc_smooth, E * nv * 4);
+    rc |= balloc(b, (void**)&B.dbg_qfrc_smooth, E * nv * 4);
+    rc |= balloc(b, (void**)&B.dbg_M, E * nv * nv * 4);
+    rc |= balloc(b, (void**)&B.dbg_con, E * DX_NCON_MAX * 16 * 4);
+    rc |= balloc(b, (void**)&B.dbg_nefc, E * 2 * 4);
+    if (rc) return rc;
+    b->debug = true;
+  } else if (!enable) {
+    B.dbg_qacc_smooth = nullptr;  // buffers stay allocated until destroy
+    B.dbg_qfrc_smooth = nullptr;
+    B.dbg_M = nullptr;
+    B.dbg_con = nullptr;
+    B.dbg_nefc = nullptr;
+    b->debug = false;
+  }
+  return 0;
+}
+
+extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats) {
+  if (!b || !name || !dst) return fail(DX_EINVAL, "null argument");
+  if (!b->debug) return fail(DX_EINVAL, "debug not enabled");
+  DevBatch& B = b->db;
+  size_t E = b->nenv, nv = b->dm.nv;
+  const void* src = nullptr;
+  size_t n = 0;
+  std::string s(name);
+  if (s == "qacc_smooth") { src = B.dbg_qacc_smooth; n = E * nv; }
+  else if (s == "qfrc_smooth") { src = B.dbg_qfrc_smooth; n = E * nv; }
+  else if (s == "M") { src = B.dbg_M; n = E * nv * nv; }
+  else if (s == "contact") { src = B.dbg_con; n = E * DX_NCON_MAX * 16; }
+  else if (s == "efc_count") { src = B.dbg_nefc; n = E * 2; }
+  else return fail(DX_EINVAL, "unknown debug field");
+  if (nfloats < n) return fail(DX_EINVAL, "destination too small");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemcpyAsync(dst, src, n * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}

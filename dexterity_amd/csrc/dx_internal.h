@@ -1,0 +1,82 @@
+// dx_internal.h -- device-side model / batch / LDS layout of libdx.so (gfx950).
+//
+// One 64-lane wavefront (= one 64-thread workgroup) advances one environment.
+// Everything per-env lives in LDS for the whole launch; the model (shared by all
+// environments, ~150-300 KB) is read from global memory and stays L2-resident.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DX_WAVE 64
+#define DX_NCON_MAX 32    // contacts kept per env per substep (MuJoCo pool: nconmax)
+#define DX_DOFMAX 16      // max dofs in a contact Jacobian (|chain(b1) xor chain(b2)|)
+#define DX_CON_STRIDE 16  // floats per contact record in LDS
+#define DX_MAX_NV 64      // dof bitmasks are uint64
+
+enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };
+enum { DXJ_FREE = 0, DXJ_HINGE = 3 };
+enum { DXR_FRIC = 0, DXR_LIMJ = 1, DXR_LIMT = 2, DXR_CON = 3, DXR_CONFL = 4 };
+
+struct DevModel {
+  int nq, nv, nbody, njnt, ngeom, nsite, nu, ntendon, nwrap, nbpair, ngpair;
+  int iterations, disable_contact, any_damping, nlevel, nroot, nfric, nlimj, nlimt;
+  float timestep, tolerance, impratio, meaninertia;
+  float gravity[3];
+  // bodies
+  const int *body_parent, *body_rootidx, *body_jntnum, *body_jntadr, *body_dofnum, *body_dofadr;
+  const int *lvl_adr, *lvl_body, *root_body;
+  const uint64_t* body_chain;  // dofs on the path body -> root
+  const float *body_pos, *body_quat, *body_ipos, *body_imat, *body_mass, *body_inertia;
+  const float *body_bsphere, *body_invweight0;
+  // joints / dofs
+  const int *jnt_type, *jnt_bodyid, *jnt_qposadr, *jnt_dofadr;
+  const float *jnt_pos, *jnt_axis, *jnt_range, *jnt_margin, *jnt_solref, *jnt_solimp, *qpos0;
+  const int *limj_jnt;  // limited hinge joints
+  const int *dof_bodyid, *dof_parentid, *dof_jntid, *fric_dof, *dof_fricrow;
+  const float *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref, *dof_solimp,
+      *dof_invweight0;
+  // geoms / meshes
+  const int *geom_type, *geom_bodyid, *geom_dataid;
+  const float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere;
+  const int *mesh_vertadr, *mesh_vertnum;
+  const float* mesh_vert;
+  // sites
+  const int* site_bodyid;
+  const float *site_pos, *site_mat;
+  // tendons (fixed) and actuators
+  const int *tendon_adr, *tendon_num, *wrap_dof, *wrap_qadr, *limt_ten;
+  const float *tendon_range, *tendon_margin, *tendon_solref, *tendon_solimp, *tendon_invweight0,
+      *wrap_coef, *tendon_J;
+  const int *actuator_trntype, *actuator_trnid, *actuator_biastype, *actuator_ctrllimited,
+      *actuator_forcelimited;
+  const float *actuator_gear, *actuator_gainprm, *actuator_biasprm, *actuator_ctrlrange,
+      *actuator_forcerange;
+  // collision pairs
+  const int *bpair_body, *bpair_adr, *bpair_num, *gpair_geom, *gpair_condim;
+  const float *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
+};
+
+struct DevBatch {
+  int nenv;
+  float *qpos, *qvel, *ctrl, *qacc_ws, *qacc, *time;
+  float *site_xpos, *site_vel, *xpos, *xquat;
+  int *ncon, *watch, *niter;
+  const float* xfrc;  // [nbody*6], shared by all envs (may be null)
+  int watch_geom, watch_body;
+  // debug (null when disabled)
+  float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
+  int* dbg_nefc;
+};
+
+// Offsets (in 4-byte words) of every per-env LDS array.
+struct Lds {
+  int qpos, qvel, ctrl, qacc, qacc_smooth, qfrc_smooth, qfrc_con;
+  int v1, v2, v3, v4, v5;  // nv-sized scratch vectors (Ma, grad, dir, Mdir, tmp)
+  int xpos, xquat, xmat, xipos, xanchor, xaxis, rcom, cinert, cdof, cvel, cdof_dot, scr;
+  int M, H, ten_len, act_len, act_force;
+  int con, cj_idx, cj_val, cq, cw;
+  int efc_meta, efc_D, efc_aref, efc_fl, efc_Rf, efc_jar, efc_jv;
+  int ints;  // misc int scalars
+  int nefc_max, cand_max;
+  int total;
+};

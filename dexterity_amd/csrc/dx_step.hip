@@ -1,0 +1,1800 @@
+// dx_step.hip -- the batched physics step for CDNA4 (gfx950).
+//
+// One 64-thread workgroup (= one wavefront) per environment; the full substep
+// pipeline of MuJoCo's mj_step (Euler) runs fused in one launch with all per-env
+// state in LDS:
+//
+//   kinematics (level-parallel over the body tree) -> com / cinert / cdof
+//   -> tendon + transmission lengths -> CRB mass matrix
+//   -> collision: body-sphere cull (lanes over body pairs) -> geom-sphere cull
+//      -> narrowphase one pair per lane (MPR / plane-box / plane-convex / capsules)
+//   -> constraint rows (dof friction, joint/tendon limits, pyramidal contacts)
+//   -> comVel, RNE + applied wrench, passive, actuation, M^-1 via wave Cholesky
+//   -> Newton solver on the primal problem (wave-parallel Hessian, Cholesky,
+//      exact line search)
+//   -> implicit-damping Euler.
+//
+// The restated MuJoCo semantics, and where the reference configures each stage,
+// are listed in oracle/dx_oracle.c (the fp64 CPU oracle these kernels are
+// parity-tested against) and DESIGN.md §3.
+#include "dx_internal.h"
+
+#include <math.h>
+
+#define LANE ((int)threadIdx.x)
+#define SYNC() __syncthreads()
+
+// ------------------------------------------------------------------------ //
+// wave helpers
+// ------------------------------------------------------------------------ //
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// exclusive prefix sum over lanes
+__device__ __forceinline__ int wave_excl_scan(int v) {
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int y = __shfl_up(x, o, 64);
+    if (LANE >= o) x += y;
+  }
+  return x - v;
+}
+
+// ------------------------------------------------------------------------ //
+// small math
+// ------------------------------------------------------------------------ //
+__device__ __forceinline__ float dot3(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void sub3(float* r, const float* a, const float* b) {
+  r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2];
+}
+__device__ __forceinline__ float norm3(const float* a) { return sqrtf(dot3(a, a)); }
+__device__ __forceinline__ void normalize3(float* a) {
+  float n = norm3(a);
+  if (n > 1e-20f) { float s = 1.0f / n; a[0] *= s; a[1] *= s; a[2] *= s; }
+}
+__device__ __forceinline__ void matvec3(float* r, const float* R, const float* v) {
+  float t0 = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  float t1 = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  float t2 = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mattvec3(float* r, const float* R, const float* v) {
+  float t0 = R[0] * v[0] + R[3] * v[1] + R[6] * v[2];
+  float t1 = R[1] * v[0] + R[4] * v[1] + R[7] * v[2];
+  float t2 = R[2] * v[0] + R[5] * v[1] + R[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void matmul3(float* r, const float* A, const float* B) {
+  float t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = t[i];
+}
+__device__ __forceinline__ void quat2mat(float* R, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void quatmul(float* r, const float* a, const float* b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void quatnorm(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < 1e-20f) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float s = 1.0f / n;
+  q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s;
+}
+// spatial algebra: [angular; linear] about the root-com frame origin
+__device__ __forceinline__ void mul_inert(float* r, const float* I, const float* v) {
+  const float* w = v;
+  const float* l = v + 3;
+  const float* mc = I + 6;
+  float m = I[9];
+  r[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2] + (mc[1] * l[2] - mc[2] * l[1]);
+  r[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2] + (mc[2] * l[0] - mc[0] * l[2]);
+  r[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2] + (mc[0] * l[1] - mc[1] * l[0]);
+  r[3] = m * l[0] - (mc[1] * w[2] - mc[2] * w[1]);
+  r[4] = m * l[1] - (mc[2] * w[0] - mc[0] * w[2]);
+  r[5] = m * l[2] - (mc[0] * w[1] - mc[1] * w[0]);
+}
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* m) {
+  float a[3], b[3], c[3];
+  cross3(a, v, m);
+  cross3(b, v, m + 3);
+  cross3(c, v + 3, m);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// ------------------------------------------------------------------------ //
+// per-env context
+// ------------------------------------------------------------------------ //
+struct Ctx {
+  const DevModel& m;
+  const Lds& L;
+  float* S;
+  int* I;  // misc ints
+  __device__ float* f(int off) const { return S + off; }
+};
+// misc int slots
+enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
+
+// ------------------------------------------------------------------------ //
+// position stage
+// ------------------------------------------------------------------------ //
+__device__ void kinematics(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* qpos = c.f(c.L.qpos);
+  float* xpos = c.f(c.L.xpos);
+  float* xquat = c.f(c.L.xquat);
+  float* xmat = c.f(c.L.xmat);
+  float* xipos = c.f(c.L.xipos);
+  float* xanchor = c.f(c.L.xanchor);
+  float* xaxis = c.f(c.L.xaxis);
+  if (LANE == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0;
+    xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+    for (int k = 0; k < 9; k++) xmat[k] = (k % 4 == 0) ? 1.f : 0.f;
+    xipos[0] = xipos[1] = xipos[2] = 0;
+  }
+  SYNC();
+  for (int lv = 0; lv < m.nlevel; lv++) {
+    int a0 = m.lvl_adr[lv], a1 = m.lvl_adr[lv + 1];
+    for (int k = a0 + LANE; k < a1; k += DX_WAVE) {
+      int b = m.lvl_body[k];
+      int p = m.body_parent[b], ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+      float xp[3], xq[4];
+      if (jn > 0 && m.jnt_type[ja] == DXJ_FREE) {
+        const float* q = qpos + m.jnt_qposadr[ja];
+        xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
+        xq[0] = q[3]; xq[1] = q[4]; xq[2] = q[5]; xq[3] = q[6];
+        quatnorm(xq);
+        xanchor[3 * ja] = xp[0]; xanchor[3 * ja + 1] = xp[1]; xanchor[3 * ja + 2] = xp[2];
+        xaxis[3 * ja] = 0; xaxis[3 * ja + 1] = 0; xaxis[3 * ja + 2] = 1;
+      } else {
+        float t[3];
+        matvec3(t, xmat + 9 * p, m.body_pos + 3 * b);
+        xp[0] = xpos[3 * p] + t[0]; xp[1] = xpos[3 * p + 1] + t[1]; xp[2] = xpos[3 * p + 2] + t[2];
+        quatmul(xq, xquat + 4 * p, m.body_quat + 4 * b);
+        for (int j = ja; j < ja + jn; j++) {
+          float R[9];
+          quat2mat(R, xq);
+          const float* jp = m.jnt_pos + 3 * j;
+          const float* ja3 = m.jnt_axis + 3 * j;
+          matvec3(t, R, jp);
+          float anc[3] = {t[0] + xp[0], t[1] + xp[1], t[2] + xp[2]};
+          float ax[3];
+          matvec3(ax, R, ja3);
+          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
+          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
+          float ang = qpos[m.jnt_qposadr[j]] - m.qpos0[m.jnt_qposadr[j]];
+          float s, co;
+          sincosf(0.5f * ang, &s, &co);
+          float ql[4] = {co, ja3[0] * s, ja3[1] * s, ja3[2] * s};
+          quatmul(xq, xq, ql);
+          quatnorm(xq);
+          quat2mat(R, xq);
+          matvec3(t, R, jp);
+          xp[0] = anc[0] - t[0]; xp[1] = anc[1] - t[1]; xp[2] = anc[2] - t[2];
+        }
+      }
+      float R[9];
+      quat2mat(R, xq);
+      for (int e = 0; e < 3; e++) xpos[3 * b + e] = xp[e];
+      for (int e = 0; e < 4; e++) xquat[4 * b + e] = xq[e];
+      for (int e = 0; e < 9; e++) xmat[9 * b + e] = R[e];
+      float t[3];
+      matvec3(t, R, m.body_ipos + 3 * b);
+      for (int e = 0; e < 3; e++) xipos[3 * b + e] = xp[e] + t[e];
+    }
+    SYNC();
+  }
+}
+
+__device__ void com_pos(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* xipos = c.f(c.L.xipos);
+  float* xmat = c.f(c.L.xmat);
+  float* rcom = c.f(c.L.rcom);
+  // subtree com of every root (only roots are needed as com-frame origins)
+  for (int r = 0; r < m.nroot; r++) {
+    float s0 = 0, s1 = 0, s2 = 0, sm = 0;
+    for (int b = 1 + LANE; b < m.nbody; b += DX_WAVE) {
+      if (m.body_rootidx[b] != r) continue;
+      float ms = m.body_mass[b];
+      s0 += ms * xipos[3 * b]; s1 += ms * xipos[3 * b + 1]; s2 += ms * xipos[3 * b + 2]; sm += ms;
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); sm = wave_sum(sm);
+    if (LANE == 0) {
+      int rb = m.root_body[r];
+      if (sm > 1e-15f) { rcom[3 * r] = s0 / sm; rcom[3 * r + 1] = s1 / sm; rcom[3 * r + 2] = s2 / sm; }
+      else { rcom[3 * r] = xipos[3 * rb]; rcom[3 * r + 1] = xipos[3 * rb + 1]; rcom[3 * r + 2] = xipos[3 * rb + 2]; }
+    }
+  }
+  SYNC();
+  float* cinert = c.f(c.L.cinert);
+  for (int b = 1 + LANE; b < m.nbody; b += DX_WAVE) {
+    float Rb[9];
+    matmul3(Rb, xmat + 9 * b, m.body_imat + 9 * b);
+    const float* I = m.body_inertia + 3 * b;
+    float mass = m.body_mass[b];
+    const float* rc = rcom + 3 * m.body_rootidx[b];
+    float off[3] = {xipos[3 * b] - rc[0], xipos[3 * b + 1] - rc[1], xipos[3 * b + 2] - rc[2]};
+    float Iw[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        Iw[3 * i + j] = Rb[3 * i] * I[0] * Rb[3 * j] + Rb[3 * i + 1] * I[1] * Rb[3 * j + 1] +
+                        Rb[3 * i + 2] * I[2] * Rb[3 * j + 2];
+    float dd = dot3(off, off);
+    float* ci = cinert + 10 * b;
+    ci[0] = Iw[0] + mass * (dd - off[0] * off[0]);
+    ci[1] = Iw[4] + mass * (dd - off[1] * off[1]);
+    ci[2] = Iw[8] + mass * (dd - off[2] * off[2]);
+    ci[3] = Iw[1] - mass * off[0] * off[1];
+    ci[4] = Iw[2] - mass * off[0] * off[2];
+    ci[5] = Iw[5] - mass * off[1] * off[2];
+    ci[6] = mass * off[0]; ci[7] = mass * off[1]; ci[8] = mass * off[2];
+    ci[9] = mass;
+  }
+  float* cdof = c.f(c.L.cdof);
+  float* xanchor = c.f(c.L.xanchor);
+  float* xaxis = c.f(c.L.xaxis);
+  for (int d = LANE; d < m.nv; d += DX_WAVE) {
+    int j = m.dof_jntid[d], b = m.dof_bodyid[d];
+    const float* rc = rcom + 3 * m.body_rootidx[b];
+    float off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
+    float* cd = cdof + 6 * d;
+    if (m.jnt_type[j] == DXJ_FREE) {
+      int k = d - m.jnt_dofadr[j];
+      if (k < 3) {
+        for (int e = 0; e < 6; e++) cd[e] = 0;
+        cd[3 + k] = 1;
+      } else {
+        const float* R = xmat + 9 * b;
+        float ax[3] = {R[k - 3], R[3 + k - 3], R[6 + k - 3]};
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cross3(cd + 3, ax, off);
+      }
+    } else {
+      const float* ax = xaxis + 3 * j;
+      cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+      cross3(cd + 3, ax, off);
+    }
+  }
+  SYNC();
+}
+
+__device__ void tendon_lengths(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* qpos = c.f(c.L.qpos);
+  float* tl = c.f(c.L.ten_len);
+  for (int t = LANE; t < m.ntendon; t += DX_WAVE) {
+    float len = 0;
+    for (int w = m.tendon_adr[t]; w < m.tendon_adr[t] + m.tendon_num[t]; w++)
+      len += m.wrap_coef[w] * qpos[m.wrap_qadr[w]];
+    tl[t] = len;
+  }
+  SYNC();
+  float* al = c.f(c.L.act_len);
+  for (int i = LANE; i < m.nu; i += DX_WAVE) {
+    float g = m.actuator_gear[i];
+    al[i] = m.actuator_trntype[i] == 0 ? g * qpos[m.jnt_qposadr[m.actuator_trnid[i]]]
+                                       : g * tl[m.actuator_trnid[i]];
+  }
+}
+
+__device__ void crb_mass(const Ctx& c) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  float* crb = c.f(c.L.scr);
+  float* cinert = c.f(c.L.cinert);
+  float* M = c.f(c.L.M);
+  float* cdof = c.f(c.L.cdof);
+  for (int k = LANE; k < 10 * m.nbody; k += DX_WAVE) crb[k] = cinert[k];
+  for (int k = LANE; k < nv * nv; k += DX_WAVE) M[k] = 0;
+  SYNC();
+  for (int lv = m.nlevel - 1; lv > 0; lv--) {
+    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
+      int b = m.lvl_body[k], p = m.body_parent[b];
+      if (p > 0)
+        for (int e = 0; e < 10; e++) atomicAdd(crb + 10 * p + e, crb[10 * b + e]);
+    }
+    SYNC();
+  }
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    float f[6];
+    mul_inert(f, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
+    for (int j = i; j >= 0; j = m.dof_parentid[j]) {
+      float v = dot6(cdof + 6 * j, f);
+      M[i * nv + j] = v;
+      M[j * nv + i] = v;
+    }
+    M[i * nv + i] += m.dof_armature[i];
+  }
+  SYNC();
+}
+
+// In-place dense Cholesky (lower) of the nv x nv matrix A, wave-parallel.
+__device__ void wave_cholesky(float* A, int n) {
+  for (int k = 0; k < n; k++) {
+    float akk = A[k * n + k];
+    akk = sqrtf(fmaxf(akk, 1e-30f));
+    float inv = 1.0f / akk;
+    SYNC();
+    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) A[i * n + k] *= inv;
+    if (LANE == 0) A[k * n + k] = akk;
+    SYNC();
+    int w = n - k - 1;  // trailing lower triangle: rows i=k+1..n-1, cols j=k+1..i
+    int tot = w * (w + 1) / 2;
+    for (int t = LANE; t < tot; t += DX_WAVE) {
+      // map t -> (ii, jj) with 0<=jj<=ii<w
+      int ii = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+      while ((ii + 1) * (ii + 2) / 2 <= t) ii++;
+      while (ii * (ii + 1) / 2 > t) ii--;
+      int jj = t - ii * (ii + 1) / 2;
+      int i = k + 1 + ii, j = k + 1 + jj;
+      A[i * n + j] -= A[i * n + k] * A[j * n + k];
+    }
+    SYNC();
+  }
+}
+// Solve (L L^T) x = b in place on x (x holds b on entry). L lower, row-major.
+__device__ void wave_chol_solve(const float* A, float* x, int n) {
+  for (int k = 0; k < n; k++) {
+    SYNC();
+    float xk = x[k] / A[k * n + k];
+    SYNC();
+    if (LANE == 0) x[k] = xk;
+    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) x[i] -= A[i * n + k] * xk;
+  }
+  for (int k = n - 1; k >= 0; k--) {
+    SYNC();
+    float xk = x[k] / A[k * n + k];
+    SYNC();
+    if (LANE == 0) x[k] = xk;
+    for (int i = LANE; i < k; i += DX_WAVE) x[i] -= A[k * n + i] * xk;
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
+// collision
+// ------------------------------------------------------------------------ //
+struct Shape {
+  int type, nvert;
+  float pos[3], mat[9], size[3], center[3], margin;
+  const float* vert;
+};
+
+__device__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
+  const DevModel& m = c.m;
+  int b = m.geom_bodyid[g];
+  const float* xp = c.f(c.L.xpos) + 3 * b;
+  const float* xm = c.f(c.L.xmat) + 9 * b;
+  float t[3];
+  matvec3(t, xm, m.geom_pos + 3 * g);
+  pos[0] = xp[0] + t[0]; pos[1] = xp[1] + t[1]; pos[2] = xp[2] + t[2];
+  matmul3(mat, xm, m.geom_mat + 9 * g);
+}
+
+__device__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
+  const DevModel& m = c.m;
+  s.type = m.geom_type[g];
+  geom_pose(c, g, s.pos, s.mat);
+  s.size[0] = m.geom_size[3 * g]; s.size[1] = m.geom_size[3 * g + 1]; s.size[2] = m.geom_size[3 * g + 2];
+  s.vert = nullptr;
+  s.nvert = 0;
+  if (s.type == DXG_MESH) {
+    int mid = m.geom_dataid[g];
+    s.vert = m.mesh_vert + 3 * m.mesh_vertadr[mid];
+    s.nvert = m.mesh_vertnum[mid];
+  }
+  float t[3];
+  matvec3(t, s.mat, m.geom_center + 3 * g);
+  s.center[0] = s.pos[0] + t[0]; s.center[1] = s.pos[1] + t[1]; s.center[2] = s.pos[2] + t[2];
+  s.margin = half_margin;
+}
+
+__device__ void support(const Shape& s, const float* dir, float* out) {
+  float ld[3];
+  mattvec3(ld, s.mat, dir);
+  float lp[3] = {0, 0, 0};
+  if (s.type == DXG_BOX) {
+    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= 0 ? s.size[k] : -s.size[k];
+  } else if (s.type == DXG_MESH) {
+    float best = -3.0e38f;
+    int bi = 0;
+    for (int i = 0; i < s.nvert; i++) {
+      const float* v = s.vert + 3 * i;
+      float d = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
+      if (d > best) { best = d; bi = i; }
+    }
+    lp[0] = s.vert[3 * bi]; lp[1] = s.vert[3 * bi + 1]; lp[2] = s.vert[3 * bi + 2];
+  } else if (s.type == DXG_SPHERE || s.type == DXG_CAPSULE) {
+    float n = norm3(ld);
+    if (n > 1e-20f) { float sc = s.size[0] / n; lp[0] = ld[0] * sc; lp[1] = ld[1] * sc; lp[2] = ld[2] * sc; }
+    if (s.type == DXG_CAPSULE) lp[2] += ld[2] >= 0 ? s.size[1] : -s.size[1];
+  }
+  matvec3(out, s.mat, lp);
+  out[0] += s.pos[0]; out[1] += s.pos[1]; out[2] += s.pos[2];
+  if (s.margin > 0) {
+    float n = norm3(dir);
+    if (n > 1e-20f) {
+      float sc = s.margin / n;
+      out[0] += dir[0] * sc; out[1] += dir[1] * sc; out[2] += dir[2] * sc;
+    }
+  }
+}
+
+struct MPoint { float v[3], a[3], b[3]; };
+
+__device__ __forceinline__ void mpr_support(const Shape& A, const Shape& B, const float* dir, MPoint& p) {
+  float nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support(A, dir, p.a);
+  support(B, nd, p.b);
+  sub3(p.v, p.a, p.b);
+}
+__device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-10f; }
+__device__ void portal_dir(const MPoint* P, float* dir) {
+  float a[3], b[3];
+  sub3(a, P[2].v, P[1].v);
+  sub3(b, P[3].v, P[1].v);
+  cross3(dir, a, b);
+  normalize3(dir);
+}
+__device__ bool portal_reach_tol(const MPoint* P, const MPoint& v4, const float* dir, float tol) {
+  float dv4 = dot3(v4.v, dir);
+  float d1 = dv4 - dot3(P[1].v, dir), d2 = dv4 - dot3(P[2].v, dir), d3 = dv4 - dot3(P[3].v, dir);
+  return fminf(d1, fminf(d2, d3)) <= tol;
+}
+__device__ void expand_portal(MPoint* P, const MPoint& v4) {
+  float v4v0[3];
+  cross3(v4v0, v4.v, P[0].v);
+  if (dot3(P[1].v, v4v0) > 0) {
+    if (dot3(P[2].v, v4v0) > 0) P[1] = v4;
+    else P[3] = v4;
+  } else {
+    if (dot3(P[3].v, v4v0) > 0) P[2] = v4;
+    else P[1] = v4;
+  }
+}
+__device__ float tri_origin_dist2(const float* a, const float* b, const float* c, float* q) {
+  float ab[3], ac[3], ap[3];
+  sub3(ab, b, a); sub3(ac, c, a);
+  ap[0] = -a[0]; ap[1] = -a[1]; ap[2] = -a[2];
+  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= 0 && d2 <= 0) { q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; return dot3(q, q); }
+  float bp[3] = {-b[0], -b[1], -b[2]};
+  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= 0 && d4 <= d3) { q[0] = b[0]; q[1] = b[1]; q[2] = b[2]; return dot3(q, q); }
+  float vc = d1 * d4 - d3 * d2;
+  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    float v = d1 / (d1 - d3);
+    for (int k = 0; k < 3; k++) q[k] = a[k] + v * ab[k];
+    return dot3(q, q);
+  }
+  float cp[3] = {-c[0], -c[1], -c[2]};
+  float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
+  if (d6 >= 0 && d5 <= d6) { q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; return dot3(q, q); }
+  float vb = d5 * d2 - d1 * d6;
+  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    float w = d2 / (d2 - d6);
+    for (int k = 0; k < 3; k++) q[k] = a[k] + w * ac[k];
+    return dot3(q, q);
+  }
+  float va = d3 * d6 - d5 * d4;
+  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    for (int k = 0; k < 3; k++) q[k] = b[k] + w * (c[k] - b[k]);
+    return dot3(q, q);
+  }
+  float denom = 1.0f / (va + vb + vc);
+  float v = vb * denom, w = vc * denom;
+  for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
+  return dot3(q, q);
+}
+__device__ void find_pos(const MPoint* P, float* pos) {
+  float dir[3];
+  portal_dir(P, dir);
+  float b[4], t[3];
+  cross3(t, P[2].v, P[3].v); b[0] = dot3(P[1].v, t);
+  cross3(t, P[2].v, P[0].v); b[1] = dot3(P[3].v, t);
+  cross3(t, P[1].v, P[3].v); b[2] = dot3(P[0].v, t);
+  cross3(t, P[1].v, P[0].v); b[3] = dot3(P[2].v, t);
+  float sum = b[0] + b[1] + b[2] + b[3];
+  if (sum <= 0) {
+    b[0] = 0;
+    cross3(t, P[3].v, dir); b[1] = dot3(P[2].v, t);
+    cross3(t, P[1].v, dir); b[2] = dot3(P[3].v, t);
+    cross3(t, P[2].v, dir); b[3] = dot3(P[1].v, t);
+    sum = b[1] + b[2] + b[3];
+  }
+  float inv = 1.0f / sum;
+  float p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int i = 0; i < 4; i++)
+    for (int k = 0; k < 3; k++) { p1[k] += b[i] * P[i].a[k]; p2[k] += b[i] * P[i].b[k]; }
+  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+}
+
+// MPR penetration on A - B (libccd structure, see oracle mpr_penetration).
+__device__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+  const float tol = 1e-6f;
+  const int maxit = 50;
+  MPoint P[4];
+  sub3(P[0].v, A.center, B.center);
+  for (int k = 0; k < 3; k++) { P[0].a[k] = A.center[k]; P[0].b[k] = B.center[k]; }
+  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-9f;
+  float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+  normalize3(dir);
+  mpr_support(A, B, dir, P[1]);
+  float dt = dot3(P[1].v, dir);
+  if (fzero(dt) || dt < 0) return false;
+  cross3(dir, P[0].v, P[1].v);
+  if (fzero(dot3(dir, dir))) {
+    if (fzero(P[1].v[0]) && fzero(P[1].v[1]) && fzero(P[1].v[2])) {
+      depth = 0;
+      normal[0] = 0; normal[1] = 0; normal[2] = 1;
+    } else {
+      depth = norm3(P[1].v);
+      for (int k = 0; k < 3; k++) normal[k] = P[1].v[k];
+      normalize3(normal);
+    }
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P[1].a[k] + P[1].b[k]);
+    return true;
+  }
+  normalize3(dir);
+  mpr_support(A, B, dir, P[2]);
+  dt = dot3(P[2].v, dir);
+  if (fzero(dt) || dt < 0) return false;
+  float va[3], vb[3];
+  sub3(va, P[1].v, P[0].v);
+  sub3(vb, P[2].v, P[0].v);
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, P[0].v) > 0) {
+    MPoint t = P[1]; P[1] = P[2]; P[2] = t;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  for (int it = 0;; it++) {
+    if (it > 1000) return false;
+    mpr_support(A, B, dir, P[3]);
+    dt = dot3(P[3].v, dir);
+    if (fzero(dt) || dt < 0) return false;
+    bool cont = false;
+    cross3(va, P[1].v, P[3].v);
+    dt = dot3(va, P[0].v);
+    if (dt < 0 && !fzero(dt)) { P[2] = P[3]; cont = true; }
+    if (!cont) {
+      cross3(va, P[3].v, P[2].v);
+      dt = dot3(va, P[0].v);
+      if (dt < 0 && !fzero(dt)) { P[1] = P[3]; cont = true; }
+    }
+    if (!cont) break;
+    sub3(va, P[1].v, P[0].v);
+    sub3(vb, P[2].v, P[0].v);
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  for (int it = 0;; it++) {
+    portal_dir(P, dir);
+    if (dot3(dir, P[1].v) >= 0) break;
+    MPoint v4;
+    mpr_support(A, B, dir, v4);
+    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P, v4, dir, tol) || it > maxit) return false;
+    expand_portal(P, v4);
+  }
+  for (int it = 0;; it++) {
+    portal_dir(P, dir);
+    MPoint v4;
+    mpr_support(A, B, dir, v4);
+    if (portal_reach_tol(P, v4, dir, tol) || it > maxit) {
+      float cl[3];
+      float d2 = tri_origin_dist2(P[1].v, P[2].v, P[3].v, cl);
+      depth = sqrtf(d2);
+      if (depth > 1e-20f) {
+        float s = 1.0f / depth;
+        normal[0] = cl[0] * s; normal[1] = cl[1] * s; normal[2] = cl[2] * s;
+      } else {
+        normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
+      }
+      find_pos(P, pos);
+      return true;
+    }
+    expand_portal(P, v4);
+  }
+}
+
+struct LocalContacts {
+  int n;
+  float pos[4][3];
+  float nrm[3];
+  float dist[4];
+};
+
+// Runs the narrowphase of geom pair gp; returns up to 4 contacts (shared normal).
+__device__ void narrowphase(const Ctx& c, int gp, LocalContacts& lc) {
+  const DevModel& m = c.m;
+  lc.n = 0;
+  int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+  int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  float margin = m.gpair_margin[gp];
+  if (t1 == DXG_PLANE) {
+    float pp[3], pm[9];
+    geom_pose(c, g1, pp, pm);
+    float n[3] = {pm[2], pm[5], pm[8]};
+    lc.nrm[0] = n[0]; lc.nrm[1] = n[1]; lc.nrm[2] = n[2];
+    if (t2 == DXG_BOX) {
+      float bp[3], bm[9];
+      geom_pose(c, g2, bp, bm);
+      const float* sz = m.geom_size + 3 * g2;
+      float rel[3];
+      sub3(rel, bp, pp);
+      float cdist = dot3(rel, n);
+      float ext = 0;
+      for (int k = 0; k < 3; k++) ext += fabsf(bm[k] * n[0] + bm[3 + k] * n[1] + bm[6 + k] * n[2]) * sz[k];
+      if (cdist > margin + ext) return;
+      for (int i = 0; i < 8 && lc.n < 4; i++) {
+        float s0 = (i & 1) ? sz[0] : -sz[0], s1 = (i & 2) ? sz[1] : -sz[1], s2 = (i & 4) ? sz[2] : -sz[2];
+        float v[3];
+        for (int k = 0; k < 3; k++) v[k] = bp[k] + bm[3 * k] * s0 + bm[3 * k + 1] * s1 + bm[3 * k + 2] * s2;
+        float r[3];
+        sub3(r, v, pp);
+        float dist = dot3(r, n);
+        if (dist <= margin) {
+          for (int k = 0; k < 3; k++) lc.pos[lc.n][k] = v[k] - 0.5f * dist * n[k];
+          lc.dist[lc.n] = dist;
+          lc.n++;
+        }
+      }
+    } else {
+      Shape s;
+      make_shape(c, g2, 0, s);
+      float nd[3] = {-n[0], -n[1], -n[2]};
+      float sp[3];
+      support(s, nd, sp);
+      float r[3];
+      sub3(r, sp, pp);
+      float dist = dot3(r, n);
+      if (dist > margin) return;
+      for (int k = 0; k < 3; k++) lc.pos[0][k] = sp[k] - 0.5f * dist * n[k];
+      lc.dist[0] = dist;
+      lc.n = 1;
+    }
+    return;
+  }
+  if (t1 == DXG_CAPSULE && t2 == DXG_CAPSULE) {
+    float p1[3], m1[9], p2[3], m2[9];
+    geom_pose(c, g1, p1, m1);
+    geom_pose(c, g2, p2, m2);
+    float r1 = m.geom_size[3 * g1], h1 = m.geom_size[3 * g1 + 1];
+    float r2 = m.geom_size[3 * g2], h2 = m.geom_size[3 * g2 + 1];
+    float a1[3] = {m1[2] * h1, m1[5] * h1, m1[8] * h1}, a2[3] = {m2[2] * h2, m2[5] * h2, m2[8] * h2};
+    float dv[3];
+    sub3(dv, p1, p2);
+    float ma = dot3(a1, a1), mb = -dot3(a1, a2), mc = dot3(a2, a2);
+    float u = -dot3(a1, dv), v = dot3(a2, dv);
+    float det = ma * mc - mb * mb;
+    float s = 0, t = 0;
+    if (det > 1e-12f) { s = (u * mc - mb * v) / det; t = (ma * v - mb * u) / det; }
+    for (int it = 0; it < 3; it++) {
+      s = fminf(1.f, fmaxf(-1.f, s));
+      t = (v - mb * s) / fmaxf(mc, 1e-12f);
+      t = fminf(1.f, fmaxf(-1.f, t));
+      s = (u - mb * t) / fmaxf(ma, 1e-12f);
+      s = fminf(1.f, fmaxf(-1.f, s));
+    }
+    float q1[3], q2[3], diff[3];
+    for (int k = 0; k < 3; k++) { q1[k] = p1[k] + s * a1[k]; q2[k] = p2[k] + t * a2[k]; }
+    sub3(diff, q2, q1);
+    float len = norm3(diff);
+    float dist = len - r1 - r2;
+    if (dist > margin) return;
+    if (len > 1e-20f) { lc.nrm[0] = diff[0] / len; lc.nrm[1] = diff[1] / len; lc.nrm[2] = diff[2] / len; }
+    else { lc.nrm[0] = 1; lc.nrm[1] = 0; lc.nrm[2] = 0; }
+    for (int k = 0; k < 3; k++) lc.pos[0][k] = q1[k] + lc.nrm[k] * (r1 + 0.5f * dist);
+    lc.dist[0] = dist;
+    lc.n = 1;
+    return;
+  }
+  Shape A, B;
+  make_shape(c, g1, 0.5f * margin, A);
+  make_shape(c, g2, 0.5f * margin, B);
+  float depth, nrm[3], pos[3];
+  if (mpr_penetration(A, B, depth, nrm, pos)) {
+    lc.nrm[0] = nrm[0]; lc.nrm[1] = nrm[1]; lc.nrm[2] = nrm[2];
+    lc.pos[0][0] = pos[0]; lc.pos[0][1] = pos[1]; lc.pos[0][2] = pos[2];
+    lc.dist[0] = margin - depth;
+    lc.n = 1;
+  }
+}
+
+__device__ __forceinline__ bool sphere_overlap(const float* c1, float r1, const float* c2, float r2, float margin) {
+  float t[3];
+  sub3(t, c1, c2);
+  float rr = r1 + r2 + margin;
+  return dot3(t, t) <= rr * rr;
+}
+
+// broadphase + mid-phase + narrowphase; writes contact records into LDS.
+// watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
+__device__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
+  const DevModel& m = c.m;
+  int* I = c.I;
+  int* cand = (int*)c.f(c.L.H);  // H is free during collision
+  int cmax = c.L.cand_max;
+  if (LANE == 0) { I[I_NCON] = 0; I[I_NCAND] = 0; }
+  SYNC();
+  if (m.disable_contact) return;
+  float* xpos = c.f(c.L.xpos);
+  float* xmat = c.f(c.L.xmat);
+  // body-pair cull, compacted into cand[] (body-pair indices); then expand to geom pairs
+  int nbc = 0;
+  for (int base = 0; base < m.nbpair; base += DX_WAVE) {
+    int bp = base + LANE;
+    bool keep = false;
+    if (bp < m.nbpair) {
+      int b1 = m.bpair_body[2 * bp], b2 = m.bpair_body[2 * bp + 1];
+      keep = true;
+      if (watch_only) keep = (b2 == wb || b1 == wb) && (m.geom_bodyid[wg] == b1 || m.geom_bodyid[wg] == b2);
+      const float* s1 = m.body_bsphere + 4 * b1;
+      const float* s2 = m.body_bsphere + 4 * b2;
+      if (keep && s1[3] >= 0 && s2[3] >= 0) {
+        float c1[3], c2[3];
+        matvec3(c1, xmat + 9 * b1, s1);
+        matvec3(c2, xmat + 9 * b2, s2);
+        for (int k = 0; k < 3; k++) { c1[k] += xpos[3 * b1 + k]; c2[k] += xpos[3 * b2 + k]; }
+        float mg = m.gpair_margin[m.bpair_adr[bp]];
+        keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+      }
+    }
+    uint64_t mask = __ballot(keep);
+    int pos = __popcll(mask & ((1ull << LANE) - 1ull));
+    if (keep && nbc + pos < cmax) cand[nbc + pos] = bp;
+    nbc += __popcll(mask);
+  }
+  nbc = min(nbc, cmax);
+  SYNC();
+  // geom-pair mid-phase: serial over surviving body pairs, lanes over geom pairs.
+  // Store survivors after the body-pair list (cand[nbc..]).
+  int* gcand = cand + nbc;
+  int gmax = cmax - nbc;
+  int ng = 0;
+  for (int q = 0; q < nbc; q++) {
+    int bp = cand[q];
+    int a0 = m.bpair_adr[bp], n0 = m.bpair_num[bp];
+    for (int base = 0; base < n0; base += DX_WAVE) {
+      int gp = a0 + base + LANE;
+      bool keep = false;
+      if (base + LANE < n0) {
+        int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+        keep = !watch_only || g1 == wg || g2 == wg;
+        if (keep) {
+          float mg = m.gpair_margin[gp];
+          float p2[3], m2[9];
+          geom_pose(c, g2, p2, m2);
+          const float* s2 = m.geom_bsphere + 4 * g2;
+          float c2[3];
+          matvec3(c2, m2, s2);
+          for (int k = 0; k < 3; k++) c2[k] += p2[k];
+          if (m.geom_type[g1] == DXG_PLANE) {
+            float p1[3], m1[9];
+            geom_pose(c, g1, p1, m1);
+            float n[3] = {m1[2], m1[5], m1[8]}, r[3];
+            sub3(r, c2, p1);
+            keep = dot3(r, n) <= s2[3] + mg;
+          } else {
+            float p1[3], m1[9];
+            geom_pose(c, g1, p1, m1);
+            const float* s1 = m.geom_bsphere + 4 * g1;
+            float c1[3];
+            matvec3(c1, m1, s1);
+            for (int k = 0; k < 3; k++) c1[k] += p1[k];
+            keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+          }
+        }
+      }
+      uint64_t mask = __ballot(keep);
+      int pos = __popcll(mask & ((1ull << LANE) - 1ull));
+      if (keep && ng + pos < gmax) gcand[ng + pos] = gp;
+      ng += __popcll(mask);
+    }
+  }
+  if (ng > gmax) {
+    if (LANE == 0) I[I_OVF] |= 1;
+    ng = gmax;
+  }
+  SYNC();
+  // narrowphase: one geom pair per lane; deterministic lane-ordered append.
+  float* con = c.f(c.L.con);
+  int ncon = 0;
+  for (int base = 0; base < ng; base += DX_WAVE) {
+    LocalContacts lc;
+    lc.n = 0;
+    int gp = -1;
+    if (base + LANE < ng) {
+      gp = gcand[base + LANE];
+      narrowphase(c, gp, lc);
+    }
+    int off = wave_excl_scan(lc.n);
+    int tot = wave_sum_i(lc.n);
+    for (int k = 0; k < lc.n; k++) {
+      int slot = ncon + off + k;
+      if (slot >= DX_NCON_MAX) break;
+      float* r = con + DX_CON_STRIDE * slot;
+      r[0] = lc.pos[k][0]; r[1] = lc.pos[k][1]; r[2] = lc.pos[k][2];
+      // frame: normal, tangent ([3P] mju_makeFrame)
+      float nx = lc.nrm[0], ny = lc.nrm[1], nz = lc.nrm[2];
+      float y[3];
+      if (fabsf(ny) < 0.5f) { y[0] = 0; y[1] = 1; y[2] = 0; }
+      else { y[0] = 0; y[1] = 0; y[2] = 1; }
+      float t = nx * y[0] + ny * y[1] + nz * y[2];
+      y[0] -= t * nx; y[1] -= t * ny; y[2] -= t * nz;
+      normalize3(y);
+      float nn[3] = {nx, ny, nz}, z[3];
+      cross3(z, nn, y);
+      r[3] = nx; r[4] = ny; r[5] = nz;
+      r[6] = y[0]; r[7] = y[1]; r[8] = y[2];
+      r[9] = z[0]; r[10] = z[1]; r[11] = z[2];
+      r[12] = lc.dist[k];
+      r[13] = __int_as_float(gp);
+    }
+    ncon += tot;
+  }
+  if (ncon > DX_NCON_MAX) {
+    if (LANE == 0) I[I_OVF] |= 2;
+    ncon = DX_NCON_MAX;
+  }
+  if (LANE == 0) I[I_NCON] = ncon;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
+// constraints
+// ------------------------------------------------------------------------ //
+__device__ float impedance(const float* solimp, float violation) {
+  float d0 = fminf(0.9999f, fmaxf(0.0001f, solimp[0]));
+  float dmax = fminf(0.9999f, fmaxf(0.0001f, solimp[1]));
+  float width = solimp[2], mid = solimp[3], power = solimp[4];
+  if (width <= 1e-15f || d0 == dmax) return 0.5f * (d0 + dmax);
+  float x = fabsf(violation) / width;
+  if (x >= 1) return dmax;
+  float y;
+  if (power == 1) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1);
+  else y = 1 - powf(1 - x, power) / powf(1 - mid, power - 1);
+  return d0 + y * (dmax - d0);
+}
+
+// row parameters -> D, aref, Rf.  vel = J*qvel.
+__device__ void row_params(const Ctx& c, int r, float pos, float margin, float floss, float diag,
+                           const float* solref, const float* solimp, float vel, float rscale, bool fric) {
+  const DevModel& m = c.m;
+  float imp = impedance(solimp, pos - margin);
+  float tc = fmaxf(solref[0], 2 * m.timestep), dr = solref[1];
+  float dmax = fminf(0.9999f, fmaxf(0.0001f, solimp[1]));
+  float K = 1.0f / fmaxf(1e-15f, dmax * dmax * tc * tc * dr * dr);
+  float B = 2.0f / fmaxf(1e-15f, dmax * tc);
+  float R = fmaxf(1e-15f, (1 - imp) / imp * diag);
+  R = fmaxf(1e-15f, R * rscale);
+  c.f(c.L.efc_D)[r] = 1.0f / R;
+  c.f(c.L.efc_fl)[r] = floss;
+  c.f(c.L.efc_Rf)[r] = R * floss;
+  float viol = fric ? 0.f : pos - margin;
+  c.f(c.L.efc_aref)[r] = -B * vel - K * imp * viol;
+}
+
+// sparse contact jacobian (frame rows) -> cj_idx / cj_val; then all rows
+__device__ void make_constraint(const Ctx& c) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  int* I = c.I;
+  float* qpos = c.f(c.L.qpos);
+  float* qvel = c.f(c.L.qvel);
+  int* meta = (int*)c.f(c.L.efc_meta);
+  int nfric = m.nfric;
+  // 1. dof friction rows: fixed positions [0, nfric)
+  for (int k = LANE; k < nfric; k += DX_WAVE) {
+    int d = m.fric_dof[k];
+    meta[k] = DXR_FRIC | (d << 8);
+    row_params(c, k, 0, 0, m.dof_frictionloss[d], m.dof_invweight0[d], m.dof_solref + 2 * d,
+               m.dof_solimp + 5 * d, qvel[d], 1.0f, true);
+  }
+  // 2. joint limits (one side at most unless range < 2 margin): lane per limited joint
+  int nrow = nfric;
+  for (int base = 0; base < m.nlimj; base += DX_WAVE) {
+    int k = base + LANE;
+    int cnt = 0;
+    float dist[2];
+    int j = -1;
+    if (k < m.nlimj) {
+      j = m.limj_jnt[k];
+      float q = qpos[m.jnt_qposadr[j]];
+      dist[0] = q - m.jnt_range[2 * j];
+      dist[1] = m.jnt_range[2 * j + 1] - q;
+      cnt = (dist[0] < m.jnt_margin[j]) + (dist[1] < m.jnt_margin[j]);
+    }
+    int off = wave_excl_scan(cnt);
+    int tot = wave_sum_i(cnt);
+    if (cnt) {
+      int r = nrow + off;
+      int d = m.jnt_dofadr[j];
+      for (int side = 0; side < 2; side++) {
+        if (dist[side] >= m.jnt_margin[j]) continue;
+        if (r < c.L.nefc_max) {
+          meta[r] = DXR_LIMJ | (side << 4) | (j << 8);
+          float v = side == 0 ? qvel[d] : -qvel[d];
+          row_params(c, r, dist[side], m.jnt_margin[j], 0, m.dof_invweight0[d], m.jnt_solref + 2 * j,
+                     m.jnt_solimp + 5 * j, v, 1.0f, false);
+        }
+        r++;
+      }
+    }
+    nrow += tot;
+  }
+  // 3. tendon limits
+  float* tl = c.f(c.L.ten_len);
+  for (int base = 0; base < m.nlimt; base += DX_WAVE) {
+    int k = base + LANE;
+    int cnt = 0;
+    float dist[2];
+    int t = -1;
+    if (k < m.nlimt) {
+      t = m.limt_ten[k];
+      dist[0] = tl[t] - m.tendon_range[2 * t];
+      dist[1] = m.tendon_range[2 * t + 1] - tl[t];
+      cnt = (dist[0] < m.tendon_margin[t]) + (dist[1] < m.tendon_margin[t]);
+    }
+    int off = wave_excl_scan(cnt);
+    int tot = wave_sum_i(cnt);
+    if (cnt) {
+      int r = nrow + off;
+      float tv = 0;
+      for (int w = m.tendon_adr[t]; w < m.tendon_adr[t] + m.tendon_num[t]; w++)
+        tv += m.wrap_coef[w] * qvel[m.wrap_dof[w]];
+      for (int side = 0; side < 2; side++) {
+        if (dist[side] >= m.tendon_margin[t]) continue;
+        if (r < c.L.nefc_max) {
+          meta[r] = DXR_LIMT | (side << 4) | (t << 8);
+          row_params(c, r, dist[side], m.tendon_margin[t], 0, m.tendon_invweight0[t],
+                     m.tendon_solref + 2 * t, m.tendon_solimp + 5 * t, side == 0 ? tv : -tv, 1.0f, false);
+        }
+        r++;
+      }
+    }
+    nrow += tot;
+  }
+  SYNC();
+  // 4. contacts: sparse frame jacobian, then pyramid rows
+  int ncon = I[I_NCON];
+  float* con = c.f(c.L.con);
+  float* cdof = c.f(c.L.cdof);
+  float* rcom = c.f(c.L.rcom);
+  int* cj_idx = (int*)c.f(c.L.cj_idx);
+  float* cj_val = c.f(c.L.cj_val);
+  float* cq = c.f(c.L.cq);
+  for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
+    float* r = con + DX_CON_STRIDE * ci;
+    int gp = __float_as_int(r[13]);
+    int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+    uint64_t c1 = m.body_chain[b1], c2 = m.body_chain[b2];
+    uint64_t sup = c1 ^ c2;
+    int nnz = 0;
+    float vel[3] = {0, 0, 0};
+    while (sup && nnz < DX_DOFMAX) {
+      int d = __ffsll((long long)sup) - 1;
+      sup &= sup - 1;
+      float sgn = (c2 >> d) & 1ull ? 1.f : -1.f;
+      int bb = m.dof_bodyid[d];
+      const float* rc = rcom + 3 * m.body_rootidx[bb];
+      const float* cd = cdof + 6 * d;
+      float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
+      float t[3];
+      cross3(t, cd, off);
+      float jp[3] = {cd[3] + t[0], cd[4] + t[1], cd[5] + t[2]};
+      cj_idx[ci * DX_DOFMAX + nnz] = d;
+      for (int k = 0; k < 3; k++) {
+        float v = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
+        cj_val[(ci * 3 + k) * DX_DOFMAX + nnz] = v;
+        vel[k] += v * qvel[d];
+      }
+      nnz++;
+    }
+    if (sup) I[I_OVF] |= 4;
+    for (int q = nnz; q < DX_DOFMAX; q++) {
+      cj_idx[ci * DX_DOFMAX + q] = -1;
+      for (int k = 0; k < 3; k++) cj_val[(ci * 3 + k) * DX_DOFMAX + q] = 0;
+    }
+    for (int k = 0; k < 3; k++) cq[3 * ci + k] = vel[k];  // frame velocities (J qvel)
+    r[14] = __int_as_float(nnz);
+  }
+  SYNC();
+  for (int base = 0; base < ncon; base += DX_WAVE) {
+    int ci = base + LANE;
+    int nr = 0;
+    int gp = 0;
+    float* r = nullptr;
+    if (ci < ncon) {
+      r = con + DX_CON_STRIDE * ci;
+      gp = __float_as_int(r[13]);
+      nr = m.gpair_condim[gp] == 1 ? 1 : 4;
+    }
+    int off = wave_excl_scan(nr);
+    int tot = wave_sum_i(nr);
+    if (nr) {
+      int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+      int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+      float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      const float* fr = m.gpair_friction + 5 * gp;
+      const float* sr = m.gpair_solref + 2 * gp;
+      const float* si = m.gpair_solimp + 5 * gp;
+      float mg = m.gpair_margin[gp];
+      r[15] = __int_as_float(nrow + off);
+      if (nr == 1) {
+        int row = nrow + off;
+        if (row < c.L.nefc_max) {
+          meta[row] = DXR_CONFL | (ci << 8);
+          row_params(c, row, r[12], mg, 0, tran, sr, si, cq[3 * ci], 1.0f, false);
+        }
+      } else {
+        float rs = 2 * fr[0] * fr[0] / m.impratio;
+        for (int e = 0; e < 4; e++) {
+          int row = nrow + off + e;
+          if (row >= c.L.nefc_max) break;
+          int k = 1 + (e >> 1);
+          float mu = fr[k - 1] * ((e & 1) ? -1.f : 1.f);
+          meta[row] = DXR_CON | (e << 4) | (ci << 8);
+          row_params(c, row, r[12], mg, 0, tran, sr, si, cq[3 * ci] + mu * cq[3 * ci + k], rs, false);
+        }
+      }
+    }
+    nrow += tot;
+  }
+  if (nrow > c.L.nefc_max) {
+    if (LANE == 0) I[I_OVF] |= 8;
+    nrow = c.L.nefc_max;
+  }
+  if (LANE == 0) I[I_NEFC] = nrow;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
+// velocity stage: comVel, RNE (+ applied wrench), passive, actuation
+// ------------------------------------------------------------------------ //
+__device__ void velocity_stage(const Ctx& c, const float* xfrc) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  float* qvel = c.f(c.L.qvel);
+  float* cdof = c.f(c.L.cdof);
+  float* cvel = c.f(c.L.cvel);
+  float* cdd = c.f(c.L.cdof_dot);
+  float* cinert = c.f(c.L.cinert);
+  float* cacc = c.f(c.L.scr);
+  float* cfrc = cacc + 6 * m.nbody;
+  if (LANE < 6) { cvel[LANE] = 0; cacc[LANE] = LANE < 3 ? 0.f : -m.gravity[LANE - 3]; }
+  SYNC();
+  for (int lv = 0; lv < m.nlevel; lv++) {
+    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
+      int b = m.lvl_body[k], p = m.body_parent[b];
+      float cv[6], ca[6];
+      for (int e = 0; e < 6; e++) { cv[e] = cvel[6 * p + e]; ca[e] = cacc[6 * p + e]; }
+      int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+      for (int j = ja; j < ja + jn; j++) {
+        int da = m.jnt_dofadr[j];
+        if (m.jnt_type[j] == DXJ_FREE) {
+          for (int q = 0; q < 3; q++)
+            for (int e = 0; e < 6; e++) cdd[6 * (da + q) + e] = 0;
+          for (int q = 0; q < 3; q++)
+            for (int e = 0; e < 6; e++) cv[e] += cdof[6 * (da + q) + e] * qvel[da + q];
+          for (int q = 3; q < 6; q++) cross_motion(cdd + 6 * (da + q), cv, cdof + 6 * (da + q));
+          for (int q = 3; q < 6; q++)
+            for (int e = 0; e < 6; e++) cv[e] += cdof[6 * (da + q) + e] * qvel[da + q];
+        } else {
+          cross_motion(cdd + 6 * da, cv, cdof + 6 * da);
+          for (int e = 0; e < 6; e++) cv[e] += cdof[6 * da + e] * qvel[da];
+        }
+      }
+      for (int d = m.body_dofadr[b]; d >= 0 && d < m.body_dofadr[b] + m.body_dofnum[b]; d++)
+        for (int e = 0; e < 6; e++) ca[e] += cdd[6 * d + e] * qvel[d];
+      for (int e = 0; e < 6; e++) { cvel[6 * b + e] = cv[e]; cacc[6 * b + e] = ca[e]; }
+      // body force: I a + v x* I v - applied wrench (as com-frame spatial force)
+      float t1[6], t2[6], t3[6];
+      mul_inert(t1, cinert + 10 * b, ca);
+      mul_inert(t2, cinert + 10 * b, cv);
+      cross_force(t3, cv, t2);
+      for (int e = 0; e < 6; e++) cfrc[6 * b + e] = t1[e] + t3[e];
+      if (xfrc) {
+        const float* f = xfrc + 6 * b;
+        if (f[0] != 0 || f[1] != 0 || f[2] != 0 || f[3] != 0 || f[4] != 0 || f[5] != 0) {
+          const float* rc = c.f(c.L.rcom) + 3 * m.body_rootidx[b];
+          const float* xi = c.f(c.L.xipos) + 3 * b;
+          float off[3] = {xi[0] - rc[0], xi[1] - rc[1], xi[2] - rc[2]};
+          float tq[3];
+          cross3(tq, off, f);
+          cfrc[6 * b + 0] -= f[3] + tq[0];
+          cfrc[6 * b + 1] -= f[4] + tq[1];
+          cfrc[6 * b + 2] -= f[5] + tq[2];
+          cfrc[6 * b + 3] -= f[0];
+          cfrc[6 * b + 4] -= f[1];
+          cfrc[6 * b + 5] -= f[2];
+        }
+      }
+    }
+    SYNC();
+  }
+  for (int lv = m.nlevel - 1; lv > 0; lv--) {
+    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
+      int b = m.lvl_body[k], p = m.body_parent[b];
+      if (p > 0)
+        for (int e = 0; e < 6; e++) atomicAdd(cfrc + 6 * p + e, cfrc[6 * b + e]);
+    }
+    SYNC();
+  }
+  // qfrc_smooth = passive - (bias - applied) + actuator
+  float* qs = c.f(c.L.qfrc_smooth);
+  for (int d = LANE; d < nv; d += DX_WAVE)
+    qs[d] = -m.dof_damping[d] * qvel[d] - dot6(cdof + 6 * d, cfrc + 6 * m.dof_bodyid[d]);
+  SYNC();
+  float* al = c.f(c.L.act_len);
+  float* ctrl = c.f(c.L.ctrl);
+  float* tl = c.f(c.L.ten_len);
+  (void)tl;
+  for (int i = LANE; i < m.nu; i += DX_WAVE) {
+    float cc = ctrl[i];
+    if (m.actuator_ctrllimited[i])
+      cc = fminf(m.actuator_ctrlrange[2 * i + 1], fmaxf(m.actuator_ctrlrange[2 * i], cc));
+    float g = m.actuator_gear[i];
+    int id = m.actuator_trnid[i];
+    float vel;
+    if (m.actuator_trntype[i] == 0) {
+      vel = g * qvel[m.jnt_dofadr[id]];
+    } else {
+      vel = 0;
+      for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++)
+        vel += g * m.wrap_coef[w] * qvel[m.wrap_dof[w]];
+    }
+    float force = m.actuator_gainprm[3 * i] * cc;
+    if (m.actuator_biastype[i] == 1)
+      force += m.actuator_biasprm[3 * i] + m.actuator_biasprm[3 * i + 1] * al[i] + m.actuator_biasprm[3 * i + 2] * vel;
+    if (m.actuator_forcelimited[i])
+      force = fminf(m.actuator_forcerange[2 * i + 1], fmaxf(m.actuator_forcerange[2 * i], force));
+    if (m.actuator_trntype[i] == 0) {
+      atomicAdd(qs + m.jnt_dofadr[id], g * force);
+    } else {
+      for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++)
+        atomicAdd(qs + m.wrap_dof[w], g * m.wrap_coef[w] * force);
+    }
+  }
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
+// Newton solver
+// ------------------------------------------------------------------------ //
+// row cost at jar -> (cost, force, hessian weight)
+__device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf, float jar, float& force, float& hw) {
+  if (type == DXR_FRIC) {
+    if (jar <= -Rf) { force = fl; hw = 0; return -fl * jar - 0.5f * Rf * fl; }
+    if (jar >= Rf) { force = -fl; hw = 0; return fl * jar - 0.5f * Rf * fl; }
+  } else if (jar >= 0) {
+    force = 0; hw = 0; return 0;
+  }
+  force = -D * jar; hw = D;
+  return 0.5f * D * jar * jar;
+}
+
+// y = M x (lanes over rows)
+__device__ void mat_vec(const float* M, const float* x, float* y, int n) {
+  for (int i = LANE; i < n; i += DX_WAVE) {
+    float s = 0;
+    for (int k = 0; k < n; k++) s += M[i * n + k] * x[k];
+    y[i] = s;
+  }
+}
+
+// J x for every row -> out[r]; uses cq as contact-frame scratch
+__device__ void jac_vec(const Ctx& c, const float* x, float* out) {
+  const DevModel& m = c.m;
+  int nefc = c.I[I_NEFC];
+  int ncon = c.I[I_NCON];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const float* cj_val = c.f(c.L.cj_val);
+  float* cq = c.f(c.L.cq);
+  const float* con = c.f(c.L.con);
+  for (int t = LANE; t < 3 * ncon; t += DX_WAVE) {
+    int ci = t / 3, k = t % 3;
+    int nnz = __float_as_int(con[DX_CON_STRIDE * ci + 14]);
+    float s = 0;
+    for (int q = 0; q < nnz; q++) s += cj_val[(ci * 3 + k) * DX_DOFMAX + q] * x[cj_idx[ci * DX_DOFMAX + q]];
+    cq[t] = s;
+  }
+  SYNC();
+  for (int r = LANE; r < nefc; r += DX_WAVE) {
+    int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
+    float v;
+    if (type == DXR_FRIC) v = x[id];
+    else if (type == DXR_LIMJ) v = aux == 0 ? x[m.jnt_dofadr[id]] : -x[m.jnt_dofadr[id]];
+    else if (type == DXR_LIMT) {
+      v = 0;
+      for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++) v += m.wrap_coef[w] * x[m.wrap_dof[w]];
+      if (aux) v = -v;
+    } else if (type == DXR_CONFL) {
+      v = cq[3 * id];
+    } else {
+      int k = 1 + (aux >> 1);
+      int gp = __float_as_int(con[DX_CON_STRIDE * id + 13]);
+      float mu = m.gpair_friction[5 * gp + k - 1] * ((aux & 1) ? -1.f : 1.f);
+      v = cq[3 * id] + mu * cq[3 * id + k];
+    }
+    out[r] = v;
+  }
+  SYNC();
+}
+
+// cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
+__device__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  const float* qs = c.f(c.L.qfrc_smooth);
+  const float* a0 = c.f(c.L.qacc_smooth);
+  float g = 0;
+  for (int i = LANE; i < nv; i += DX_WAVE) g += 0.5f * (qacc[i] - a0[i]) * (Ma[i] - qs[i]);
+  int nefc = c.I[I_NEFC];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* jar = c.f(c.L.efc_jar);
+  for (int r = LANE; r < nefc; r += DX_WAVE) {
+    float f, hw;
+    g += row_cost(meta[r] & 15, D[r], fl[r], Rf[r], jar[r], f, hw);
+  }
+  return wave_sum(g);
+}
+
+// jar = J qacc - aref, Ma = M qacc; returns cost
+__device__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
+  int nv = c.m.nv;
+  mat_vec(c.f(c.L.M), qacc, Ma, nv);
+  float* jar = c.f(c.L.efc_jar);
+  jac_vec(c, qacc, jar);
+  const float* aref = c.f(c.L.efc_aref);
+  int nefc = c.I[I_NEFC];
+  for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] -= aref[r];
+  SYNC();
+  return total_cost(c, qacc, Ma);
+}
+
+// out[d] = sum_r J[r][d] * w[r] computed as J^T applied to the per-row force of the
+// current jar (force mode) -- lane per dof, deterministic.
+__device__ void jac_t_force(const Ctx& c, float* out) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  int nefc = c.I[I_NEFC];
+  int ncon = c.I[I_NCON];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* jar = c.f(c.L.efc_jar);
+  const float* con = c.f(c.L.con);
+  float* cw = c.f(c.L.cw);  // contact frame forces [ncon][3]
+  // contact frame forces
+  for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
+    const float* r = con + DX_CON_STRIDE * ci;
+    int row0 = __float_as_int(r[15]);
+    int gp = __float_as_int(r[13]);
+    float fc[3] = {0, 0, 0};
+    if (m.gpair_condim[gp] == 1) {
+      float f, hw;
+      if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); fc[0] = f; }
+    } else {
+      for (int e = 0; e < 4; e++) {
+        int row = row0 + e;
+        if (row >= nefc) break;
+        float f, hw;
+        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+        int k = 1 + (e >> 1);
+        float mu = m.gpair_friction[5 * gp + k - 1] * ((e & 1) ? -1.f : 1.f);
+        fc[0] += f;
+        fc[k] += mu * f;
+      }
+    }
+    cw[3 * ci] = fc[0]; cw[3 * ci + 1] = fc[1]; cw[3 * ci + 2] = fc[2];
+  }
+  SYNC();
+  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const float* cj_val = c.f(c.L.cj_val);
+  for (int d = LANE; d < nv; d += DX_WAVE) {
+    float s = 0;
+    // friction row of this dof
+    int fr = m.dof_fricrow[d];
+    if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += f; }
+    for (int r = m.nfric; r < nefc; r++) {
+      int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
+      if (type == DXR_LIMJ) {
+        if (m.jnt_dofadr[id] != d) continue;
+        float f, hw;
+        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        s += aux ? -f : f;
+      } else if (type == DXR_LIMT) {
+        float tj = m.tendon_J[id * nv + d];
+        if (tj == 0) continue;
+        float f, hw;
+        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        s += (aux ? -tj : tj) * f;
+      } else {
+        break;  // contact rows are last
+      }
+    }
+    uint64_t bit = 1ull << d;
+    for (int ci = 0; ci < ncon; ci++) {
+      const float* r = con + DX_CON_STRIDE * ci;
+      int gp = __float_as_int(r[13]);
+      int b1 = m.geom_bodyid[m.gpair_geom[2 * gp]], b2 = m.geom_bodyid[m.gpair_geom[2 * gp + 1]];
+      uint64_t sup = m.body_chain[b1] ^ m.body_chain[b2];
+      if (!(sup & bit)) continue;
+      int q = __popcll(sup & (bit - 1));
+      if (q >= DX_DOFMAX) continue;
+      s += cj_val[(ci * 3 + 0) * DX_DOFMAX + q] * cw[3 * ci] + cj_val[(ci * 3 + 1) * DX_DOFMAX + q] * cw[3 * ci + 1] +
+           cj_val[(ci * 3 + 2) * DX_DOFMAX + q] * cw[3 * ci + 2];
+    }
+    out[d] = s;
+  }
+  SYNC();
+}
+
+// H = M + J^T D_active J  (at the current jar)
+__device__ void build_hessian(const Ctx& c) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  int nefc = c.I[I_NEFC];
+  int ncon = c.I[I_NCON];
+  float* H = c.f(c.L.H);
+  const float* M = c.f(c.L.M);
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* jar = c.f(c.L.efc_jar);
+  for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
+  SYNC();
+  // unit rows (friction, joint limits) -> diagonal; lane per dof
+  for (int d = LANE; d < nv; d += DX_WAVE) {
+    float s = 0;
+    int fr = m.dof_fricrow[d];
+    if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
+    for (int r = m.nfric; r < nefc; r++) {
+      int mt = meta[r], type = mt & 15, id = mt >> 8;
+      if (type != DXR_LIMJ) { if (type == DXR_LIMT) continue; break; }
+      if (m.jnt_dofadr[id] != d) continue;
+      float f, hw;
+      row_cost(type, D[r], 0, 0, jar[r], f, hw);
+      s += hw;
+    }
+    H[d * nv + d] += s;
+  }
+  SYNC();
+  // tendon limit rows: dense outer products, lanes over entries
+  for (int r = m.nfric; r < nefc; r++) {
+    int mt = meta[r], type = mt & 15, id = mt >> 8;
+    if (type == DXR_CON || type == DXR_CONFL) break;
+    if (type != DXR_LIMT) continue;
+    float f, hw;
+    row_cost(type, D[r], 0, 0, jar[r], f, hw);
+    if (hw == 0) continue;
+    const float* tj = m.tendon_J + id * nv;
+    for (int k = LANE; k < nv * nv; k += DX_WAVE) {
+      int i = k / nv, j = k % nv;
+      H[k] += hw * tj[i] * tj[j];
+    }
+    SYNC();
+  }
+  // contacts: W = sum_active_edges D c c^T in frame space; H[idx_a][idx_b] += J^T W J
+  const float* con = c.f(c.L.con);
+  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const float* cj_val = c.f(c.L.cj_val);
+  for (int ci = 0; ci < ncon; ci++) {
+    const float* r = con + DX_CON_STRIDE * ci;
+    int row0 = __float_as_int(r[15]);
+    int gp = __float_as_int(r[13]);
+    int nnz = __float_as_int(r[14]);
+    float W[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    if (m.gpair_condim[gp] == 1) {
+      float f, hw;
+      if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); W[0] = hw; }
+    } else {
+      for (int e = 0; e < 4; e++) {
+        int row = row0 + e;
+        if (row >= nefc) break;
+        float f, hw;
+        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+        if (hw == 0) continue;
+        int k = 1 + (e >> 1);
+        float mu = m.gpair_friction[5 * gp + k - 1] * ((e & 1) ? -1.f : 1.f);
+        W[0] += hw;
+        W[k] += hw * mu;
+        W[3 * k] += hw * mu;
+        W[4 * k] += hw * mu * mu;
+      }
+    }
+    if (W[0] == 0 && W[4] == 0 && W[8] == 0) continue;
+    for (int t = LANE; t < nnz * nnz; t += DX_WAVE) {
+      int a = t / nnz, b = t % nnz;
+      float ja[3], jb[3];
+      for (int k = 0; k < 3; k++) {
+        ja[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + a];
+        jb[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + b];
+      }
+      float s = 0;
+      for (int p = 0; p < 3; p++)
+        for (int q = 0; q < 3; q++) s += ja[p] * W[3 * p + q] * jb[q];
+      H[cj_idx[ci * DX_DOFMAX + a] * nv + cj_idx[ci * DX_DOFMAX + b]] += s;
+    }
+    SYNC();
+  }
+}
+
+__device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  float* Mdir = c.f(c.L.v4);
+  mat_vec(c.f(c.L.M), dir, Mdir, nv);
+  float* jv = c.f(c.L.efc_jv);
+  jac_vec(c, dir, jv);  // includes SYNC
+  const float* qs = c.f(c.L.qfrc_smooth);
+  float qa = 0, qb = 0;
+  for (int i = LANE; i < nv; i += DX_WAVE) { qa += dir[i] * Mdir[i]; qb += dir[i] * (Ma[i] - qs[i]); }
+  qa = wave_sum(qa);
+  qb = wave_sum(qb);
+  int nefc = c.I[I_NEFC];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* jar = c.f(c.L.efc_jar);
+  float lo = 0, hi = -1, alpha = 0, g0 = 0;
+  for (int it = 0; it < 40; it++) {
+    float g = 0, h = 0;
+    for (int r = LANE; r < nefc; r += DX_WAVE) {
+      float j = jv[r];
+      if (j == 0) continue;
+      float f, hw;
+      row_cost(meta[r] & 15, D[r], fl[r], Rf[r], jar[r] + alpha * j, f, hw);
+      g -= f * j;
+      h += hw * j * j;
+    }
+    g = wave_sum(g) + qa * alpha + qb;
+    h = wave_sum(h) + qa;
+    if (it == 0) g0 = g;
+    if (fabsf(g) <= 1e-6f * fabsf(g0)) break;
+    if (g < 0) lo = alpha; else hi = alpha;
+    float next = h > 0 ? alpha - g / h : alpha + 1;
+    if (hi >= 0 && (next <= lo || next >= hi)) next = 0.5f * (lo + hi);
+    if (hi < 0 && next <= lo) next = lo + 1;
+    if (fabsf(next - alpha) <= 1e-7f * fabsf(alpha)) break;
+    alpha = next;
+  }
+  return alpha;
+}
+
+__device__ void solve(const Ctx& c) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  float* qacc = c.f(c.L.qacc);
+  float* a0 = c.f(c.L.qacc_smooth);
+  float* ws = c.f(c.L.v5);  // warmstart copy held in v5 by the caller
+  float* Ma = c.f(c.L.v1);
+  float* grad = c.f(c.L.v2);
+  float* dir = c.f(c.L.v3);
+  const float* qs = c.f(c.L.qfrc_smooth);
+  int nefc = c.I[I_NEFC];
+  if (nefc == 0) {
+    for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i];
+    if (LANE == 0) c.I[I_NITER] = 0;
+    SYNC();
+    return;
+  }
+  float scale = 1.0f / (m.meaninertia * (float)max(1, nv));
+  float tol = fmaxf(m.tolerance, 1e-6f);
+  // warm start vs smooth
+  for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
+  SYNC();
+  float cw = eval_cost(c, qacc, Ma);
+  for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i];
+  SYNC();
+  float cs = eval_cost(c, qacc, Ma);
+  float cost = cs;
+  if (cw < cs) {
+    for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
+    SYNC();
+    cost = eval_cost(c, qacc, Ma);
+  }
+  int it = 0;
+  for (; it < m.iterations; it++) {
+    jac_t_force(c, grad);  // grad <- J^T f
+    float gn = 0;
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      grad[i] = Ma[i] - qs[i] - grad[i];
+      gn += grad[i] * grad[i];
+    }
+    gn = sqrtf(wave_sum(gn)) * scale;
+    if (gn < tol) break;
+    build_hessian(c);
+    float* H = c.f(c.L.H);
+    wave_cholesky(H, nv);
+    for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
+    SYNC();
+    wave_chol_solve(H, dir, nv);
+    float alpha = line_search(c, qacc, Ma, dir);
+    for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] += alpha * dir[i];
+    SYNC();
+    float nc = eval_cost(c, qacc, Ma);
+    float impr = scale * (cost - nc);
+    cost = nc;
+    if (impr < tol) { it++; break; }
+  }
+  if (LANE == 0) c.I[I_NITER] = it;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
+// forward + Euler
+// ------------------------------------------------------------------------ //
+__device__ void position_stage(const Ctx& c) {
+  kinematics(c);
+  com_pos(c);
+  tendon_lengths(c);
+  crb_mass(c);
+  collision(c, 0, -1, -1);
+  make_constraint(c);
+}
+
+__device__ void forward(const Ctx& c, const float* xfrc) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  position_stage(c);
+  velocity_stage(c, xfrc);
+  // qacc_smooth = M^-1 qfrc_smooth via Cholesky in H
+  float* H = c.f(c.L.H);
+  const float* M = c.f(c.L.M);
+  for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
+  float* a0 = c.f(c.L.qacc_smooth);
+  const float* qs = c.f(c.L.qfrc_smooth);
+  for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
+  SYNC();
+  wave_cholesky(H, nv);
+  wave_chol_solve(H, a0, nv);
+  solve(c);
+  // qfrc_constraint = J^T f at the solution
+  float* qc = c.f(c.L.qfrc_con);
+  if (c.I[I_NEFC] > 0) {
+    jac_t_force(c, qc);
+  } else {
+    for (int i = LANE; i < nv; i += DX_WAVE) qc[i] = 0;
+    SYNC();
+  }
+}
+
+__device__ void euler(const Ctx& c, float* time) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  float h = m.timestep;
+  float* qacc = c.f(c.L.qacc);
+  float* qvel = c.f(c.L.qvel);
+  float* qpos = c.f(c.L.qpos);
+  float* acc = c.f(c.L.v1);
+  if (m.any_damping) {
+    float* H = c.f(c.L.H);
+    const float* M = c.f(c.L.M);
+    for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
+    SYNC();
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      H[i * nv + i] += h * m.dof_damping[i];
+      acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
+    }
+    SYNC();
+    wave_cholesky(H, nv);
+    wave_chol_solve(H, acc, nv);
+  } else {
+    for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
+    SYNC();
+  }
+  for (int i = LANE; i < nv; i += DX_WAVE) qvel[i] += h * acc[i];
+  SYNC();
+  for (int j = LANE; j < m.njnt; j += DX_WAVE) {
+    int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
+    if (m.jnt_type[j] == DXJ_FREE) {
+      for (int k = 0; k < 3; k++) qpos[qa + k] += h * qvel[da + k];
+      float* q = qpos + qa + 3;
+      const float* w = qvel + da + 3;
+      float wn = norm3(w);
+      if (wn > 1e-20f) {
+        float ang = h * wn, s, co;
+        sincosf(0.5f * ang, &s, &co);
+        float dq[4] = {co, w[0] / wn * s, w[1] / wn * s, w[2] / wn * s};
+        quatmul(q, q, dq);
+      }
+      quatnorm(q);
+    } else {
+      qpos[qa] += h * qvel[da];
+    }
+  }
+  if (LANE == 0) *time += h;
+  SYNC();
+}
+
+// observation pass at the new state: kinematics, com, velocities, sites, watch contact
+__device__ void observe(const Ctx& c, const DevBatch& B, int env) {
+  const DevModel& m = c.m;
+  kinematics(c);
+  com_pos(c);
+  // cvel (no forces)
+  float* qvel = c.f(c.L.qvel);
+  float* cdof = c.f(c.L.cdof);
+  float* cvel = c.f(c.L.cvel);
+  if (LANE < 6) cvel[LANE] = 0;
+  SYNC();
+  for (int lv = 0; lv < m.nlevel; lv++) {
+    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
+      int b = m.lvl_body[k], p = m.body_parent[b];
+      float cv[6];
+      for (int e = 0; e < 6; e++) cv[e] = cvel[6 * p + e];
+      for (int d = m.body_dofadr[b]; d >= 0 && d < m.body_dofadr[b] + m.body_dofnum[b]; d++)
+        for (int e = 0; e < 6; e++) cv[e] += cdof[6 * d + e] * qvel[d];
+      for (int e = 0; e < 6; e++) cvel[6 * b + e] = cv[e];
+    }
+    SYNC();
+  }
+  float* xpos = c.f(c.L.xpos);
+  float* xmat = c.f(c.L.xmat);
+  float* rcom = c.f(c.L.rcom);
+  for (int s = LANE; s < m.nsite; s += DX_WAVE) {
+    int b = m.site_bodyid[s];
+    float t[3];
+    matvec3(t, xmat + 9 * b, m.site_pos + 3 * s);
+    float p[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
+    float* out = B.site_xpos + ((size_t)env * m.nsite + s) * 3;
+    out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
+    const float* cv = cvel + 6 * b;
+    const float* rc = rcom + 3 * m.body_rootidx[b];
+    float off[3] = {p[0] - rc[0], p[1] - rc[1], p[2] - rc[2]};
+    float wx[3];
+    cross3(wx, cv, off);
+    float* vo = B.site_vel + ((size_t)env * m.nsite + s) * 6;
+    vo[0] = cv[3] + wx[0]; vo[1] = cv[4] + wx[1]; vo[2] = cv[5] + wx[2];
+    vo[3] = cv[0]; vo[4] = cv[1]; vo[5] = cv[2];
+  }
+  if (B.watch_geom >= 0 && B.watch) {
+    collision(c, 1, B.watch_geom, B.watch_body);
+    int n = c.I[I_NCON];
+    const float* con = c.f(c.L.con);
+    int hit = 0;
+    for (int k = LANE; k < n; k += DX_WAVE) hit |= con[DX_CON_STRIDE * k + 12] <= 1e-8f;
+    hit = __any(hit);
+    if (LANE == 0) B.watch[env] = hit;
+  }
+}
+
+// ------------------------------------------------------------------------ //
+// kernels
+// ------------------------------------------------------------------------ //
+// mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
+extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+  extern __shared__ float smem[];
+  int env = blockIdx.x;
+  if (env >= B.nenv) return;
+  int* I = (int*)(smem + L.ints);
+  Ctx c{m, L, smem, I};
+  float* qpos = c.f(L.qpos);
+  float* qvel = c.f(L.qvel);
+  float* ctrl = c.f(L.ctrl);
+  float* ws = c.f(L.v5);
+  for (int i = LANE; i < m.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * m.nq + i];
+  for (int i = LANE; i < m.nv; i += DX_WAVE) {
+    qvel[i] = B.qvel[(size_t)env * m.nv + i];
+    ws[i] = B.qacc_ws[(size_t)env * m.nv + i];
+  }
+  for (int i = LANE; i < m.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * m.nu + i];
+  if (LANE < I_NINT) I[LANE] = 0;
+  float time = B.time[env];
+  SYNC();
+  int steps = mode == 0 ? nsub : 1;
+  for (int s = 0; s < steps; s++) {
+    forward(c, B.xfrc);
+    if (mode == 0) {
+      // warmstart <- solved qacc
+      for (int i = LANE; i < m.nv; i += DX_WAVE) ws[i] = c.f(L.qacc)[i];
+      SYNC();
+      euler(c, &time);
+    }
+  }
+  // debug record of the last forward
+  if (B.dbg_qacc_smooth) {
+    for (int i = LANE; i < m.nv; i += DX_WAVE) {
+      B.dbg_qacc_smooth[(size_t)env * m.nv + i] = c.f(L.qacc_smooth)[i];
+      B.dbg_qfrc_smooth[(size_t)env * m.nv + i] = c.f(L.qfrc_smooth)[i];
+    }
+    for (int k = LANE; k < m.nv * m.nv; k += DX_WAVE) B.dbg_M[(size_t)env * m.nv * m.nv + k] = c.f(L.M)[k];
+    int n = I[I_NCON];
+    for (int k = LANE; k < DX_NCON_MAX * 16; k += DX_WAVE) {
+      int ci = k / 16, e = k % 16;
+      float v = 0;
+      if (ci < n) {
+        const float* r = c.f(L.con) + DX_CON_STRIDE * ci;
+        if (e < 13) v = r[e];
+        else {
+          int gp = __float_as_int(r[13]);
+          v = e == 13 ? (float)m.gpair_geom[2 * gp] : e == 14 ? (float)m.gpair_geom[2 * gp + 1] : (float)m.gpair_condim[gp];
+        }
+      }
+      B.dbg_con[(size_t)env * DX_NCON_MAX * 16 + k] = v;
+    }
+    if (LANE == 0) { B.dbg_nefc[2 * env] = I[I_NEFC]; B.dbg_nefc[2 * env + 1] = I[I_OVF]; }
+  }
+  if (LANE == 0) {
+    B.ncon[env] = I[I_NCON];
+    B.niter[env] = I[I_NITER];
+  }
+  for (int i = LANE; i < m.nv; i += DX_WAVE) B.qacc[(size_t)env * m.nv + i] = c.f(L.qacc)[i];
+  SYNC();
+  observe(c, B, env);
+  for (int i = LANE; i < m.nq; i += DX_WAVE) B.qpos[(size_t)env * m.nq + i] = qpos[i];
+  for (int i = LANE; i < m.nv; i += DX_WAVE) {
+    B.qvel[(size_t)env * m.nv + i] = qvel[i];
+    B.qacc_ws[(size_t)env * m.nv + i] = ws[i];
+  }
+  float* xpos = c.f(L.xpos);
+  float* xquat = c.f(L.xquat);
+  for (int k = LANE; k < 3 * m.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * m.nbody + k] = xpos[k];
+  for (int k = LANE; k < 4 * m.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * m.nbody + k] = xquat[k];
+  if (LANE == 0) B.time[env] = time;
+}
+
+// reset envs [env0, env0+n) to qpos0
+extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int n) {
+  int env = env0 + blockIdx.x;
+  if (blockIdx.x >= n || env >= B.nenv) return;
+  for (int i = LANE; i < m.nq; i += blockDim.x) B.qpos[(size_t)env * m.nq + i] = m.qpos0[i];
+  for (int i = LANE; i < m.nv; i += blockDim.x) {
+    B.qvel[(size_t)env * m.nv + i] = 0;
+    B.qacc_ws[(size_t)env * m.nv + i] = 0;
+    B.qacc[(size_t)env * m.nv + i] = 0;
+  }
+  for (int i = LANE; i < m.nu; i += blockDim.x) B.ctrl[(size_t)env * m.nu + i] = 0;
+  if (LANE == 0) B.time[env] = 0;
+}

@@ -1,0 +1,131 @@
+/*
+ * dx.h -- C ABI of the MI355X batched physics step (libdx.so).
+ *
+ * This is the drop-in boundary for the reference's hot path.  In the reference
+ * (v-wewei/dexterity) every environment owns one MuJoCo mjModel/mjData pair behind
+ * dm_control's `mjcf.Physics`, and the path is driven through these calls
+ * ([3P] MuJoCo C API):
+ *
+ *   physics.step()            -> mj_step2(m,d); mj_step1(m,d)   (composer substep loop,
+ *                                 reorient.py:58,61,168 / reach.py:54,59,139)
+ *   physics.forward()         -> mj_forward(m,d)                (fingertip_position.py:95)
+ *   physics.bind(acts).ctrl=  -> d->ctrl                        (effectors/mujoco_actuation.py:33)
+ *   bind(joints).qpos/.qvel   -> d->qpos / d->qvel              (shadow_hand_e.py:121, reorient.py:187)
+ *   xfrc_applied[:] = -m g    -> d->xfrc_applied                (utils/mujoco_utils.py:91-99)
+ *   bind(sites).xpos          -> d->site_xpos                   (dexterous_hand.py:286-291)
+ *   physics.data.contact      -> d->contact, d->ncon            (utils/mujoco_collisions.py:95-119)
+ *
+ * Here one handle (`dx_batch`) owns B environments that share one compiled model;
+ * all state stays resident in HBM and one call advances every environment.
+ *
+ * Conventions:
+ *  - every function returns 0 on success or a negative DX_E* code; the message of
+ *    the last failure on the calling thread is in dx_last_error();
+ *  - state arrays are float32, environment-major: field[env][n];
+ *  - pointers passed to dx_set_field / dx_get_field may be host or device memory
+ *    (resolved through HIP's unified addressing);
+ *  - calls on one dx_batch are serialised on its own HIP stream; a dx_batch is not
+ *    thread-safe; different handles are independent;
+ *  - the library owns all device memory it allocates.
+ */
+#ifndef DX_H
+#define DX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DX_ABI_VERSION 1
+
+typedef struct dx_model dx_model;
+typedef struct dx_batch dx_batch;
+
+enum dx_error {
+  DX_OK = 0,
+  DX_EINVAL = -1,   /* bad argument                        */
+  DX_EMODEL = -2,   /* malformed or unsupported model blob */
+  DX_EHIP = -3,     /* HIP runtime failure                 */
+  DX_ENOMEM = -4,   /* allocation failure                  */
+  DX_ELIMIT = -5    /* model exceeds kernel limits         */
+};
+
+/* Per-environment fields addressable through dx_set_field / dx_get_field /
+ * dx_field_ptr.  Widths are per environment. */
+enum dx_field {
+  DX_QPOS = 0,          /* nq                                    rw */
+  DX_QVEL = 1,          /* nv                                    rw */
+  DX_CTRL = 2,          /* nu                                    rw */
+  DX_QACC_WARMSTART = 3,/* nv                                    rw */
+  DX_QACC = 4,          /* nv   last solved acceleration         r  */
+  DX_TIME = 5,          /* 1                                     rw */
+  DX_SITE_XPOS = 6,     /* 3*nsite  (after dx_step / dx_forward) r  */
+  DX_SITE_VEL = 7,      /* 6*nsite  linear(3) + angular(3), world frame, at site r */
+  DX_XPOS = 8,          /* 3*nbody                               r  */
+  DX_XQUAT = 9,         /* 4*nbody                               r  */
+  DX_NCON = 10,         /* 1  (int32 bits)                       r  */
+  DX_GROUND_CONTACT = 11, /* 1 (int32 bits): any contact involving geom
+                           `ground_geom` with dist <= 1e-8 (reorient.py:229-235) */
+  DX_NITER = 12,        /* 1  (int32 bits) solver iterations of the last substep */
+  DX_NFIELD
+};
+
+/* Model ------------------------------------------------------------------ */
+/* Loads a compiled-model blob (dexterity_amd/blob.py).  The blob is copied. */
+dx_model* dx_model_load(const void* blob, size_t nbytes);
+void dx_model_free(dx_model* m);
+/* Sizes: out[0..11] = nq nv nbody njnt ngeom nsite nu ntendon nbpair ngpair ncon_max nefc_max */
+int dx_model_sizes(const dx_model* m, int32_t out[12]);
+/* Width (in 4-byte words per environment) of a dx_field. */
+int dx_field_width(const dx_model* m, int field);
+
+/* Batch ------------------------------------------------------------------ */
+/* Allocates nenv environments on HIP device `device`, reset to qpos0. */
+dx_batch* dx_batch_create(const dx_model* m, int32_t nenv, int32_t device);
+void dx_batch_destroy(dx_batch* b);
+int dx_batch_nenv(const dx_batch* b);
+/* Resets environments [env0, env0+n) to qpos0, zero velocity, zero ctrl. */
+int dx_reset(dx_batch* b, int32_t env0, int32_t n);
+
+/* Copies n environments' worth of a field, starting at env0. */
+int dx_set_field(dx_batch* b, int field, const void* src, int32_t env0, int32_t n);
+int dx_get_field(dx_batch* b, int field, void* dst, int32_t env0, int32_t n);
+/* Device pointer of a field's [nenv][width] array (zero-copy access). */
+int dx_field_ptr(dx_batch* b, int field, void** devptr);
+/* Batch-shared applied body wrench xfrc_applied[nbody][6] (force, torque), the
+ * gravity-compensation write of utils/mujoco_utils.py:91-99. */
+int dx_set_xfrc(dx_batch* b, const float* xfrc, int32_t nbody);
+/* Geom whose contacts set DX_GROUND_CONTACT (-1 disables). */
+int dx_set_ground_geom(dx_batch* b, int32_t geom);
+/* DX_GROUND_CONTACT watches contacts between `geom` and any geom of `body`
+ * (reorient.py:229-235: prop geoms vs the arena ground). */
+int dx_set_watch(dx_batch* b, int32_t geom, int32_t body);
+
+/* Stepping --------------------------------------------------------------- */
+/* Advances every environment by nsubstep physics steps (ctrl held constant),
+ * then recomputes position-dependent outputs (site poses, velocities, ground
+ * contact) at the new state: the step2->step1 contract of dm_control. */
+int dx_step(dx_batch* b, int32_t nsubstep);
+/* mj_forward equivalent: outputs at the current state, no integration. */
+int dx_forward(dx_batch* b);
+/* Stream the batch's kernels are enqueued on (hipStream_t) and a blocking sync. */
+void* dx_stream(dx_batch* b);
+int dx_sync(dx_batch* b);
+
+/* Debug / parity -------------------------------------------------------- */
+/* When enabled, dx_forward/dx_step record per-env intermediates of the LAST
+ * substep: qacc_smooth, qfrc_bias(+applied), qfrc_actuator, M (nv*nv), contacts. */
+int dx_debug_enable(dx_batch* b, int enable);
+/* name: "qacc_smooth" "qfrc_smooth" "M" "contact" (16 floats/contact: pos3 frame9
+ * dist geom1 geom2 condim) "efc_count" ; dst is host memory for all envs. */
+int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
+
+const char* dx_last_error(void);
+int dx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,80 @@
+/*
+ * dx_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * fp64, single-environment, scalar C restatement of the MuJoCo `mj_step`
+ * pipeline as configured by the dexterity scenes.  It is the parity oracle for
+ * the HIP kernels in dexterity_amd/csrc and the `cpu_baseline` leg of bench.py.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline may load it;
+ * nothing on the product path links or calls it.
+ *
+ * PARITY STATUS vs the reference: the reference path is MuJoCo's C library
+ * ([3P], absent from /root/reference and not installable here).  This file
+ * restates MuJoCo's published pipeline from the model data the
+ * reference configures; it is pinned only by the reference's own known-answer
+ * tests restated under tests/ (reorient_test.py:13-50 reward KAT,
+ * hands_test.py:26-31 projections, physical invariants).  Dynamics parity against
+ * real MuJoCo is UNPINNED.
+ */
+#ifndef DX_ORACLE_H
+#define DX_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dxo_model dxo_model;
+typedef struct dxo_data dxo_data;
+
+/* Stage FLOP counters (flops counted as mul/add/div/sqrt = 1). */
+enum {
+  DXO_ST_KIN = 0,   /* kinematics + com + cdof                        */
+  DXO_ST_CRB,       /* tendon, transmission, CRB, factorization       */
+  DXO_ST_COL,       /* broadphase + narrowphase                       */
+  DXO_ST_CON,       /* constraint assembly (J, R, aref)               */
+  DXO_ST_SMOOTH,    /* comVel, passive, RNE, actuation, qacc_smooth   */
+  DXO_ST_SOLVE,     /* Newton solver                                  */
+  DXO_ST_INT,       /* implicit-damping Euler                         */
+  DXO_NSTAGE
+};
+
+dxo_model* dxo_model_load(const void* blob, size_t nbytes);
+void dxo_model_free(dxo_model* m);
+dxo_data* dxo_data_create(const dxo_model* m);
+void dxo_data_free(dxo_data* d);
+void dxo_reset(const dxo_model* m, dxo_data* d);
+
+/* mj_forward: everything up to and including the constraint solve. */
+int dxo_forward(const dxo_model* m, dxo_data* d);
+/* mj_step with the Euler integrator: forward + implicit-damping Euler. */
+int dxo_step(const dxo_model* m, dxo_data* d);
+/* Position-only pass (kinematics + collision), as used for observations. */
+int dxo_kinematics(const dxo_model* m, dxo_data* d);
+
+/* Field access: returns a pointer to the named double array and its length.
+ * Names: qpos qvel ctrl qacc qacc_warmstart qacc_smooth qfrc_bias qfrc_passive
+ * qfrc_actuator qfrc_applied qfrc_smooth qfrc_constraint xfrc_applied xpos xquat
+ * xmat xipos site_xpos M actuator_force actuator_length ten_length cvel
+ * efc_force efc_aref efc_R efc_pos efc_J time.  */
+double* dxo_field(dxo_data* d, const char* name, int* len);
+
+int dxo_ncon(const dxo_data* d);
+/* contact i: out[0:3]=pos, [3:12]=frame, [12]=dist, [13]=geom1, [14]=geom2, [15]=condim */
+void dxo_contact(const dxo_data* d, int i, double out[16]);
+int dxo_nefc(const dxo_data* d);
+int dxo_solver_niter(const dxo_data* d);
+void dxo_flops(const dxo_data* d, double out[DXO_NSTAGE]);
+void dxo_flops_reset(dxo_data* d);
+
+/* Batched CPU stepping for the baseline timing: nenv independent envs,
+ * OpenMP over envs when built with -fopenmp. state arrays are [nenv, n]. */
+int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
+                   const double* ctrl, double* qacc_warmstart, const double* xfrc,
+                   int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

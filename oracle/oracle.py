@@ -1,0 +1,159 @@
+"""ctypes binding of the CPU oracle -- TEST INFRASTRUCTURE ONLY.
+
+Loaded only by tests/, `__graft_entry__.smoke()` and bench.py's cpu_baseline leg.
+Parity status: see dx_oracle.h (MuJoCo dynamics parity unpinned).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+NSTAGE = 7
+STAGES = ("kinematics", "crb", "collision", "constraint", "smooth", "solver", "integrate")
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, sz, ip = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.dxo_model_load.restype = vp
+        L.dxo_model_load.argtypes = [ctypes.c_char_p, sz]
+        L.dxo_model_free.argtypes = [vp]
+        L.dxo_data_create.restype = vp
+        L.dxo_data_create.argtypes = [vp]
+        L.dxo_data_free.argtypes = [vp]
+        L.dxo_reset.argtypes = [vp, vp]
+        for fn in ("dxo_forward", "dxo_step", "dxo_kinematics"):
+            getattr(L, fn).argtypes = [vp, vp]
+            getattr(L, fn).restype = ip
+        L.dxo_field.restype = dp
+        L.dxo_field.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ip)]
+        L.dxo_ncon.argtypes = [vp]
+        L.dxo_ncon.restype = ip
+        L.dxo_nefc.argtypes = [vp]
+        L.dxo_nefc.restype = ip
+        L.dxo_solver_niter.argtypes = [vp]
+        L.dxo_solver_niter.restype = ip
+        L.dxo_contact.argtypes = [vp, ip, dp]
+        L.dxo_flops.argtypes = [vp, dp]
+        L.dxo_flops_reset.argtypes = [vp]
+        L.dxo_batch_step.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip]
+        L.dxo_batch_step.restype = ip
+        _lib = L
+    return _lib
+
+
+class OracleModel:
+    def __init__(self, blob: bytes):
+        self._blob = blob
+        self.ptr = lib().dxo_model_load(blob, len(blob))
+        if not self.ptr:
+            raise RuntimeError("oracle failed to load model blob")
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.dxo_model_free(self.ptr)
+            self.ptr = None
+
+
+class OracleData:
+    """One environment's state, with numpy views onto the oracle's arrays."""
+
+    def __init__(self, model: OracleModel):
+        self.model = model
+        self.ptr = lib().dxo_data_create(model.ptr)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) and _lib is not None:
+            _lib.dxo_data_free(self.ptr)
+            self.ptr = None
+
+    def field(self, name: str) -> np.ndarray:
+        n = ctypes.c_int(0)
+        p = lib().dxo_field(self.ptr, name.encode(), ctypes.byref(n))
+        if not p:
+            raise KeyError(name)
+        if n.value == 0:
+            return np.zeros(0)
+        return np.ctypeslib.as_array(p, shape=(n.value,))
+
+    def __getattr__(self, item):
+        if item in ("model", "ptr"):
+            raise AttributeError(item)
+        return self.field(item)
+
+    def reset(self):
+        lib().dxo_reset(self.model.ptr, self.ptr)
+
+    def forward(self):
+        return lib().dxo_forward(self.model.ptr, self.ptr)
+
+    def step(self):
+        return lib().dxo_step(self.model.ptr, self.ptr)
+
+    def kinematics(self):
+        return lib().dxo_kinematics(self.model.ptr, self.ptr)
+
+    @property
+    def ncon(self) -> int:
+        return lib().dxo_ncon(self.ptr)
+
+    @property
+    def nefc(self) -> int:
+        return lib().dxo_nefc(self.ptr)
+
+    @property
+    def niter(self) -> int:
+        return lib().dxo_solver_niter(self.ptr)
+
+    def contacts(self) -> np.ndarray:
+        out = np.zeros((self.ncon, 16))
+        buf = (ctypes.c_double * 16)()
+        for i in range(self.ncon):
+            lib().dxo_contact(self.ptr, i, buf)
+            out[i] = np.frombuffer(buf, dtype=np.float64)
+        return out
+
+    def flops(self) -> np.ndarray:
+        buf = (ctypes.c_double * NSTAGE)()
+        lib().dxo_flops(self.ptr, buf)
+        return np.frombuffer(buf, dtype=np.float64).copy()
+
+    def flops_reset(self):
+        lib().dxo_flops_reset(self.ptr)
+
+
+def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub: int, nthreads: int = 0):
+    """Steps nenv independent envs nsub times (OpenMP over envs). Arrays are updated in place."""
+    dp = ctypes.POINTER(ctypes.c_double)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (qpos, qvel, ctrl, qacc_warmstart)]
+    x = None if xfrc is None else np.ascontiguousarray(xfrc, dtype=np.float64)
+    rc = lib().dxo_batch_step(
+        model.ptr,
+        arrs[0].shape[0],
+        nsub,
+        arrs[0].ctypes.data_as(dp),
+        arrs[1].ctypes.data_as(dp),
+        arrs[2].ctypes.data_as(dp),
+        arrs[3].ctypes.data_as(dp),
+        None if x is None else x.ctypes.data_as(dp),
+        nthreads,
+    )
+    return rc, arrs[0], arrs[1], arrs[3]
