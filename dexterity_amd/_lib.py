@@ -24,7 +24,11 @@ EXPORTS = (
     "dx_set_field", "dx_get_field", "dx_field_ptr", "dx_set_xfrc", "dx_set_ground_geom",
     "dx_set_watch", "dx_step", "dx_forward", "dx_stream", "dx_sync",
     "dx_debug_enable", "dx_debug_get", "dx_last_error", "dx_abi_version",
+    "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
+    "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
 )
+OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
+TASK_REORIENT = 0
 
 _lib = None
 
@@ -68,6 +72,17 @@ def load(path: str = LIB_PATH):
     L.dx_debug_get.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.dx_last_error.restype = ctypes.c_char_p
     L.dx_abi_version.restype = ctypes.c_int
+    L.dx_env_create.restype = vp
+    L.dx_env_create.argtypes = [vp, i32, i32, i32, ctypes.c_uint64, vp, i32]
+    L.dx_env_destroy.argtypes = [vp]
+    L.dx_env_batch.restype = vp
+    L.dx_env_batch.argtypes = [vp]
+    L.dx_env_obs_dim.argtypes = [vp]
+    L.dx_env_reset.argtypes = [vp]
+    L.dx_env_step.argtypes = [vp, vp]
+    L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
+    L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
+    L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]
     _lib = L
     return L
 

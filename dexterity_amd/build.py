@@ -8,7 +8,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdx.so")
-SOURCES = ("dx_step.hip", "dx_api.hip")
+SOURCES = ("dx_step.hip", "dx_task.hip", "dx_api.hip")
 HEADERS = ("dx_internal.h",)
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 

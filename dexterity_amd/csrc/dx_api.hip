@@ -623,3 +623,154 @@ extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nf
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;
 }
+
+// ------------------------------------------------------------------------ //
+// environments: physics batch + on-device task logic
+// ------------------------------------------------------------------------ //
+extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatch B, const float* qpos0,
+                                              const float* action);
+extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B);
+
+struct dx_env {
+  dx_batch* batch;
+  TaskParams P;
+  TaskState S;
+  int nsub;
+  std::vector<void*> allocs;
+};
+
+extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task,
+                                 uint64_t seed, const float* params, int32_t nparams) {
+  if (task != DX_TASK_REORIENT) { fail(DX_EINVAL, "unknown task kind"); return nullptr; }
+  if (!params || nparams < DX_REORIENT_NPARAMS) { fail(DX_EINVAL, "reorient needs 26 params"); return nullptr; }
+  dx_batch* b = dx_batch_create(m, nenv, device);
+  if (!b) return nullptr;
+  dx_env* e = new dx_env();
+  e->batch = b;
+  const DevModel& d = b->dm;
+  TaskParams& P = e->P;
+  memset(&P, 0, sizeof(P));
+  P.kind = task;
+  P.nenv = nenv; P.nq = d.nq; P.nv = d.nv; P.nu = d.nu; P.nsite = d.nsite;
+  e->nsub = (int)params[0];
+  P.hand_nq = (int)params[1]; P.hand_nv = (int)params[2];
+  P.prop_qadr = (int)params[3]; P.prop_dadr = (int)params[4];
+  P.tip_site0 = (int)params[5]; P.ntips = (int)params[6];
+  P.successes_needed = (int)params[7]; P.steps_before_change = (int)params[8];
+  P.fall_termination = (int)params[9];
+  P.threshold = params[10]; P.eps = params[11]; P.w_orient = params[12]; P.w_success = params[13];
+  P.w_action = params[14]; P.max_time = params[15];
+  for (int k = 0; k < 3; k++) { P.bbox_lo[k] = params[16 + k]; P.bbox_hi[k] = params[19 + k]; }
+  int watch_geom = (int)params[22], watch_body = (int)params[23];
+  P.seed = seed;
+  P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + (P.prop_qadr >= 0 ? 17 : 0) + 4;
+  if (P.hand_nq > d.nq || P.hand_nv > d.nv || P.tip_site0 + P.ntips > d.nsite || e->nsub < 1 ||
+      (P.prop_qadr >= 0 && (P.prop_qadr + 7 > d.nq || P.prop_dadr + 6 > d.nv))) {
+    fail(DX_EINVAL, "task parameters inconsistent with the model");
+    dx_batch_destroy(b);
+    delete e;
+    return nullptr;
+  }
+  if (watch_geom >= 0 && dx_set_watch(b, watch_geom, watch_body) != 0) { dx_batch_destroy(b); delete e; return nullptr; }
+  TaskState& S = e->S;
+  size_t E = nenv;
+  auto al = [&](void** p, size_t bytes) { return balloc(b, p, bytes); };
+  int rc = 0;
+  rc |= al((void**)&S.goal, E * 16); rc |= al((void**)&S.solve_start, E * 4);
+  rc |= al((void**)&S.reward, E * 4); rc |= al((void**)&S.discount, E * 4);
+  rc |= al((void**)&S.obs, E * P.obs_dim * 4);
+  rc |= al((void**)&S.successes, E * 4); rc |= al((void**)&S.counter, E * 4);
+  rc |= al((void**)&S.registered, E * 4); rc |= al((void**)&S.exceeded, E * 4);
+  rc |= al((void**)&S.step_type, E * 4); rc |= al((void**)&S.episode, E * 4);
+  rc |= al((void**)&S.skip, E * 4); rc |= al((void**)&S.failure, E * 4);
+  if (rc) { dx_batch_destroy(b); delete e; return nullptr; }
+  std::vector<int> neg(E, -1);
+  if (hipMemcpy(S.episode, neg.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    fail(DX_EHIP, "hipMemcpy failed");
+    dx_batch_destroy(b);
+    delete e;
+    return nullptr;
+  }
+  b->db.skip = S.skip;
+  return e;
+}
+
+extern "C" void dx_env_destroy(dx_env* e) {
+  if (!e) return;
+  dx_batch_destroy(e->batch);
+  delete e;
+}
+
+extern "C" dx_batch* dx_env_batch(dx_env* e) { return e ? e->batch : nullptr; }
+extern "C" int dx_env_obs_dim(const dx_env* e) { return e ? e->P.obs_dim : fail(DX_EINVAL, "null env"); }
+
+static int env_run(dx_env* e, const float* action) {
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  int nb = (e->P.nenv + 63) / 64;
+  hipLaunchKernelGGL(dx_task_pre_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db,
+                     b->dm.qpos0, action);
+  HIPCHK(hipGetLastError());
+  if (int rc = launch_step(b, e->nsub, 0)) return rc;
+  hipLaunchKernelGGL(dx_task_post_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int dx_env_reset(dx_env* e) {
+  if (!e) return fail(DX_EINVAL, "null env");
+  std::vector<int> neg(e->P.nenv, -1);
+  // episode < 0 forces initialize_episode in the pre-kernel for every env
+  std::vector<int> cur(e->P.nenv);
+  HIPCHK(hipMemcpyAsync(cur.data(), e->S.episode, cur.size() * 4, hipMemcpyDeviceToHost, e->batch->stream));
+  HIPCHK(hipStreamSynchronize(e->batch->stream));
+  std::vector<int> last(e->P.nenv, 2);
+  HIPCHK(hipMemcpyAsync(e->S.step_type, last.data(), last.size() * 4, hipMemcpyHostToDevice, e->batch->stream));
+  HIPCHK(hipStreamSynchronize(e->batch->stream));
+  return env_run(e, nullptr);
+}
+
+extern "C" int dx_env_step(dx_env* e, const float* action) {
+  if (!e || !action) return fail(DX_EINVAL, "null env or action");
+  return env_run(e, action);
+}
+
+extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
+  if (!e || !devptr) return fail(DX_EINVAL, "null argument");
+  switch (which) {
+    case DX_OUT_OBS: *devptr = e->S.obs; return 0;
+    case DX_OUT_REWARD: *devptr = e->S.reward; return 0;
+    case DX_OUT_DISCOUNT: *devptr = e->S.discount; return 0;
+    case DX_OUT_STEP_TYPE: *devptr = e->S.step_type; return 0;
+    case DX_OUT_GOAL: *devptr = e->S.goal; return 0;
+    case DX_OUT_SUCCESSES: *devptr = e->S.successes; return 0;
+  }
+  return fail(DX_EINVAL, "unknown output");
+}
+
+extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
+                                                    int step, float* out);
+
+extern "C" int dx_env_action_buffer(dx_env* e, void** devptr) {
+  if (!e || !devptr) return fail(DX_EINVAL, "null argument");
+  if (e->allocs.empty()) {
+    void* p = nullptr;
+    if (int rc = balloc(e->batch, &p, (size_t)e->P.nenv * std::max(e->P.nu, 1) * 4)) return rc;
+    e->allocs.push_back(p);
+  }
+  *devptr = e->allocs[0];
+  return 0;
+}
+
+extern "C" int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step) {
+  if (!e) return fail(DX_EINVAL, "null env");
+  void* buf = nullptr;
+  if (int rc = dx_env_action_buffer(e, &buf)) return rc;
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  int n = e->P.nenv * e->P.nu;
+  hipLaunchKernelGGL(dx_sample_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
+                     e->P.nu, b->dm.actuator_ctrlrange, seed, step, (float*)buf);
+  HIPCHK(hipGetLastError());
+  return 0;
+}

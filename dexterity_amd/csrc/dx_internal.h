@@ -62,6 +62,7 @@ struct DevBatch {
   float *site_xpos, *site_vel, *xpos, *xquat;
   int *ncon, *watch, *niter;
   const float* xfrc;  // [nbody*6], shared by all envs (may be null)
+  const int* skip;    // [nenv] nonzero: env was just reset, observe only (may be null)
   int watch_geom, watch_body;
   // debug (null when disabled)
   float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
@@ -80,3 +81,23 @@ struct Lds {
   int nefc_max, cand_max;
   int total;
 };
+
+// Task (reorient) parameters and per-env task state, see dx_task.hip.
+struct TaskParams {
+  int kind;                 // 0 = reorient
+  int nenv, nq, nv, nu, nsite;
+  int hand_nq, hand_nv;     // hand joints are qpos[0:hand_nq], qvel[0:hand_nv]
+  int prop_qadr, prop_dadr; // free joint of the prop
+  int tip_site0, ntips;     // fingertip sites
+  int obs_dim;
+  int successes_needed, steps_before_change, fall_termination;
+  float threshold, eps, w_orient, w_success, w_action, max_time, timestep_ctrl;
+  float bbox_lo[3], bbox_hi[3];
+  uint64_t seed;
+};
+
+struct TaskState {
+  float *goal, *solve_start, *reward, *discount, *obs;
+  int *successes, *counter, *registered, *exceeded, *step_type, *episode, *skip, *failure;
+};
+

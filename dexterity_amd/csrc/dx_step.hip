@@ -1734,6 +1734,7 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
   float time = B.time[env];
   SYNC();
   int steps = mode == 0 ? nsub : 1;
+  if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
   for (int s = 0; s < steps; s++) {
     forward(c, B.xfrc);
     if (mode == 0) {

@@ -1,0 +1,193 @@
+// dx_task.hip -- batched task logic on the device.
+//
+// The reference runs these per environment in Python around every control step
+// (composer hooks):
+//   GoalTask.before_step       task.py:154-165   goal change after >5 successes
+//   GoalTask.after_step        task.py:167-185   distance, success counters, per-goal timeout
+//   ReOrient.after_step        reorient.py:201-209 + _is_prop_fallen :229-235
+//   should_terminate_episode   task.py:187-193, reorient.py:211-213
+//   get_discount               task.py:195-204, reorient.py:222-225
+//   get_reward                 reorient.py:215-220 -> _get_shaped_reorientation_reward :238-284
+//   observables                dexterous_hand.py:250-310 (sin/cos, qvel, fingertip pos/vel),
+//                              prop pose sensors, goal task.py:207-216
+//   initialize_episode         reorient.py:182-188 (PropPlacer bbox :70-78, UniformQuaternion goal)
+// Here they run as two tiny kernels (one thread per environment) bracketing the
+// fused physics step, so an env-step never leaves the GPU.
+//
+// dm_env semantics: after a LAST step the next step() of that env resets it and
+// returns FIRST (composer.Environment.step), done here by the pre-kernel + the
+// physics kernel's skip mask.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "dx_internal.h"
+
+enum { ST_FIRST = 0, ST_MID = 1, ST_LAST = 2 };
+
+// counter-based RNG: splitmix64 over (seed, env, episode, draw)
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float urand(uint64_t seed, int env, int episode, int draw) {
+  uint64_t h = mix64(seed ^ mix64(((uint64_t)env << 32) ^ (uint64_t)episode) ^ mix64(0x51ed27ull + draw));
+  return (float)((h >> 40) * (1.0 / 16777216.0));
+}
+// uniform unit quaternion (Shoemake), as dm_control rotations.UniformQuaternion
+__device__ void uniform_quat(uint64_t seed, int env, int episode, int draw0, float* q) {
+  float u1 = urand(seed, env, episode, draw0), u2 = urand(seed, env, episode, draw0 + 1),
+        u3 = urand(seed, env, episode, draw0 + 2);
+  float a = sqrtf(1 - u1), b = sqrtf(u1);
+  float s2, c2, s3, c3;
+  sincosf(6.283185307179586f * u2, &s2, &c2);
+  sincosf(6.283185307179586f * u3, &s3, &c3);
+  q[0] = b * c3; q[1] = a * s2; q[2] = a * c2; q[3] = b * s3;
+}
+
+// orientation distance || axisangle(quat_diff_active(cur, goal)) || = 2 acos(|<goal, cur>|)
+// (prop_orientation.py:40-50, [3P] dm_robotics quat_diff_active / quat_to_axisangle)
+__device__ __forceinline__ float quat_distance(const float* g, const float* c) {
+  float n = sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2] + c[3] * c[3]);
+  float d = fabsf(g[0] * c[0] + g[1] * c[1] + g[2] * c[2] + g[3] * c[3]) / fmaxf(n, 1e-20f);
+  return 2.0f * acosf(fminf(1.0f, d));
+}
+
+extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatch B, const float* qpos0,
+                                              const float* action) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= P.nenv) return;
+  // action -> ctrl (effectors/mujoco_actuation.py:33; MuJoCo clamps internally)
+  if (action)
+    for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = action[(size_t)env * P.nu + i];
+  int st = S.step_type[env];
+  if (st == ST_LAST || S.episode[env] < 0) {
+    // initialize_episode: qpos0, prop placed uniformly in the bbox with a uniform
+    // orientation, new goal; reorient.py:182-188
+    int ep = S.episode[env] + 1;
+    S.episode[env] = ep;
+    float* q = B.qpos + (size_t)env * P.nq;
+    for (int i = 0; i < P.nq; i++) q[i] = qpos0[i];
+    for (int i = 0; i < P.nv; i++) {
+      B.qvel[(size_t)env * P.nv + i] = 0;
+      B.qacc_ws[(size_t)env * P.nv + i] = 0;
+    }
+    if (action)
+      for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = 0;
+    B.time[env] = 0;
+    float* g = S.goal + 4 * env;
+    uniform_quat(P.seed, env, ep, 0, g);  // goal first (GoalTask.initialize_episode)
+    if (P.prop_qadr >= 0) {
+      for (int k = 0; k < 3; k++)
+        q[P.prop_qadr + k] = P.bbox_lo[k] + (P.bbox_hi[k] - P.bbox_lo[k]) * urand(P.seed, env, ep, 3 + k);
+      uniform_quat(P.seed, env, ep, 6, q + P.prop_qadr + 3);
+    }
+    S.successes[env] = 0;
+    S.counter[env] = 0;
+    S.registered[env] = 0;
+    S.exceeded[env] = 0;
+    S.failure[env] = 0;
+    S.solve_start[env] = 0;
+    S.skip[env] = 1;
+    return;
+  }
+  S.skip[env] = 0;
+  // GoalTask.before_step (task.py:154-165)
+  if (S.counter[env] > P.steps_before_change) {
+    int draw = 16 + 3 * S.successes[env];
+    uniform_quat(P.seed, env, S.episode[env], draw, S.goal + 4 * env);
+    S.counter[env] = 0;
+    S.exceeded[env] = 0;
+    S.solve_start[env] = B.time[env];
+    S.registered[env] = 0;
+  }
+}
+
+extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B) {
+  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= P.nenv) return;
+  const float* q = B.qpos + (size_t)env * P.nq;
+  const float* v = B.qvel + (size_t)env * P.nv;
+  const float* g = S.goal + 4 * env;
+  float cur[4] = {1, 0, 0, 0};
+  if (P.prop_qadr >= 0)
+    for (int k = 0; k < 4; k++) cur[k] = q[P.prop_qadr + 3 + k];
+  float dist = quat_distance(g, cur);
+  bool reset = S.skip[env] != 0;
+  if (reset) {
+    S.step_type[env] = ST_FIRST;
+    S.reward[env] = 0;
+    S.discount[env] = 1;
+  } else {
+    // GoalTask.after_step (task.py:167-185)
+    float time = B.time[env];
+    if (dist <= P.threshold) {
+      S.counter[env] += 1;
+      if (!S.registered[env]) { S.successes[env] += 1; S.registered[env] = 1; }
+    } else if (P.max_time > 0 && time - S.solve_start[env] > P.max_time) {
+      S.exceeded[env] = 1;
+    }
+    // ReOrient.after_step: fall detection (prop-ground contact at the new state)
+    int failure = P.fall_termination && B.watch && B.watch[env];
+    S.failure[env] = failure;
+    bool success_done = S.successes[env] >= P.successes_needed;
+    bool terminate = success_done || S.exceeded[env] || failure;
+    // reward (reorient.py:238-284): 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
+    float cn = 0;
+    for (int i = 0; i < P.nu; i++) {
+      float c = B.ctrl[(size_t)env * P.nu + i];
+      cn += c * c;
+    }
+    float r = P.w_orient * (1.0f / (dist + P.eps)) + P.w_success * (dist <= P.threshold ? 1.0f : 0.0f) +
+              P.w_action * cn;
+    S.reward[env] = r;
+    // discount (reorient.py:222-225, task.py:195-204)
+    S.discount[env] = failure ? 1.0f : (success_done ? 0.0f : 1.0f);
+    S.step_type[env] = terminate ? ST_LAST : ST_MID;
+  }
+  // observation (STATE_ONLY), flat layout:
+  // [sin/cos(qpos_hand) 2*hand_nq | qvel_hand | tip pos 3*ntips | tip linvel 3*ntips |
+  //  prop pos 3 | prop quat 4 | prop linvel 3 | prop angvel 3 | target quat 4 | goal 4]
+  float* o = S.obs + (size_t)env * P.obs_dim;
+  int k = 0;
+  for (int i = 0; i < P.hand_nq; i++) {
+    float s, c;
+    sincosf(q[i], &s, &c);
+    o[k++] = s;
+    o[k++] = c;
+  }
+  for (int i = 0; i < P.hand_nv; i++) o[k++] = v[i];
+  for (int t = 0; t < P.ntips; t++)
+    for (int e = 0; e < 3; e++) o[k++] = B.site_xpos[((size_t)env * P.nsite + P.tip_site0 + t) * 3 + e];
+  for (int t = 0; t < P.ntips; t++)
+    for (int e = 0; e < 3; e++) o[k++] = B.site_vel[((size_t)env * P.nsite + P.tip_site0 + t) * 6 + e];
+  if (P.prop_qadr >= 0) {
+    for (int e = 0; e < 3; e++) o[k++] = q[P.prop_qadr + e];
+    float n = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2] + cur[3] * cur[3]);
+    for (int e = 0; e < 4; e++) o[k++] = cur[e] / n;
+    for (int e = 0; e < 3; e++) o[k++] = v[P.prop_dadr + e];
+    // frameangvel: world-frame angular velocity = R(quat) * local omega
+    float w0 = cur[0] / n, x = cur[1] / n, y = cur[2] / n, z = cur[3] / n;
+    float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w0 * z), 2 * (x * z + w0 * y),
+                  2 * (x * y + w0 * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w0 * x),
+                  2 * (x * z - w0 * y), 2 * (y * z + w0 * x), 1 - 2 * (x * x + y * y)};
+    const float* wl = v + P.prop_dadr + 3;
+    for (int e = 0; e < 3; e++) o[k++] = R[3 * e] * wl[0] + R[3 * e + 1] * wl[1] + R[3 * e + 2] * wl[2];
+    for (int e = 0; e < 4; e++) o[k++] = g[e];  // target_prop/orientation (hint cube = goal)
+  }
+  for (int e = 0; e < 4; e++) o[k++] = g[e];  // goal_state
+}
+
+// Uniform random actions within the actuator ctrlrange: the synthetic agent of
+// manipulation_test.py:44-45 (random_state.uniform(spec.minimum, spec.maximum)).
+extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
+                                                    int step, float* out) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nenv * nu) return;
+  int env = t / nu, i = t % nu;
+  float u = urand(seed, env, step, 1000 + i);
+  float lo = ctrlrange[2 * i], hi = ctrlrange[2 * i + 1];
+  out[t] = lo + (hi - lo) * u;
+}

@@ -1,0 +1,272 @@
+"""Task suite and batched environments (manipulation/__init__.py in the reference).
+
+`load(domain, task, seed, num_envs, device)` mirrors `manipulation.load`
+(manipulation/__init__.py:56-86) and returns a `GoalEnvironment` whose
+`reset()` / `step(action)` follow dm_env semantics for every one of `num_envs`
+environments at once (batched TimeStep, leading env axis).  The physics and the
+task logic run on the GPU (dx_env_* in include/dx.h); these classes hold the
+reference's constants and the host-side API.
+
+Suite (names as in the reference):
+  reorient.state_dense   manipulation/tasks/reorient.py:367-371  (Shadow hand + cube)
+"""
+
+from __future__ import annotations
+
+import collections
+import ctypes
+import dataclasses
+import os
+from typing import Dict, Optional
+
+import numpy as np
+
+from dexterity_amd import _lib
+from dexterity_amd import effectors as effectors_lib
+from dexterity_amd import physics as physics_lib
+from dexterity_amd.mjcf.compiler import CompiledModel
+from dexterity_amd.specs import Array, BoundedArray, StepType, TimeStep
+
+ASSETS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets")
+
+
+@dataclasses.dataclass(frozen=True)
+class ReOrientConfig:
+    """Constants of manipulation/tasks/reorient.py:40-78 and GoalTask defaults."""
+
+    physics_timestep: float = 0.005  # reorient.py:58
+    control_timestep: float = 0.025  # reorient.py:61
+    orientation_eps: float = 0.1  # reorient.py:50
+    orientation_threshold: float = 0.1  # reorient.py:52
+    orientation_weight: float = 1.0  # reorient.py:54
+    success_bonus_weight: float = 800.0  # reorient.py:55
+    action_smoothing_weight: float = -0.1  # reorient.py:56
+    successes_needed: int = 1  # reorient.py:64
+    max_steps_single_solve: int = 300  # reorient.py:67
+    steps_before_moving_target: int = 5  # reorient.py:70
+    fall_termination: bool = True  # reorient.py:103
+    prop_bbox_lower: tuple = (-0.025, -0.155, 0.16)  # reorient.py:72-78
+    prop_bbox_upper: tuple = (0.025, -0.105, 0.16)
+
+    @property
+    def n_sub_steps(self) -> int:
+        return int(round(self.control_timestep / self.physics_timestep))
+
+    @property
+    def max_time_per_goal(self) -> float:
+        return self.max_steps_single_solve * self.control_timestep
+
+
+def observation_layout(hand_nq: int, hand_nv: int, ntips: int, with_prop: bool, hand: str) -> "collections.OrderedDict[str, slice]":
+    """Named slices of the flat observation vector written by dx_task_post_kernel."""
+    out = collections.OrderedDict()
+    k = 0
+
+    def add(name, n):
+        nonlocal k
+        out[name] = slice(k, k + n)
+        k += n
+
+    add(f"{hand}/joint_positions_sin_cos", 2 * hand_nq)
+    add(f"{hand}/joint_velocities", hand_nv)
+    add(f"{hand}/fingertip_positions", 3 * ntips)
+    add(f"{hand}/fingertip_linear_velocities", 3 * ntips)
+    if with_prop:
+        add("prop/position", 3)
+        add("prop/orientation", 4)
+        add("prop/linear_velocity", 3)
+        add("prop/angular_velocity", 3)
+        add("target_prop/orientation", 4)
+    add("goal_state", 4)
+    return out
+
+
+class ReOrient:
+    """Batched counterpart of `ReOrient` (reorient.py:90-235)."""
+
+    domain = "reorient"
+
+    def __init__(self, config: ReOrientConfig = ReOrientConfig(), asset: str = "shadow_reorient.npz"):
+        self.config = config
+        self.compiled = CompiledModel.load(os.path.join(ASSETS, asset))
+        cm = self.compiled
+        if abs(cm.timestep - config.physics_timestep) > 1e-12:
+            raise ValueError("asset timestep does not match the task's physics timestep")
+        self.hand_name = "shadow_hand_e"
+        names = cm.names
+        self.hand_joint_ids = [i for i, n in enumerate(names["joint"]) if n.startswith(self.hand_name + "/")]
+        self.hand_nq = len(self.hand_joint_ids)
+        self.hand_nv = self.hand_nq
+        prop_j = names["joint"].index("prop/")
+        self.prop_qadr = int(cm.jnt_qposadr[prop_j])
+        self.prop_dadr = int(cm.jnt_dofadr[prop_j])
+        self.prop_body = names["body"].index("prop/")
+        self.ground_geom = names["geom"].index("ground")
+        tip_sites = [f"{self.hand_name}/{t}_site" for t in ("fftip", "mftip", "rftip", "lftip", "thtip")]
+        self.tip_site0 = names["site"].index(tip_sites[0])
+        assert [names["site"].index(s) for s in tip_sites] == list(range(self.tip_site0, self.tip_site0 + 5))
+        self.ntips = 5
+        self.actuator_ids = list(range(cm.nu))
+        self.hand_effector = effectors_lib.HandEffector(self.actuator_ids, self.hand_name)
+        self.gravity_compensation = physics_lib.gravity_compensation(cm, self.hand_name + "/")
+
+    def params(self) -> np.ndarray:
+        c = self.config
+        p = np.zeros(26, dtype=np.float32)
+        p[0] = c.n_sub_steps
+        p[1], p[2] = self.hand_nq, self.hand_nv
+        p[3], p[4] = self.prop_qadr, self.prop_dadr
+        p[5], p[6] = self.tip_site0, self.ntips
+        p[7], p[8], p[9] = c.successes_needed, c.steps_before_moving_target, int(c.fall_termination)
+        p[10], p[11] = c.orientation_threshold, c.orientation_eps
+        p[12], p[13], p[14] = c.orientation_weight, c.success_bonus_weight, c.action_smoothing_weight
+        p[15] = c.max_time_per_goal
+        p[16:19] = c.prop_bbox_lower
+        p[19:22] = c.prop_bbox_upper
+        p[22], p[23] = self.ground_geom, self.prop_body
+        return p
+
+    def observation_layout(self):
+        return observation_layout(self.hand_nq, self.hand_nv, self.ntips, True, self.hand_name)
+
+
+class GoalEnvironment:
+    """Batched `GoalEnvironment` (environment.py:9-34) over `num_envs` environments.
+
+    `step(action)` accepts a host array [num_envs, nu] or, with `device_action=True`,
+    the integer address of a device buffer; outputs stay on the device unless read
+    through `timestep()` / `observation()`.
+    """
+
+    def __init__(self, task: ReOrient, num_envs: int, seed: Optional[int] = None, device: int = 0):
+        self.task = task
+        self.num_envs = int(num_envs)
+        self.model = physics_lib.Model(task.compiled)
+        L = _lib.load()
+        p = task.params()
+        self._seed = 0 if seed is None else int(seed)
+        self.ptr = L.dx_env_create(self.model.ptr, self.num_envs, device, _lib.TASK_REORIENT,
+                                   self._seed, p.ctypes.data, len(p))
+        if not self.ptr:
+            raise _lib.DxError(f"dx_env_create failed: {L.dx_last_error().decode()}")
+        batch_ptr = L.dx_env_batch(self.ptr)
+        self.physics = physics_lib.BatchedPhysics.borrowed(self.model, batch_ptr, self.num_envs, device)
+        # gravity compensation (shadow_hand_e.py:35-41 in initialize_episode)
+        self.physics.set_xfrc(task.gravity_compensation)
+        self.obs_dim = _lib.check(L.dx_env_obs_dim(self.ptr))
+        self._layout = task.observation_layout()
+        self._action_spec = task.hand_effector.action_spec(self.physics)
+        self._host_action = np.zeros((self.num_envs, self.model.nu), dtype=np.float32)
+        self._dev_action = self._out(-1)
+
+    def close(self):
+        if getattr(self, "physics", None) is not None:
+            self.physics.ptr = None
+        if getattr(self, "ptr", None) and _lib._lib is not None:
+            _lib._lib.dx_env_destroy(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+    def _out(self, which: int) -> int:
+        p = ctypes.c_void_p()
+        L = _lib.load()
+        if which < 0:
+            _lib.check(L.dx_env_action_buffer(self.ptr, ctypes.byref(p)))
+        else:
+            _lib.check(L.dx_env_output(self.ptr, which, ctypes.byref(p)))
+        return p.value
+
+    # ---------------------------------------------------------------- specs
+    def action_spec(self) -> BoundedArray:
+        return self._action_spec
+
+    def observation_spec(self) -> "collections.OrderedDict[str, Array]":
+        return collections.OrderedDict(
+            (k, Array((s.stop - s.start,), np.float64, name=k)) for k, s in self._layout.items()
+        )
+
+    # ---------------------------------------------------------------- stepping
+    def reset(self) -> TimeStep:
+        _lib.check(_lib.load().dx_env_reset(self.ptr))
+        return self.timestep(first=True)
+
+    def step(self, action, device_action: bool = False) -> Optional[TimeStep]:
+        L = _lib.load()
+        if device_action:
+            _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(int(action))))
+            return None
+        a = np.ascontiguousarray(action, dtype=np.float32).reshape(self.num_envs, -1)
+        _lib.check(_lib.load().dx_set_field(self.physics.ptr, _lib.CTRL, a.ctypes.data, 0, self.num_envs))
+        # copy host actions into the device action buffer via the ctrl field
+        ctrl_ptr = self.physics.field_ptr(_lib.CTRL)
+        self.physics.sync()
+        _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(ctrl_ptr)))
+        return self.timestep()
+
+    def sample_actions(self, step: int) -> int:
+        """Fills the device action buffer with uniform actions; returns its address."""
+        _lib.check(_lib.load().dx_env_sample_actions(self.ptr, self._seed, step))
+        return self._dev_action
+
+    def _read(self, which: int, dtype, width: int) -> np.ndarray:
+        out = np.empty((self.num_envs, width), dtype=dtype)
+        ptr = self._out(which)
+        L = _lib.load()
+        stream = L.dx_stream(self.physics.ptr)
+        del stream
+        self.physics.sync()
+        _copy_d2h(out, ptr)
+        return out
+
+    def timestep(self, first: bool = False) -> TimeStep:
+        obs = self._read(_lib.OUT_OBS, np.float32, self.obs_dim)
+        st = self._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0]
+        rew = self._read(_lib.OUT_REWARD, np.float32, 1)[:, 0].astype(np.float64)
+        disc = self._read(_lib.OUT_DISCOUNT, np.float32, 1)[:, 0].astype(np.float64)
+        observation = collections.OrderedDict(
+            (k, obs[:, s].astype(np.float64)) for k, s in self._layout.items()
+        )
+        return TimeStep(st.astype(np.int32), rew, disc, observation)
+
+    def goals(self) -> np.ndarray:
+        return self._read(_lib.OUT_GOAL, np.float32, 4)
+
+    def successes(self) -> np.ndarray:
+        return self._read(_lib.OUT_SUCCESSES, np.int32, 1)[:, 0]
+
+
+def _copy_d2h(out: np.ndarray, devptr: int) -> None:
+    """Device -> host copy through the HIP runtime libdx is linked against."""
+    global _hip
+    if _hip is None:
+        try:
+            _hip = ctypes.CDLL("libamdhip64.so.7")
+        except OSError:
+            _hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rc = _hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(devptr), out.nbytes, 2)  # DeviceToHost
+    if rc != 0:
+        raise _lib.DxError(f"hipMemcpy failed ({rc})")
+
+
+_hip = None
+
+SUITE = {("reorient", "state_dense"): ReOrient}
+ALL_TASKS = tuple(sorted(SUITE))
+ALL_NAMES = [".".join(t) for t in ALL_TASKS]
+
+
+def load(domain_name: str, task_name: str, seed: Optional[int] = None, num_envs: int = 1,
+         device: int = 0) -> GoalEnvironment:
+    """manipulation/__init__.py:56-86 (batched)."""
+    key = (domain_name, task_name)
+    if domain_name not in {d for d, _ in SUITE}:
+        raise ValueError(f"Unknown domain: {domain_name}")
+    if key not in SUITE:
+        raise ValueError(f"Unknown task: {task_name}")
+    return GoalEnvironment(SUITE[key](), num_envs=num_envs, seed=seed, device=device)
+
+
+__all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "ALL_TASKS", "ALL_NAMES", "StepType"]

@@ -56,15 +56,24 @@ class BatchedPhysics:
         self.nenv = int(nenv)
         self.device = device
         self.ptr = L.dx_batch_create(model.ptr, self.nenv, device)
+        self._owned = True
         if not self.ptr:
             raise _lib.DxError(f"dx_batch_create failed: {L.dx_last_error().decode()}")
 
-    def close(self):
-        if getattr(self, "ptr", None) and _lib._lib is not None:
-            _lib._lib.dx_batch_destroy(self.ptr)
-            self.ptr = None
+    @classmethod
+    def borrowed(cls, model: Model, ptr: int, nenv: int, device: int) -> "BatchedPhysics":
+        """A view of a batch owned elsewhere (e.g. by a dx_env); never destroyed here."""
+        self = cls.__new__(cls)
+        self.model, self.ptr, self.nenv, self.device, self._owned = model, ptr, int(nenv), device, False
+        return self
 
-    __del__ = close
+    def close(self):
+        if getattr(self, "ptr", None) and getattr(self, "_owned", False) and _lib._lib is not None:
+            _lib._lib.dx_batch_destroy(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        self.close()
 
     # ------------------------------------------------------------------ #
     def step(self, nsubstep: int = 1) -> None:

@@ -122,6 +122,42 @@ int dx_debug_enable(dx_batch* b, int enable);
  * dist geom1 geom2 condim) "efc_count" ; dst is host memory for all envs. */
 int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
 
+/* Environments: a dx_batch plus on-device task logic ------------------- */
+/* One dx_env is B copies of a reference task (composer.Environment + Task,
+ * environment.py:9-34, task.py:137-204): dx_env_step = GoalTask.before_step,
+ * n_sub_steps physics steps, after_step, reward, discount, termination and the
+ * observation vector, for every env, with dm_env auto-reset (an env that returned
+ * LAST is re-initialised by its next step and returns FIRST). */
+typedef struct dx_env dx_env;
+enum dx_task_kind { DX_TASK_REORIENT = 0 };
+/* Reorient params (float[26]), reorient.py:40-78 / task.py:120-135:
+ *  0 n_sub_steps  1 hand_nq  2 hand_nv  3 prop_qposadr  4 prop_dofadr
+ *  5 first fingertip site  6 n fingertips  7 successes_needed
+ *  8 steps_before_changing_goal  9 fall_termination  10 success_threshold
+ *  11 orientation_eps  12 w_orientation  13 w_success  14 w_action
+ *  15 max_time_per_goal  16-18 prop bbox lower  19-21 prop bbox upper
+ *  22 ground geom  23 prop body  24-25 reserved */
+#define DX_REORIENT_NPARAMS 26
+enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT_STEP_TYPE = 3,
+                  DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5 };
+dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task, uint64_t seed,
+                      const float* params, int32_t nparams);
+void dx_env_destroy(dx_env* e);
+dx_batch* dx_env_batch(dx_env* e);
+int dx_env_obs_dim(const dx_env* e);
+/* Re-initialises every env (initialize_episode) and computes FIRST observations. */
+int dx_env_reset(dx_env* e);
+/* One control step for every env; action is [nenv][nu] float32, device memory. */
+int dx_env_step(dx_env* e, const float* action);
+/* Device pointers of the outputs: obs [nenv][obs_dim] f32, reward/discount [nenv] f32,
+ * step_type [nenv] i32 (0 FIRST, 1 MID, 2 LAST), goal [nenv][4] f32, successes i32. */
+int dx_env_output(dx_env* e, int which, void** devptr);
+/* Library-owned [nenv][nu] device action buffer, and a fill of it with actions
+ * drawn uniformly within each actuator's ctrlrange (the random agent of
+ * manipulation_test.py:44-45), keyed by (seed, env, step). */
+int dx_env_action_buffer(dx_env* e, void** devptr);
+int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
+
 const char* dx_last_error(void);
 int dx_abi_version(void);
 
