@@ -26,6 +26,7 @@ EXPORTS = (
     "dx_debug_enable", "dx_debug_get", "dx_last_error", "dx_abi_version",
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
+    "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read",
 )
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
 TASK_REORIENT = 0
@@ -83,6 +84,9 @@ def load(path: str = LIB_PATH):
     L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
     L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]
+    L.dx_env_pack_outputs.argtypes = [vp, vp]
+    L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
+    L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     _lib = L
     return L
 

@@ -550,11 +550,17 @@ extern "C" int dx_set_watch(dx_batch* b, int32_t geom, int32_t body) {
   return 0;
 }
 
+static void timing_begin(dx_batch* b, hipEvent_t* start);
+static void timing_end(dx_batch* b, hipEvent_t start);
+
 static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
+  hipEvent_t t0;
+  timing_begin(b, &t0);
   hipLaunchKernelGGL(dx_step_kernel, dim3(b->nenv), dim3(64), lds, b->stream, b->dm, b->db,
                      b->model->lds, nsub, mode);
+  timing_end(b, t0);
   HIPCHK(hipGetLastError());
   return 0;
 }
@@ -771,6 +777,70 @@ extern "C" int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step) {
   int n = e->P.nenv * e->P.nu;
   hipLaunchKernelGGL(dx_sample_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
                      e->P.nu, b->dm.actuator_ctrlrange, seed, step, (float*)buf);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------------ //
+// kernel timing (HIP events around every step-kernel launch on the batch stream)
+// ------------------------------------------------------------------------ //
+struct TimingState {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+  bool on = false;
+};
+static std::map<const dx_batch*, TimingState> g_timing;
+
+static void timing_begin(dx_batch* b, hipEvent_t* start) {
+  auto it = g_timing.find(b);
+  *start = nullptr;
+  if (it == g_timing.end() || !it->second.on) return;
+  hipEventCreate(start);
+  hipEventRecord(*start, b->stream);
+}
+static void timing_end(dx_batch* b, hipEvent_t start) {
+  if (!start) return;
+  hipEvent_t stop;
+  hipEventCreate(&stop);
+  hipEventRecord(stop, b->stream);
+  g_timing[b].ev.emplace_back(start, stop);
+}
+
+extern "C" int dx_timing_enable(dx_batch* b, int enable) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  g_timing[b].on = enable != 0;
+  return 0;
+}
+
+extern "C" int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count) {
+  if (!b || !total_ms || !count) return fail(DX_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  double tot = 0;
+  auto& st = g_timing[b];
+  for (auto& p : st.ev) {
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    tot += ms;
+    hipEventDestroy(p.first);
+    hipEventDestroy(p.second);
+  }
+  *total_ms = tot;
+  *count = (int32_t)st.ev.size();
+  st.ev.clear();
+  return 0;
+}
+
+// packs [obs | reward | discount | step_type] per env into dst (device, [nenv][obs_dim+3])
+extern "C" __global__ void dx_pack_outputs_kernel(int nenv, int obs_dim, const float* obs, const float* rew,
+                                                  const float* disc, const int* st, float* dst);
+
+extern "C" int dx_env_pack_outputs(dx_env* e, float* dst_dev) {
+  if (!e || !dst_dev) return fail(DX_EINVAL, "null argument");
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  int n = e->P.nenv * (e->P.obs_dim + 3);
+  hipLaunchKernelGGL(dx_pack_outputs_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
+                     e->P.obs_dim, e->S.obs, e->S.reward, e->S.discount, e->S.step_type, dst_dev);
   HIPCHK(hipGetLastError());
   return 0;
 }

@@ -191,3 +191,17 @@ extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const floa
   float lo = ctrlrange[2 * i], hi = ctrlrange[2 * i + 1];
   out[t] = lo + (hi - lo) * u;
 }
+
+extern "C" __global__ void dx_pack_outputs_kernel(int nenv, int obs_dim, const float* obs, const float* rew,
+                                                  const float* disc, const int* st, float* dst) {
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  int w = obs_dim + 3;
+  if (t >= nenv * w) return;
+  int env = t / w, k = t % w;
+  float v;
+  if (k < obs_dim) v = obs[(size_t)env * obs_dim + k];
+  else if (k == obs_dim) v = rew[env];
+  else if (k == obs_dim + 1) v = disc[env];
+  else v = (float)st[env];
+  dst[t] = v;
+}

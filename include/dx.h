@@ -158,6 +158,16 @@ int dx_env_output(dx_env* e, int which, void** devptr);
 int dx_env_action_buffer(dx_env* e, void** devptr);
 int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
 
+/* Packs [obs | reward | discount | step_type] per env into dst ([nenv][obs_dim+3]
+ * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */
+int dx_env_pack_outputs(dx_env* e, float* dst_dev);
+
+/* Timing ---------------------------------------------------------------- */
+/* When enabled, HIP events bracket every step-kernel launch on the batch stream;
+ * dx_timing_read syncs, returns the summed kernel time and launch count, and clears. */
+int dx_timing_enable(dx_batch* b, int enable);
+int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
+
 const char* dx_last_error(void);
 int dx_abi_version(void);
 
