@@ -15,8 +15,8 @@ LIB_PATH = os.path.join(_HERE, "libdx.so")
 
 # dx_field
 QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
-SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER = 6, 7, 8, 9, 10, 11, 12
-INT_FIELDS = (NCON, GROUND_CONTACT, NITER)
+SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND = 6, 7, 8, 9, 10, 11, 12, 13
+INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND)
 
 EXPORTS = (
     "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_field_width",
@@ -26,8 +26,11 @@ EXPORTS = (
     "dx_debug_enable", "dx_debug_get", "dx_last_error", "dx_abi_version",
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
-    "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read",
+    "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
 )
+STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
+          "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
+          "qfrc_constraint", "euler", "observe", "io")
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
 TASK_REORIENT = 0
 
@@ -87,6 +90,8 @@ def load(path: str = LIB_PATH):
     L.dx_env_pack_outputs.argtypes = [vp, vp]
     L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
+    L.dx_stage_timing.argtypes = [vp, ctypes.c_int]
+    L.dx_stage_read.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), i32]
     _lib = L
     return L
 

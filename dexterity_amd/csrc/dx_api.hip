@@ -115,18 +115,18 @@ static const char* kFloatArrays[] = {
     "body_pos", "body_quat", "body_ipos", "body_iquat", "body_mass", "body_inertia", "body_bsphere",
     "body_invweight0", "jnt_pos", "jnt_axis", "jnt_range", "jnt_margin", "jnt_solref", "jnt_solimp",
     "qpos0", "dof_armature", "dof_damping", "dof_frictionloss", "dof_solref", "dof_solimp",
-    "dof_invweight0", "geom_size", "geom_pos", "geom_quat", "geom_center", "geom_bsphere", "mesh_vert",
+    "dof_invweight0", "geom_size", "geom_pos", "geom_quat", "geom_center", "geom_bsphere", "geom_aabb", "mesh_vert",
     "site_pos", "site_quat", "tendon_range", "tendon_margin", "tendon_solref", "tendon_solimp",
     "tendon_invweight0", "wrap_coef", "actuator_gear", "actuator_gainprm", "actuator_biasprm",
     "actuator_ctrlrange", "actuator_forcerange", "gpair_friction", "gpair_solref", "gpair_solimp",
-    "gpair_margin", "gravity"};
+    "gpair_margin", "gravity", "bpair_sphere"};
 static const char* kIntArrays[] = {
     "body_parent", "body_rootid", "body_jntnum", "body_jntadr", "body_dofnum", "body_dofadr",
     "jnt_type", "jnt_bodyid", "jnt_qposadr", "jnt_dofadr", "jnt_limited", "dof_bodyid",
     "dof_parentid", "dof_jntid", "geom_type", "geom_bodyid", "geom_dataid", "mesh_vertadr",
     "mesh_vertnum", "site_bodyid", "tendon_adr", "tendon_num", "tendon_limited", "wrap_dof",
     "actuator_trntype", "actuator_trnid", "actuator_biastype", "actuator_ctrllimited",
-    "actuator_forcelimited", "bpair_body", "bpair_adr", "bpair_num", "gpair_geom", "gpair_condim"};
+    "actuator_forcelimited", "bpair_body", "bpair_adr", "bpair_num", "bpair_plane", "gpair_geom", "gpair_condim"};
 
 extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   if (!blob) { fail(DX_EINVAL, "null blob"); return nullptr; }
@@ -210,6 +210,33 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   mats("body_iquat", "body_imat", nb);
   mats("geom_quat", "geom_mat", d.ngeom);
   mats("site_quat", "site_mat", d.nsite);
+  // geom bounding spheres with centres in the body frame (mid-phase cull)
+  {
+    std::vector<float> gb(4 * std::max(d.ngeom, 1), 0.f);
+    auto& gs = m->hf["geom_bsphere"];
+    auto& gp = m->hf["geom_pos"];
+    auto& gm = m->hf["geom_mat"];
+    for (int g = 0; g < d.ngeom; g++) {
+      const float* R = gm.data() + 9 * g;
+      const float* cc = gs.data() + 4 * g;
+      for (int k = 0; k < 3; k++)
+        gb[4 * g + k] = gp[3 * g + k] + R[3 * k] * cc[0] + R[3 * k + 1] * cc[1] + R[3 * k + 2] * cc[2];
+      gb[4 * g + 3] = cc[3];
+    }
+    m->hf["geom_bsphere_b"] = gb;
+    // oriented bounding box in the body frame: centre(3), R(9) body<-box, half extents(3)
+    std::vector<float> ob(15 * std::max(d.ngeom, 1), 0.f);
+    auto& ga = m->hf["geom_aabb"];
+    for (int g = 0; g < d.ngeom; g++) {
+      const float* R = gm.data() + 9 * g;
+      const float* a = ga.data() + 6 * g;
+      for (int k = 0; k < 3; k++)
+        ob[15 * g + k] = gp[3 * g + k] + R[3 * k] * a[0] + R[3 * k + 1] * a[1] + R[3 * k + 2] * a[2];
+      for (int k = 0; k < 9; k++) ob[15 * g + 3 + k] = R[k];
+      for (int k = 0; k < 3; k++) ob[15 * g + 12 + k] = a[3 + k];
+    }
+    m->hf["geom_obb_b"] = ob;
+  }
   // friction rows / limited joints / limited tendons
   std::vector<int> fric_dof, dof_fricrow(nv, -1), limj, limt;
   auto& floss = m->hf["dof_frictionloss"];
@@ -259,7 +286,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.rcom = take(3 * std::max(d.nroot, 1)); L.cinert = take(10 * nb); L.cdof = take(6 * nv);
   L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.scr = take(12 * nb);
   L.M = take(nv * nv);
-  L.cand_max = std::max(nv * nv, 512);
+  L.cand_max = std::max(nv * nv, 768);
   L.H = take(L.cand_max);
   L.ten_len = take(std::max(d.ntendon, 1)); L.act_len = take(std::max(d.nu, 1));
   L.act_force = take(std::max(d.nu, 1));
@@ -272,6 +299,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_fl = take(L.nefc_max); L.efc_Rf = take(L.nefc_max); L.efc_jar = take(L.nefc_max);
   L.efc_jv = take(L.nefc_max);
+  L.tri = take((nv * (nv + 1) / 2 + 1) / 2);
   L.ints = take(16);
   L.total = off;
   m->ncon_max = DX_NCON_MAX;
@@ -312,7 +340,7 @@ extern "C" int dx_field_width(const dx_model* m, int field) {
     case DX_QPOS: return d.nq;
     case DX_QVEL: case DX_QACC_WARMSTART: case DX_QACC: return d.nv;
     case DX_CTRL: return d.nu;
-    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: return 1;
+    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: case DX_NCAND: return 1;
     case DX_SITE_XPOS: return 3 * d.nsite;
     case DX_SITE_VEL: return 6 * d.nsite;
     case DX_XPOS: return 3 * d.nbody;
@@ -358,7 +386,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UI(limj_jnt); UI(dof_bodyid); UI(dof_parentid); UI(dof_jntid); UI(fric_dof); UI(dof_fricrow);
   UF(dof_armature); UF(dof_damping); UF(dof_frictionloss); UF(dof_solref); UF(dof_solimp); UF(dof_invweight0);
   UI(geom_type); UI(geom_bodyid); UI(geom_dataid);
-  UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere);
+  UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere); UF(geom_bsphere_b); UF(geom_obb_b);
   UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert);
   UI(site_bodyid); UF(site_pos); UF(site_mat);
   UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
@@ -367,7 +395,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UI(actuator_trntype); UI(actuator_trnid); UI(actuator_biastype); UI(actuator_ctrllimited);
   UI(actuator_forcelimited);
   UF(actuator_gear); UF(actuator_gainprm); UF(actuator_biasprm); UF(actuator_ctrlrange); UF(actuator_forcerange);
-  UI(bpair_body); UI(bpair_adr); UI(bpair_num); UI(gpair_geom); UI(gpair_condim);
+  UI(bpair_body); UI(bpair_adr); UI(bpair_num); UI(bpair_plane); UF(bpair_sphere); UI(gpair_geom); UI(gpair_condim);
   UF(gpair_friction); UF(gpair_solref); UF(gpair_solimp); UF(gpair_margin);
 #undef UF
 #undef UI
@@ -442,6 +470,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.ncon, E * 4);
   rc |= balloc(b, (void**)&B.watch, E * 4);
   rc |= balloc(b, (void**)&B.niter, E * 4);
+  rc |= balloc(b, (void**)&B.ncand, E * 4);
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
@@ -487,6 +516,7 @@ static void* field_base(dx_batch* b, int field) {
     case DX_NCON: return B.ncon;
     case DX_GROUND_CONTACT: return B.watch;
     case DX_NITER: return B.niter;
+    case DX_NCAND: return B.ncand;
   }
   return nullptr;
 }
@@ -842,5 +872,27 @@ extern "C" int dx_env_pack_outputs(dx_env* e, float* dst_dev) {
   hipLaunchKernelGGL(dx_pack_outputs_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
                      e->P.obs_dim, e->S.obs, e->S.reward, e->S.discount, e->S.step_type, dst_dev);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+extern "C" int dx_stage_timing(dx_batch* b, int enable) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (enable && !b->db.stage_acc) {
+    void* p = nullptr;
+    if (int rc = balloc(b, &p, DX_NSTAGE * 8)) return rc;
+    b->db.stage_acc = (unsigned long long*)p;
+  } else if (!enable) {
+    b->db.stage_acc = nullptr;
+  }
+  return 0;
+}
+
+extern "C" int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n) {
+  if (!b || !out) return fail(DX_EINVAL, "null argument");
+  if (!b->db.stage_acc) return fail(DX_EINVAL, "stage timing not enabled");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemcpyAsync(out, b->db.stage_acc, std::min(n, DX_NSTAGE) * 8, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipMemsetAsync(b->db.stage_acc, 0, DX_NSTAGE * 8, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
   return 0;
 }

@@ -37,7 +37,7 @@ struct DevModel {
       *dof_invweight0;
   // geoms / meshes
   const int *geom_type, *geom_bodyid, *geom_dataid;
-  const float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere;
+  const float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere, *geom_bsphere_b, *geom_obb_b;
   const int *mesh_vertadr, *mesh_vertnum;
   const float* mesh_vert;
   // sites
@@ -52,7 +52,8 @@ struct DevModel {
   const float *actuator_gear, *actuator_gainprm, *actuator_biasprm, *actuator_ctrlrange,
       *actuator_forcerange;
   // collision pairs
-  const int *bpair_body, *bpair_adr, *bpair_num, *gpair_geom, *gpair_condim;
+  const int *bpair_body, *bpair_adr, *bpair_num, *bpair_plane, *gpair_geom, *gpair_condim;
+  const float* bpair_sphere;  // [nbpair][8]: sphere of side 1, side 2 (body frames)
   const float *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
 };
 
@@ -60,14 +61,16 @@ struct DevBatch {
   int nenv;
   float *qpos, *qvel, *ctrl, *qacc_ws, *qacc, *time;
   float *site_xpos, *site_vel, *xpos, *xquat;
-  int *ncon, *watch, *niter;
+  int *ncon, *watch, *niter, *ncand;
   const float* xfrc;  // [nbody*6], shared by all envs (may be null)
   const int* skip;    // [nenv] nonzero: env was just reset, observe only (may be null)
   int watch_geom, watch_body;
   // debug (null when disabled)
   float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
   int* dbg_nefc;
+  unsigned long long* stage_acc;  // [DX_NSTAGE] s_memtime cycles per stage (null: off)
 };
+#define DX_NSTAGE 24
 
 // Offsets (in 4-byte words) of every per-env LDS array.
 struct Lds {
@@ -77,6 +80,7 @@ struct Lds {
   int M, H, ten_len, act_len, act_force;
   int con, cj_idx, cj_val, cq, cw;
   int efc_meta, efc_D, efc_aref, efc_fl, efc_Rf, efc_jar, efc_jv;
+  int tri;   // ushort lower-triangle index table
   int ints;  // misc int scalars
   int nefc_max, cand_max;
   int total;

@@ -37,6 +37,40 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// DPP row reductions (gfx9 family): quad_perm, row_half_mirror, row_mirror, then
+// row_bcast15 / row_bcast31 carry the partial results up to lane 63.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK, 0xF, false));
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ float wave_max_f(float m) {
+  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x141, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x140, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x142, 0xA>(m));
+  m = fmaxf(m, dpp_f<0x143, 0xC>(m));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 63));
+}
+__device__ __forceinline__ int wave_min_i(int m) {
+  m = min(m, dpp_i<0xB1, 0xF>(m));
+  m = min(m, dpp_i<0x4E, 0xF>(m));
+  m = min(m, dpp_i<0x141, 0xF>(m));
+  m = min(m, dpp_i<0x140, 0xF>(m));
+  m = min(m, dpp_i<0x142, 0xA>(m));
+  m = min(m, dpp_i<0x143, 0xC>(m));
+  return __builtin_amdgcn_readlane(m, 63);
+}
+// index of the first (lowest-index) maximum over lanes' (best, index) pairs
+__device__ __forceinline__ int wave_argmax_first(float best, int bi) {
+  float vmax = wave_max_f(best);
+  return wave_min_i(best == vmax ? bi : 0x7fffffff);
+}
+
 // exclusive prefix sum over lanes
 __device__ __forceinline__ int wave_excl_scan(int v) {
   int x = v;
@@ -147,8 +181,22 @@ struct Ctx {
   const Lds& L;
   float* S;
   int* I;  // misc ints
+  unsigned long long* stage_acc;
   __device__ float* f(int off) const { return S + off; }
 };
+// Per-stage cycle accounting (runtime-gated by DevBatch::stage_acc, lane 0 only).
+enum {
+  ST_KIN = 0, ST_CRB, ST_BROAD, ST_MID, ST_NARROW, ST_CON, ST_VEL, ST_SMOOTH, ST_NEWTON_EVAL,
+  ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO
+};
+__device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
+  if (c.stage_acc && LANE == 0) {
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    unsigned long long* last = (unsigned long long*)(c.I + 10);
+    atomicAdd(c.stage_acc + k, t - *last);
+    *last = t;
+  }
+}
 // misc int slots
 enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
 
@@ -347,46 +395,46 @@ __device__ void crb_mass(const Ctx& c) {
   SYNC();
 }
 
-// In-place dense Cholesky (lower) of the nv x nv matrix A, wave-parallel.
-__device__ void wave_cholesky(float* A, int n) {
+// In-place dense Cholesky (lower, row-major) of the n x n matrix A, one wave.
+// Column k: lanes scale the sub-diagonal of column k, then update the trailing
+// lower triangle; entry t of a w x w trailing triangle maps to (ii, jj) through
+// the LDS table tri[t] = ii << 8 | jj (built once per launch), so the update is
+// branch-free and balanced over the 64 lanes.  Two barriers per column.
+__device__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
   for (int k = 0; k < n; k++) {
-    float akk = A[k * n + k];
-    akk = sqrtf(fmaxf(akk, 1e-30f));
-    float inv = 1.0f / akk;
-    SYNC();
+    float d = sqrtf(fmaxf(A[k * n + k], 1e-30f));
+    float inv = 1.0f / d;
     for (int i = k + 1 + LANE; i < n; i += DX_WAVE) A[i * n + k] *= inv;
-    if (LANE == 0) A[k * n + k] = akk;
     SYNC();
-    int w = n - k - 1;  // trailing lower triangle: rows i=k+1..n-1, cols j=k+1..i
+    if (LANE == 0) A[k * n + k] = d;
+    int w = n - k - 1;
     int tot = w * (w + 1) / 2;
     for (int t = LANE; t < tot; t += DX_WAVE) {
-      // map t -> (ii, jj) with 0<=jj<=ii<w
-      int ii = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-      while ((ii + 1) * (ii + 2) / 2 <= t) ii++;
-      while (ii * (ii + 1) / 2 > t) ii--;
-      int jj = t - ii * (ii + 1) / 2;
-      int i = k + 1 + ii, j = k + 1 + jj;
+      int e = tri[t];
+      int i = k + 1 + (e >> 8), j = k + 1 + (e & 255);
       A[i * n + j] -= A[i * n + k] * A[j * n + k];
     }
     SYNC();
   }
 }
-// Solve (L L^T) x = b in place on x (x holds b on entry). L lower, row-major.
+// Solve (L L^T) x = b; x holds b on entry (LDS).  Lane i keeps x_i in a register;
+// the dependent chain uses readlane broadcasts and no barriers.  n <= 64.
 __device__ void wave_chol_solve(const float* A, float* x, int n) {
+  float xi = LANE < n ? x[LANE] : 0.f;
   for (int k = 0; k < n; k++) {
-    SYNC();
-    float xk = x[k] / A[k * n + k];
-    SYNC();
-    if (LANE == 0) x[k] = xk;
-    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) x[i] -= A[i * n + k] * xk;
+    float lik = LANE > k && LANE < n ? A[LANE * n + k] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[k * n + k];
+    if (LANE == k) xi = v;
+    xi -= lik * v;
   }
   for (int k = n - 1; k >= 0; k--) {
-    SYNC();
-    float xk = x[k] / A[k * n + k];
-    SYNC();
-    if (LANE == 0) x[k] = xk;
-    for (int i = LANE; i < k; i += DX_WAVE) x[i] -= A[k * n + i] * xk;
+    float lki = LANE < k ? A[k * n + LANE] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[k * n + k];
+    if (LANE == k) xi = v;
+    xi -= lki * v;
   }
+  SYNC();
+  if (LANE < n) x[LANE] = xi;
   SYNC();
 }
 
@@ -637,17 +685,218 @@ __device__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, fl
   }
 }
 
-struct LocalContacts {
-  int n;
-  float pos[4][3];
-  float nrm[3];
-  float dist[4];
-};
+// Wave-cooperative support point: every lane runs the same (uniform) MPR control
+// flow; for mesh hulls the 64 lanes scan the vertices (staged in LDS) and an
+// argmax reduction picks the first maximal vertex, as the serial loop would.
+__device__ void support_wave(const Shape& s, const float* dir, float* out) {
+  float ld[3];
+  mattvec3(ld, s.mat, dir);
+  float lp[3] = {0, 0, 0};
+  if (s.type == DXG_MESH) {
+    float best = -3.0e38f;
+    int bi = 0x7fffffff;
+    for (int i = LANE; i < s.nvert; i += DX_WAVE) {
+      const float* v = s.vert + 3 * i;
+      float d = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
+      if (d > best) { best = d; bi = i; }
+    }
+    bi = wave_argmax_first(best, bi);
+    lp[0] = s.vert[3 * bi]; lp[1] = s.vert[3 * bi + 1]; lp[2] = s.vert[3 * bi + 2];
+  } else if (s.type == DXG_BOX) {
+    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= 0 ? s.size[k] : -s.size[k];
+  } else if (s.type == DXG_SPHERE || s.type == DXG_CAPSULE) {
+    float n = norm3(ld);
+    if (n > 1e-20f) { float sc = s.size[0] / n; lp[0] = ld[0] * sc; lp[1] = ld[1] * sc; lp[2] = ld[2] * sc; }
+    if (s.type == DXG_CAPSULE) lp[2] += ld[2] >= 0 ? s.size[1] : -s.size[1];
+  }
+  matvec3(out, s.mat, lp);
+  out[0] += s.pos[0]; out[1] += s.pos[1]; out[2] += s.pos[2];
+  if (s.margin > 0) {
+    float n = norm3(dir);
+    if (n > 1e-20f) {
+      float sc = s.margin / n;
+      out[0] += dir[0] * sc; out[1] += dir[1] * sc; out[2] += dir[2] * sc;
+    }
+  }
+}
 
-// Runs the narrowphase of geom pair gp; returns up to 4 contacts (shared normal).
-__device__ void narrowphase(const Ctx& c, int gp, LocalContacts& lc) {
+__device__ __forceinline__ void mpr_support_wave(const Shape& A, const Shape& B, const float* dir, MPoint& p) {
+  float nd[3] = {-dir[0], -dir[1], -dir[2]};
+  support_wave(A, dir, p.a);
+  support_wave(B, nd, p.b);
+  sub3(p.v, p.a, p.b);
+}
+
+// MPR penetration on A - B with wave-parallel support (see oracle mpr_penetration).
+__device__ bool mpr_wave(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+  const float tol = 1e-6f;
+  const int maxit = 50;
+  MPoint P[4];
+  sub3(P[0].v, A.center, B.center);
+  for (int k = 0; k < 3; k++) { P[0].a[k] = A.center[k]; P[0].b[k] = B.center[k]; }
+  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-9f;
+  float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+  normalize3(dir);
+  mpr_support_wave(A, B, dir, P[1]);
+  float dt = dot3(P[1].v, dir);
+  if (fzero(dt) || dt < 0) return false;
+  cross3(dir, P[0].v, P[1].v);
+  if (fzero(dot3(dir, dir))) {
+    if (fzero(P[1].v[0]) && fzero(P[1].v[1]) && fzero(P[1].v[2])) {
+      depth = 0;
+      normal[0] = 0; normal[1] = 0; normal[2] = 1;
+    } else {
+      depth = norm3(P[1].v);
+      for (int k = 0; k < 3; k++) normal[k] = P[1].v[k];
+      normalize3(normal);
+    }
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P[1].a[k] + P[1].b[k]);
+    return true;
+  }
+  normalize3(dir);
+  mpr_support_wave(A, B, dir, P[2]);
+  dt = dot3(P[2].v, dir);
+  if (fzero(dt) || dt < 0) return false;
+  float va[3], vb[3];
+  sub3(va, P[1].v, P[0].v);
+  sub3(vb, P[2].v, P[0].v);
+  cross3(dir, va, vb);
+  normalize3(dir);
+  if (dot3(dir, P[0].v) > 0) {
+    MPoint t = P[1]; P[1] = P[2]; P[2] = t;
+    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+  }
+  for (int it = 0;; it++) {
+    if (it > 1000) return false;
+    mpr_support_wave(A, B, dir, P[3]);
+    dt = dot3(P[3].v, dir);
+    if (fzero(dt) || dt < 0) return false;
+    bool cont = false;
+    cross3(va, P[1].v, P[3].v);
+    dt = dot3(va, P[0].v);
+    if (dt < 0 && !fzero(dt)) { P[2] = P[3]; cont = true; }
+    if (!cont) {
+      cross3(va, P[3].v, P[2].v);
+      dt = dot3(va, P[0].v);
+      if (dt < 0 && !fzero(dt)) { P[1] = P[3]; cont = true; }
+    }
+    if (!cont) break;
+    sub3(va, P[1].v, P[0].v);
+    sub3(vb, P[2].v, P[0].v);
+    cross3(dir, va, vb);
+    normalize3(dir);
+  }
+  for (int it = 0;; it++) {
+    portal_dir(P, dir);
+    if (dot3(dir, P[1].v) >= 0) break;
+    MPoint v4;
+    mpr_support_wave(A, B, dir, v4);
+    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P, v4, dir, tol) || it > maxit) return false;
+    expand_portal(P, v4);
+  }
+  for (int it = 0;; it++) {
+    portal_dir(P, dir);
+    MPoint v4;
+    mpr_support_wave(A, B, dir, v4);
+    if (portal_reach_tol(P, v4, dir, tol) || it > maxit) {
+      float cl[3];
+      float d2 = tri_origin_dist2(P[1].v, P[2].v, P[3].v, cl);
+      depth = sqrtf(d2);
+      if (depth > 1e-20f) {
+        float s = 1.0f / depth;
+        normal[0] = cl[0] * s; normal[1] = cl[1] * s; normal[2] = cl[2] * s;
+      } else {
+        normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
+      }
+      find_pos(P, pos);
+      return true;
+    }
+    expand_portal(P, v4);
+  }
+}
+
+__device__ __forceinline__ bool sphere_overlap(const float* c1, float r1, const float* c2, float r2, float margin) {
+  float t[3];
+  sub3(t, c1, c2);
+  float rr = r1 + r2 + margin;
+  return dot3(t, t) <= rr * rr;
+}
+
+// Separating-axis test of two oriented boxes (Gottschalk's 15 axes), inflated by margin.
+// obb: [centre(3) in body frame, R(9) body<-box, half extents(3)].
+__device__ bool obb_overlap(const float* o1, const float* xp1, const float* xm1, const float* o2,
+                            const float* xp2, const float* xm2, float margin) {
+  float ca[3], cb[3], Ra[9], Rb[9];
+  matvec3(ca, xm1, o1);
+  matvec3(cb, xm2, o2);
+  for (int k = 0; k < 3; k++) { ca[k] += xp1[k]; cb[k] += xp2[k]; }
+  matmul3(Ra, xm1, o1 + 3);
+  matmul3(Rb, xm2, o2 + 3);
+  const float* ea = o1 + 12;
+  const float* eb = o2 + 12;
+  float t0[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+  float t[3], R[9], AR[9];
+  // t in a's frame, R = Ra^T Rb
+  for (int i = 0; i < 3; i++) {
+    t[i] = Ra[i] * t0[0] + Ra[3 + i] * t0[1] + Ra[6 + i] * t0[2];
+    for (int j = 0; j < 3; j++) {
+      R[3 * i + j] = Ra[i] * Rb[j] + Ra[3 + i] * Rb[3 + j] + Ra[6 + i] * Rb[6 + j];
+      AR[3 * i + j] = fabsf(R[3 * i + j]) + 1e-6f;
+    }
+  }
+  for (int i = 0; i < 3; i++) {
+    float rb = eb[0] * AR[3 * i] + eb[1] * AR[3 * i + 1] + eb[2] * AR[3 * i + 2];
+    if (fabsf(t[i]) > ea[i] + rb + margin) return false;
+  }
+  for (int j = 0; j < 3; j++) {
+    float ra = ea[0] * AR[j] + ea[1] * AR[3 + j] + ea[2] * AR[6 + j];
+    float tj = t[0] * R[j] + t[1] * R[3 + j] + t[2] * R[6 + j];
+    if (fabsf(tj) > ra + eb[j] + margin) return false;
+  }
+  for (int i = 0; i < 3; i++) {
+    int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    for (int j = 0; j < 3; j++) {
+      int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      float ra = ea[i1] * AR[3 * i2 + j] + ea[i2] * AR[3 * i1 + j];
+      float rb = eb[j1] * AR[3 * i + j2] + eb[j2] * AR[3 * i + j1];
+      float tt = t[i2] * R[3 * i1 + j] - t[i1] * R[3 * i2 + j];
+      if (fabsf(tt) > ra + rb + margin) return false;
+    }
+  }
+  return true;
+}
+
+// Appends one contact record (called by a single lane).
+__device__ void write_contact(float* con, int slot, const float* pos, const float* n, float dist, int gp) {
+  float* r = con + DX_CON_STRIDE * slot;
+  r[0] = pos[0]; r[1] = pos[1]; r[2] = pos[2];
+  // frame: normal, tangent ([3P] mju_makeFrame)
+  float y[3];
+  if (fabsf(n[1]) < 0.5f) { y[0] = 0; y[1] = 1; y[2] = 0; }
+  else { y[0] = 0; y[1] = 0; y[2] = 1; }
+  float t = n[0] * y[0] + n[1] * y[1] + n[2] * y[2];
+  y[0] -= t * n[0]; y[1] -= t * n[1]; y[2] -= t * n[2];
+  normalize3(y);
+  float z[3];
+  cross3(z, n, y);
+  r[3] = n[0]; r[4] = n[1]; r[5] = n[2];
+  r[6] = y[0]; r[7] = y[1]; r[8] = y[2];
+  r[9] = z[0]; r[10] = z[1]; r[11] = z[2];
+  r[12] = dist;
+  r[13] = __int_as_float(gp);
+}
+
+// Copies a mesh hull's vertices into LDS staging (returns the LDS pointer or the
+// global one when it does not fit).
+__device__ const float* stage_hull(const float* src, int nvert, float* dst, int cap) {
+  if (3 * nvert > cap) return src;
+  for (int k = LANE; k < 3 * nvert; k += DX_WAVE) dst[k] = src[k];
+  return dst;
+}
+
+// Narrowphase of one geom pair by the whole wave; appends up to 4 contacts.
+__device__ int narrowphase_wave(const Ctx& c, int gp, float* con, int ncon) {
   const DevModel& m = c.m;
-  lc.n = 0;
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   float margin = m.gpair_margin[gp];
@@ -655,7 +904,6 @@ __device__ void narrowphase(const Ctx& c, int gp, LocalContacts& lc) {
     float pp[3], pm[9];
     geom_pose(c, g1, pp, pm);
     float n[3] = {pm[2], pm[5], pm[8]};
-    lc.nrm[0] = n[0]; lc.nrm[1] = n[1]; lc.nrm[2] = n[2];
     if (t2 == DXG_BOX) {
       float bp[3], bm[9];
       geom_pose(c, g2, bp, bm);
@@ -665,35 +913,44 @@ __device__ void narrowphase(const Ctx& c, int gp, LocalContacts& lc) {
       float cdist = dot3(rel, n);
       float ext = 0;
       for (int k = 0; k < 3; k++) ext += fabsf(bm[k] * n[0] + bm[3 + k] * n[1] + bm[6 + k] * n[2]) * sz[k];
-      if (cdist > margin + ext) return;
-      for (int i = 0; i < 8 && lc.n < 4; i++) {
+      if (cdist > margin + ext) return ncon;
+      // corners i = 0..7 on lanes 0..7; keep the first 4 (in corner order) within the margin
+      bool hit = false;
+      float v[3], dist = 0;
+      if (LANE < 8) {
+        int i = LANE;
         float s0 = (i & 1) ? sz[0] : -sz[0], s1 = (i & 2) ? sz[1] : -sz[1], s2 = (i & 4) ? sz[2] : -sz[2];
-        float v[3];
         for (int k = 0; k < 3; k++) v[k] = bp[k] + bm[3 * k] * s0 + bm[3 * k + 1] * s1 + bm[3 * k + 2] * s2;
         float r[3];
         sub3(r, v, pp);
-        float dist = dot3(r, n);
-        if (dist <= margin) {
-          for (int k = 0; k < 3; k++) lc.pos[lc.n][k] = v[k] - 0.5f * dist * n[k];
-          lc.dist[lc.n] = dist;
-          lc.n++;
-        }
+        dist = dot3(r, n);
+        hit = dist <= margin;
       }
-    } else {
-      Shape s;
-      make_shape(c, g2, 0, s);
-      float nd[3] = {-n[0], -n[1], -n[2]};
-      float sp[3];
-      support(s, nd, sp);
-      float r[3];
-      sub3(r, sp, pp);
-      float dist = dot3(r, n);
-      if (dist > margin) return;
-      for (int k = 0; k < 3; k++) lc.pos[0][k] = sp[k] - 0.5f * dist * n[k];
-      lc.dist[0] = dist;
-      lc.n = 1;
+      uint64_t mask = __ballot(hit);
+      int rank = __popcll(mask & ((1ull << LANE) - 1ull));
+      if (hit && rank < 4 && ncon + rank < DX_NCON_MAX) {
+        float pos[3] = {v[0] - 0.5f * dist * n[0], v[1] - 0.5f * dist * n[1], v[2] - 0.5f * dist * n[2]};
+        write_contact(con, ncon + rank, pos, n, dist, gp);
+      }
+      return ncon + min(4, __popcll(mask));
     }
-    return;
+    Shape s;
+    make_shape(c, g2, 0, s);
+    if (s.type == DXG_MESH) s.vert = stage_hull(s.vert, s.nvert, c.f(c.L.cj_val), 3 * DX_NCON_MAX * DX_DOFMAX);
+    SYNC();
+    float nd[3] = {-n[0], -n[1], -n[2]};
+    float sp[3];
+    support_wave(s, nd, sp);
+    SYNC();
+    float r[3];
+    sub3(r, sp, pp);
+    float dist = dot3(r, n);
+    if (dist > margin) return ncon;
+    if (LANE == 0 && ncon < DX_NCON_MAX) {
+      float pos[3] = {sp[0] - 0.5f * dist * n[0], sp[1] - 0.5f * dist * n[1], sp[2] - 0.5f * dist * n[2]};
+      write_contact(con, ncon, pos, n, dist, gp);
+    }
+    return ncon + 1;
   }
   if (t1 == DXG_CAPSULE && t2 == DXG_CAPSULE) {
     float p1[3], m1[9], p2[3], m2[9];
@@ -721,34 +978,39 @@ __device__ void narrowphase(const Ctx& c, int gp, LocalContacts& lc) {
     sub3(diff, q2, q1);
     float len = norm3(diff);
     float dist = len - r1 - r2;
-    if (dist > margin) return;
-    if (len > 1e-20f) { lc.nrm[0] = diff[0] / len; lc.nrm[1] = diff[1] / len; lc.nrm[2] = diff[2] / len; }
-    else { lc.nrm[0] = 1; lc.nrm[1] = 0; lc.nrm[2] = 0; }
-    for (int k = 0; k < 3; k++) lc.pos[0][k] = q1[k] + lc.nrm[k] * (r1 + 0.5f * dist);
-    lc.dist[0] = dist;
-    lc.n = 1;
-    return;
+    if (dist > margin) return ncon;
+    float n[3];
+    if (len > 1e-20f) { n[0] = diff[0] / len; n[1] = diff[1] / len; n[2] = diff[2] / len; }
+    else { n[0] = 1; n[1] = 0; n[2] = 0; }
+    if (LANE == 0 && ncon < DX_NCON_MAX) {
+      float pos[3];
+      for (int k = 0; k < 3; k++) pos[k] = q1[k] + n[k] * (r1 + 0.5f * dist);
+      write_contact(con, ncon, pos, n, dist, gp);
+    }
+    return ncon + 1;
   }
   Shape A, B;
   make_shape(c, g1, 0.5f * margin, A);
   make_shape(c, g2, 0.5f * margin, B);
+  float* stg = c.f(c.L.cj_val);
+  int cap = 3 * DX_NCON_MAX * DX_DOFMAX;
+  int used = 0;
+  if (A.type == DXG_MESH && 3 * A.nvert <= cap) { A.vert = stage_hull(A.vert, A.nvert, stg, cap); used = 3 * A.nvert; }
+  if (B.type == DXG_MESH) B.vert = stage_hull(B.vert, B.nvert, stg + used, cap - used);
+  SYNC();
   float depth, nrm[3], pos[3];
-  if (mpr_penetration(A, B, depth, nrm, pos)) {
-    lc.nrm[0] = nrm[0]; lc.nrm[1] = nrm[1]; lc.nrm[2] = nrm[2];
-    lc.pos[0][0] = pos[0]; lc.pos[0][1] = pos[1]; lc.pos[0][2] = pos[2];
-    lc.dist[0] = margin - depth;
-    lc.n = 1;
+  int out = ncon;
+  if (mpr_wave(A, B, depth, nrm, pos)) {
+    if (LANE == 0 && ncon < DX_NCON_MAX) write_contact(con, ncon, pos, nrm, margin - depth, gp);
+    out = ncon + 1;
   }
+  SYNC();
+  return out;
 }
 
-__device__ __forceinline__ bool sphere_overlap(const float* c1, float r1, const float* c2, float r2, float margin) {
-  float t[3];
-  sub3(t, c1, c2);
-  float rr = r1 + r2 + margin;
-  return dot3(t, t) <= rr * rr;
-}
-
-// broadphase + mid-phase + narrowphase; writes contact records into LDS.
+// broadphase (body spheres, lanes over body pairs) -> flattened mid-phase (geom
+// spheres, lanes over every geom pair of the surviving body pairs) -> narrowphase
+// (whole wave per pair).  Writes contact records into LDS.
 // watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
 __device__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
   const DevModel& m = c.m;
@@ -760,125 +1022,125 @@ __device__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
   if (m.disable_contact) return;
   float* xpos = c.f(c.L.xpos);
   float* xmat = c.f(c.L.xmat);
-  // body-pair cull, compacted into cand[] (body-pair indices); then expand to geom pairs
-  int nbc = 0;
+  // 1. body-pair cull -> cand[0..nbc) body-pair ids, pref[0..nbc] prefix of geom-pair counts
+  int half = cmax / 3;
+  int* pref = cand + half;
+  int nbc = 0, ngp = 0;
   for (int base = 0; base < m.nbpair; base += DX_WAVE) {
     int bp = base + LANE;
     bool keep = false;
+    int cnt = 0;
     if (bp < m.nbpair) {
       int b1 = m.bpair_body[2 * bp], b2 = m.bpair_body[2 * bp + 1];
       keep = true;
       if (watch_only) keep = (b2 == wb || b1 == wb) && (m.geom_bodyid[wg] == b1 || m.geom_bodyid[wg] == b2);
-      const float* s1 = m.body_bsphere + 4 * b1;
-      const float* s2 = m.body_bsphere + 4 * b2;
-      if (keep && s1[3] >= 0 && s2[3] >= 0) {
-        float c1[3], c2[3];
-        matvec3(c1, xmat + 9 * b1, s1);
+      const float* s1 = m.bpair_sphere + 8 * bp;
+      const float* s2 = s1 + 4;
+      float mg = m.gpair_margin[m.bpair_adr[bp]];
+      if (keep && s2[3] >= 0) {
+        float c2[3];
         matvec3(c2, xmat + 9 * b2, s2);
-        for (int k = 0; k < 3; k++) { c1[k] += xpos[3 * b1 + k]; c2[k] += xpos[3 * b2 + k]; }
-        float mg = m.gpair_margin[m.bpair_adr[bp]];
-        keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+        for (int k = 0; k < 3; k++) c2[k] += xpos[3 * b2 + k];
+        int pg = m.bpair_plane[bp];
+        if (pg >= 0) {
+          float pp[3], pm[9];
+          geom_pose(c, pg, pp, pm);
+          float r[3] = {c2[0] - pp[0], c2[1] - pp[1], c2[2] - pp[2]};
+          keep = r[0] * pm[2] + r[1] * pm[5] + r[2] * pm[8] <= s2[3] + mg;
+        } else if (s1[3] >= 0) {
+          float c1[3];
+          matvec3(c1, xmat + 9 * b1, s1);
+          for (int k = 0; k < 3; k++) c1[k] += xpos[3 * b1 + k];
+          keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+        }
+      }
+      cnt = keep ? m.bpair_num[bp] : 0;
+    }
+    uint64_t mask = __ballot(keep);
+    int pos = __popcll(mask & ((1ull << LANE) - 1ull));
+    int off = wave_excl_scan(cnt);
+    if (keep && nbc + pos < half) {
+      cand[nbc + pos] = bp;
+      pref[nbc + pos] = ngp + off;
+    }
+    nbc += __popcll(mask);
+    ngp += wave_sum_i(cnt);
+  }
+  if (nbc > half) { nbc = half; if (LANE == 0) I[I_OVF] |= 1; }
+  if (LANE == 0) pref[nbc] = ngp;
+  SYNC();
+  stage_mark(c, ST_BROAD);
+  // 2. flattened geom-pair mid-phase: lane t -> (body pair q, geom pair) by binary search
+  int* gcand = pref + half;
+  int gmax = cmax - 2 * half;
+  int ng = 0;
+  int total = nbc > 0 ? pref[nbc] : 0;
+  for (int base = 0; base < total; base += DX_WAVE) {
+    int t = base + LANE;
+    bool keep = false;
+    int gp = -1;
+    if (t < total) {
+      int lo = 0, hi = nbc;  // pref[lo] <= t < pref[hi]
+      while (hi - lo > 1) {
+        int mid = (lo + hi) >> 1;
+        if (pref[mid] <= t) lo = mid; else hi = mid;
+      }
+      gp = m.bpair_adr[cand[lo]] + (t - pref[lo]);
+      int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+      keep = !watch_only || g1 == wg || g2 == wg;
+      if (keep) {
+        float mg = m.gpair_margin[gp];
+        int b2 = m.geom_bodyid[g2];
+        const float* s2 = m.geom_bsphere_b + 4 * g2;
+        float c2[3];
+        matvec3(c2, xmat + 9 * b2, s2);
+        for (int k = 0; k < 3; k++) c2[k] += xpos[3 * b2 + k];
+        int b1 = m.geom_bodyid[g1];
+        if (m.geom_type[g1] == DXG_PLANE) {
+          float p1[3], m1[9];
+          geom_pose(c, g1, p1, m1);
+          float n[3] = {m1[2], m1[5], m1[8]}, r[3];
+          sub3(r, c2, p1);
+          keep = dot3(r, n) <= s2[3] + mg;
+        } else {
+          const float* s1 = m.geom_bsphere_b + 4 * g1;
+          float c1[3];
+          matvec3(c1, xmat + 9 * b1, s1);
+          for (int k = 0; k < 3; k++) c1[k] += xpos[3 * b1 + k];
+          keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+          if (keep)
+            keep = obb_overlap(m.geom_obb_b + 15 * g1, xpos + 3 * b1, xmat + 9 * b1, m.geom_obb_b + 15 * g2,
+                               xpos + 3 * b2, xmat + 9 * b2, mg);
+        }
       }
     }
     uint64_t mask = __ballot(keep);
     int pos = __popcll(mask & ((1ull << LANE) - 1ull));
-    if (keep && nbc + pos < cmax) cand[nbc + pos] = bp;
-    nbc += __popcll(mask);
-  }
-  nbc = min(nbc, cmax);
-  SYNC();
-  // geom-pair mid-phase: serial over surviving body pairs, lanes over geom pairs.
-  // Store survivors after the body-pair list (cand[nbc..]).
-  int* gcand = cand + nbc;
-  int gmax = cmax - nbc;
-  int ng = 0;
-  for (int q = 0; q < nbc; q++) {
-    int bp = cand[q];
-    int a0 = m.bpair_adr[bp], n0 = m.bpair_num[bp];
-    for (int base = 0; base < n0; base += DX_WAVE) {
-      int gp = a0 + base + LANE;
-      bool keep = false;
-      if (base + LANE < n0) {
-        int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
-        keep = !watch_only || g1 == wg || g2 == wg;
-        if (keep) {
-          float mg = m.gpair_margin[gp];
-          float p2[3], m2[9];
-          geom_pose(c, g2, p2, m2);
-          const float* s2 = m.geom_bsphere + 4 * g2;
-          float c2[3];
-          matvec3(c2, m2, s2);
-          for (int k = 0; k < 3; k++) c2[k] += p2[k];
-          if (m.geom_type[g1] == DXG_PLANE) {
-            float p1[3], m1[9];
-            geom_pose(c, g1, p1, m1);
-            float n[3] = {m1[2], m1[5], m1[8]}, r[3];
-            sub3(r, c2, p1);
-            keep = dot3(r, n) <= s2[3] + mg;
-          } else {
-            float p1[3], m1[9];
-            geom_pose(c, g1, p1, m1);
-            const float* s1 = m.geom_bsphere + 4 * g1;
-            float c1[3];
-            matvec3(c1, m1, s1);
-            for (int k = 0; k < 3; k++) c1[k] += p1[k];
-            keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
-          }
-        }
-      }
-      uint64_t mask = __ballot(keep);
-      int pos = __popcll(mask & ((1ull << LANE) - 1ull));
-      if (keep && ng + pos < gmax) gcand[ng + pos] = gp;
-      ng += __popcll(mask);
-    }
+    if (keep && ng + pos < gmax) gcand[ng + pos] = gp;
+    ng += __popcll(mask);
   }
   if (ng > gmax) {
     if (LANE == 0) I[I_OVF] |= 1;
     ng = gmax;
   }
+  if (LANE == 0) I[I_NCAND] = ng;
   SYNC();
-  // narrowphase: one geom pair per lane; deterministic lane-ordered append.
+  stage_mark(c, ST_MID);
+  // 3. narrowphase: whole wave per candidate, in candidate order (deterministic)
   float* con = c.f(c.L.con);
   int ncon = 0;
-  for (int base = 0; base < ng; base += DX_WAVE) {
-    LocalContacts lc;
-    lc.n = 0;
-    int gp = -1;
-    if (base + LANE < ng) {
-      gp = gcand[base + LANE];
-      narrowphase(c, gp, lc);
-    }
-    int off = wave_excl_scan(lc.n);
-    int tot = wave_sum_i(lc.n);
-    for (int k = 0; k < lc.n; k++) {
-      int slot = ncon + off + k;
-      if (slot >= DX_NCON_MAX) break;
-      float* r = con + DX_CON_STRIDE * slot;
-      r[0] = lc.pos[k][0]; r[1] = lc.pos[k][1]; r[2] = lc.pos[k][2];
-      // frame: normal, tangent ([3P] mju_makeFrame)
-      float nx = lc.nrm[0], ny = lc.nrm[1], nz = lc.nrm[2];
-      float y[3];
-      if (fabsf(ny) < 0.5f) { y[0] = 0; y[1] = 1; y[2] = 0; }
-      else { y[0] = 0; y[1] = 0; y[2] = 1; }
-      float t = nx * y[0] + ny * y[1] + nz * y[2];
-      y[0] -= t * nx; y[1] -= t * ny; y[2] -= t * nz;
-      normalize3(y);
-      float nn[3] = {nx, ny, nz}, z[3];
-      cross3(z, nn, y);
-      r[3] = nx; r[4] = ny; r[5] = nz;
-      r[6] = y[0]; r[7] = y[1]; r[8] = y[2];
-      r[9] = z[0]; r[10] = z[1]; r[11] = z[2];
-      r[12] = lc.dist[k];
-      r[13] = __int_as_float(gp);
-    }
-    ncon += tot;
+  for (int q = 0; q < ng; q++) {
+    int gp = __builtin_amdgcn_readfirstlane(gcand[q]);
+    ncon = narrowphase_wave(c, gp, con, ncon);
   }
   if (ncon > DX_NCON_MAX) {
     if (LANE == 0) I[I_OVF] |= 2;
     ncon = DX_NCON_MAX;
   }
+  SYNC();
   if (LANE == 0) I[I_NCON] = ncon;
   SYNC();
+  stage_mark(c, ST_NARROW);
 }
 
 // ------------------------------------------------------------------------ //
@@ -1469,7 +1731,13 @@ __device__ void build_hessian(const Ctx& c) {
   }
 }
 
-__device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir) {
+// zone of a row's cost at jar: 0 zero, 1 quadratic, 2 / 3 linear friction zones
+__device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
+  if (type == DXR_FRIC) return jar <= -Rf ? 3 : (jar >= Rf ? 2 : 1);
+  return jar < 0 ? 1 : 0;
+}
+
+__device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float* Mdir = c.f(c.L.v4);
@@ -1509,6 +1777,13 @@ __device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, c
     if (fabsf(next - alpha) <= 1e-7f * fabsf(alpha)) break;
     alpha = next;
   }
+  // rows whose cost zone differs between the current point and the new one
+  int ch = 0;
+  for (int r = LANE; r < nefc; r += DX_WAVE) {
+    int type = meta[r] & 15;
+    ch += row_zone(type, Rf[r], jar[r]) != row_zone(type, Rf[r], jar[r] + alpha * jv[r]);
+  }
+  *changed = wave_sum_i(ch);
   return alpha;
 }
 
@@ -1545,6 +1820,7 @@ __device__ void solve(const Ctx& c) {
     cost = eval_cost(c, qacc, Ma);
   }
   int it = 0;
+  stage_mark(c, ST_NEWTON_EVAL);
   for (; it < m.iterations; it++) {
     jac_t_force(c, grad);  // grad <- J^T f
     float gn = 0;
@@ -1553,20 +1829,33 @@ __device__ void solve(const Ctx& c) {
       gn += grad[i] * grad[i];
     }
     gn = sqrtf(wave_sum(gn)) * scale;
+    stage_mark(c, ST_NEWTON_GRAD);
     if (gn < tol) break;
     build_hessian(c);
+    stage_mark(c, ST_NEWTON_HESS);
     float* H = c.f(c.L.H);
-    wave_cholesky(H, nv);
+    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
     for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
     SYNC();
     wave_chol_solve(H, dir, nv);
-    float alpha = line_search(c, qacc, Ma, dir);
+    stage_mark(c, ST_NEWTON_CHOL);
+    int changed = 0;
+    float alpha = line_search(c, qacc, Ma, dir, &changed);
+    stage_mark(c, ST_NEWTON_LS);
     for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] += alpha * dir[i];
     SYNC();
     float nc = eval_cost(c, qacc, Ma);
+    stage_mark(c, ST_NEWTON_EVAL);
     float impr = scale * (cost - nc);
+    float prev = cost;
     cost = nc;
-    if (impr < tol) { it++; break; }
+    // Converged when (a) the full Newton step kept every row in its cost zone: the
+    // cost is quadratic on that zone set, so the step landed on its exact minimiser;
+    // or (b) the improvement is below the tolerance or at fp32 noise level of the cost.
+    if ((changed == 0 && fabsf(alpha - 1.0f) < 1e-3f) || impr < tol || (prev - nc) <= 2e-6f * fabsf(prev)) {
+      it++;
+      break;
+    }
   }
   if (LANE == 0) c.I[I_NITER] = it;
   SYNC();
@@ -1578,10 +1867,13 @@ __device__ void solve(const Ctx& c) {
 __device__ void position_stage(const Ctx& c) {
   kinematics(c);
   com_pos(c);
+  stage_mark(c, ST_KIN);
   tendon_lengths(c);
   crb_mass(c);
+  stage_mark(c, ST_CRB);
   collision(c, 0, -1, -1);
   make_constraint(c);
+  stage_mark(c, ST_CON);
 }
 
 __device__ void forward(const Ctx& c, const float* xfrc) {
@@ -1589,6 +1881,7 @@ __device__ void forward(const Ctx& c, const float* xfrc) {
   int nv = m.nv;
   position_stage(c);
   velocity_stage(c, xfrc);
+  stage_mark(c, ST_VEL);
   // qacc_smooth = M^-1 qfrc_smooth via Cholesky in H
   float* H = c.f(c.L.H);
   const float* M = c.f(c.L.M);
@@ -1597,8 +1890,9 @@ __device__ void forward(const Ctx& c, const float* xfrc) {
   const float* qs = c.f(c.L.qfrc_smooth);
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
   SYNC();
-  wave_cholesky(H, nv);
+  wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
   wave_chol_solve(H, a0, nv);
+  stage_mark(c, ST_SMOOTH);
   solve(c);
   // qfrc_constraint = J^T f at the solution
   float* qc = c.f(c.L.qfrc_con);
@@ -1608,6 +1902,7 @@ __device__ void forward(const Ctx& c, const float* xfrc) {
     for (int i = LANE; i < nv; i += DX_WAVE) qc[i] = 0;
     SYNC();
   }
+  stage_mark(c, ST_QFRC);
 }
 
 __device__ void euler(const Ctx& c, float* time) {
@@ -1628,7 +1923,7 @@ __device__ void euler(const Ctx& c, float* time) {
       acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
     }
     SYNC();
-    wave_cholesky(H, nv);
+    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
     wave_chol_solve(H, acc, nv);
   } else {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
@@ -1656,6 +1951,7 @@ __device__ void euler(const Ctx& c, float* time) {
   }
   if (LANE == 0) *time += h;
   SYNC();
+  stage_mark(c, ST_EULER);
 }
 
 // observation pass at the new state: kinematics, com, velocities, sites, watch contact
@@ -1719,7 +2015,8 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
   int env = blockIdx.x;
   if (env >= B.nenv) return;
   int* I = (int*)(smem + L.ints);
-  Ctx c{m, L, smem, I};
+  Ctx c{m, L, smem, I, B.stage_acc};
+  if (B.stage_acc && LANE == 0) *(unsigned long long*)(I + 10) = __builtin_amdgcn_s_memtime();
   float* qpos = c.f(L.qpos);
   float* qvel = c.f(L.qvel);
   float* ctrl = c.f(L.ctrl);
@@ -1731,6 +2028,17 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
   }
   for (int i = LANE; i < m.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * m.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
+  {
+    // lower-triangle index table for wave_cholesky: t -> (i << 8 | j), row-major
+    unsigned short* tri = (unsigned short*)c.f(L.tri);
+    int T = m.nv * (m.nv + 1) / 2;
+    for (int t = LANE; t < T; t += DX_WAVE) {
+      int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+      while ((i + 1) * (i + 2) / 2 <= t) i++;
+      while (i * (i + 1) / 2 > t) i--;
+      tri[t] = (unsigned short)((i << 8) | (t - i * (i + 1) / 2));
+    }
+  }
   float time = B.time[env];
   SYNC();
   int steps = mode == 0 ? nsub : 1;
@@ -1770,10 +2078,13 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
   if (LANE == 0) {
     B.ncon[env] = I[I_NCON];
     B.niter[env] = I[I_NITER];
+    B.ncand[env] = I[I_NCAND];
   }
   for (int i = LANE; i < m.nv; i += DX_WAVE) B.qacc[(size_t)env * m.nv + i] = c.f(L.qacc)[i];
   SYNC();
+  stage_mark(c, ST_IO);
   observe(c, B, env);
+  stage_mark(c, ST_OBSERVE);
   for (int i = LANE; i < m.nq; i += DX_WAVE) B.qpos[(size_t)env * m.nq + i] = qpos[i];
   for (int i = LANE; i < m.nv; i += DX_WAVE) {
     B.qvel[(size_t)env * m.nv + i] = qvel[i];

@@ -827,49 +827,90 @@ def _compile(scene: Scene) -> CompiledModel:
         t1, t2 = geoms[r["g1"]][1]["type"], geoms[r["g2"]][1]["type"]
         if t1 > t2:
             r["g1"], r["g2"] = r["g2"], r["g1"]
-    # Group geom pairs by body pair for the two-level broadphase.
+    # Body-frame point sets of every collision geom (hull vertices / box corners).
+    def geom_points(gi):
+        gb, g = geoms[gi]
+        if g["type"] == GEOM_PLANE:
+            return None
+        R = m3.quat_to_mat(g["quat"])
+        if g["type"] == GEOM_MESH:
+            P = hulls[geom_dataid[gi]].vert
+        else:
+            c, e = geom_aabb[gi][:3], geom_aabb[gi][3:]
+            P = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]) * e + c
+        return g["pos"] + (R @ P.T).T
+
+    gpts = [geom_points(gi) for gi in range(ngeom)]
+
+    def sphere_of(geom_ids):
+        if any(gpts[g] is None for g in geom_ids):
+            return np.array([0.0, 0.0, 0.0, -1.0])  # contains a plane: never sphere-culled
+        P = np.concatenate([gpts[g] for g in geom_ids])
+        c = (P.min(0) + P.max(0)) / 2
+        return np.concatenate([c, [np.max(np.linalg.norm(P - c, axis=1))]])
+
+    # Group geom pairs by body pair; a side with many geoms (the 145-piece Shadow
+    # palm) is split into spatial clusters of <= CLUSTER geoms, each becoming its own
+    # broadphase unit with a tight bounding sphere, so the broadphase culls whole
+    # clusters instead of the mid-phase testing every piece.
+    CLUSTER = 12
     by_bpair: Dict[tuple, list] = {}
     for idx, r in enumerate(pair_rows):
         b1, b2 = geoms[r["g1"]][0], geoms[r["g2"]][0]
         by_bpair.setdefault((b1, b2), []).append(idx)
-    bpair_list = sorted(by_bpair.keys())
-    gp_order = []
-    bpair_b = np.zeros((len(bpair_list), 2), np.int32)
-    bpair_adr = np.zeros(len(bpair_list), np.int32)
-    bpair_num = np.zeros(len(bpair_list), np.int32)
-    for k, bp in enumerate(bpair_list):
-        bpair_b[k] = bp
-        bpair_adr[k] = len(gp_order)
-        bpair_num[k] = len(by_bpair[bp])
-        gp_order.extend(by_bpair[bp])
-    pair_rows = [pair_rows[i] for i in gp_order]
 
-    # Body bounding spheres (body frame), over the collision geoms of each body.
-    body_bsphere = np.zeros((nbody, 4))  # center(3), radius; radius<0: never culled
-    body_bsphere[:, 3] = 0.0
+    def bisect(gs):
+        if len(gs) <= CLUSTER:
+            return [gs]
+        C = np.array([(gpts[g].min(0) + gpts[g].max(0)) / 2 for g in gs])
+        ax = int(np.argmax(C.max(0) - C.min(0)))
+        order = [gs[i] for i in np.argsort(C[:, ax], kind="stable")]
+        h = len(order) // 2
+        return bisect(order[:h]) + bisect(order[h:])
+
+    units = []  # (b1, b2, pair idxs, sphere1, sphere2, plane geom on side 1)
+    for (b1, b2) in sorted(by_bpair):
+        idxs = by_bpair[(b1, b2)]
+        G1 = sorted({pair_rows[i]["g1"] for i in idxs})
+        G2 = sorted({pair_rows[i]["g2"] for i in idxs})
+        plane = G1[0] if len(G1) == 1 and gpts[G1[0]] is None else -1
+        if len(G1) > CLUSTER and len(G1) >= len(G2) and plane < 0:
+            for cl in bisect(G1):
+                cs = set(cl)
+                sub = [i for i in idxs if pair_rows[i]["g1"] in cs]
+                units.append((b1, b2, sub, sphere_of(cl), sphere_of(sorted({pair_rows[i]["g2"] for i in sub})), plane))
+        elif len(G2) > CLUSTER:
+            for cl in bisect(G2):
+                cs = set(cl)
+                sub = [i for i in idxs if pair_rows[i]["g2"] in cs]
+                s1 = sphere_of(sorted({pair_rows[i]["g1"] for i in sub}))
+                units.append((b1, b2, sub, s1, sphere_of(cl), plane))
+        else:
+            units.append((b1, b2, idxs, sphere_of(G1), sphere_of(G2), plane))
+    gp_order = []
+    nbp = len(units)
+    bpair_b = np.zeros((nbp, 2), np.int32)
+    bpair_adr = np.zeros(nbp, np.int32)
+    bpair_num = np.zeros(nbp, np.int32)
+    bpair_sphere = np.zeros((nbp, 8))
+    bpair_plane = -np.ones(nbp, np.int32)
+    for k, (b1, b2, idxs, s1, s2, plane) in enumerate(units):
+        bpair_b[k] = (b1, b2)
+        bpair_adr[k] = len(gp_order)
+        bpair_num[k] = len(idxs)
+        bpair_sphere[k, :4] = s1
+        bpair_sphere[k, 4:] = s2
+        bpair_plane[k] = plane
+        gp_order.extend(idxs)
+    pair_rows = [pair_rows[i] for i in gp_order]
+    bpair_list = units
+
+    # Body bounding spheres (body frame) over each body's collision geoms.
+    body_bsphere = np.zeros((nbody, 4))
     for bi in range(nbody):
-        pts = []
-        for gi, (gb, g) in enumerate(geoms):
-            if gb != bi or (g["contype"] == 0 and g["conaffinity"] == 0):
-                continue
-            if g["type"] == GEOM_PLANE:
-                pts = None
-                break
-            if g["type"] == GEOM_MESH:
-                h = hulls[geom_dataid[gi]]
-                pts.append(g["pos"] + (m3.quat_to_mat(g["quat"]) @ h.vert.T).T)
-            else:
-                c = geom_aabb[gi][:3]
-                e = geom_aabb[gi][3:]
-                corners = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]) * e + c
-                pts.append(g["pos"] + (m3.quat_to_mat(g["quat"]) @ corners.T).T)
-        if pts is None:
-            body_bsphere[bi] = (0, 0, 0, -1.0)  # contains a plane: never culled
-            continue
-        if pts:
-            P = np.concatenate(pts)
-            c = (P.min(0) + P.max(0)) / 2
-            body_bsphere[bi] = np.concatenate([c, [np.max(np.linalg.norm(P - c, axis=1))]])
+        gs = [gi for gi in range(ngeom) if geoms[gi][0] == bi]
+        if gs:
+            body_bsphere[bi] = sphere_of(gs)
 
     # ---------------- assemble arrays ---------------- #
     A["nq"] = np.array([nq], np.int32)
@@ -978,6 +1019,8 @@ def _compile(scene: Scene) -> CompiledModel:
     A["actuator_forcelimited"] = np.array([int(a["forcelimited"]) for a in acts], np.int32)
     A["actuator_forcerange"] = np.array([a["forcerange"] for a in acts]).reshape(-1, 2)
 
+    A["bpair_sphere"] = bpair_sphere
+    A["bpair_plane"] = bpair_plane
     A["bpair_body"] = bpair_b
     A["bpair_adr"] = bpair_adr
     A["bpair_num"] = bpair_num

@@ -69,6 +69,7 @@ enum dx_field {
   DX_GROUND_CONTACT = 11, /* 1 (int32 bits): any contact involving geom
                            `ground_geom` with dist <= 1e-8 (reorient.py:229-235) */
   DX_NITER = 12,        /* 1  (int32 bits) solver iterations of the last substep */
+  DX_NCAND = 13,        /* 1  (int32 bits) narrowphase candidates of the last collision pass */
   DX_NFIELD
 };
 
@@ -167,6 +168,10 @@ int dx_env_pack_outputs(dx_env* e, float* dst_dev);
  * dx_timing_read syncs, returns the summed kernel time and launch count, and clears. */
 int dx_timing_enable(dx_batch* b, int enable);
 int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
+/* Per-stage shader-clock accounting inside the fused step kernel (diagnostics):
+ * out[k] = summed s_memtime cycles of stage k over all envs since the last read. */
+int dx_stage_timing(dx_batch* b, int enable);
+int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n);
 
 const char* dx_last_error(void);
 int dx_abi_version(void);

@@ -56,7 +56,7 @@ struct dxo_model {
   const double *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref, *dof_solimp,
       *dof_invweight0;
   const int *geom_type, *geom_bodyid, *geom_dataid;
-  const double *geom_size, *geom_pos, *geom_quat, *geom_center, *geom_bsphere;
+  const double *geom_size, *geom_pos, *geom_quat, *geom_center, *geom_bsphere, *geom_aabb;
   const int *mesh_vertadr, *mesh_vertnum;
   const double* mesh_vert;
   const int* site_bodyid;
@@ -68,7 +68,8 @@ struct dxo_model {
       *actuator_forcelimited;
   const double *actuator_gear, *actuator_gainprm, *actuator_biasprm, *actuator_ctrlrange,
       *actuator_forcerange;
-  const int *bpair_body, *bpair_adr, *bpair_num, *gpair_geom, *gpair_condim;
+  const int *bpair_body, *bpair_adr, *bpair_num, *bpair_plane, *gpair_geom, *gpair_condim;
+  const double* bpair_sphere;
   const double *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
 };
 
@@ -136,7 +137,7 @@ dxo_model* dxo_model_load(const void* blob, size_t nbytes) {
   GETD(dof_armature); GETD(dof_damping); GETD(dof_frictionloss); GETD(dof_solref);
   GETD(dof_solimp); GETD(dof_invweight0);
   GETI(geom_type); GETI(geom_bodyid); GETI(geom_dataid);
-  GETD(geom_size); GETD(geom_pos); GETD(geom_quat); GETD(geom_center); GETD(geom_bsphere);
+  GETD(geom_size); GETD(geom_pos); GETD(geom_quat); GETD(geom_center); GETD(geom_bsphere); GETD(geom_aabb);
   GETI(mesh_vertadr); GETI(mesh_vertnum); GETD(mesh_vert);
   GETI(site_bodyid); GETD(site_pos); GETD(site_quat);
   GETI(tendon_adr); GETI(tendon_num); GETI(tendon_limited); GETI(wrap_dof);
@@ -146,7 +147,8 @@ dxo_model* dxo_model_load(const void* blob, size_t nbytes) {
   GETI(actuator_ctrllimited); GETI(actuator_forcelimited);
   GETD(actuator_gear); GETD(actuator_gainprm); GETD(actuator_biasprm); GETD(actuator_ctrlrange);
   GETD(actuator_forcerange);
-  GETI(bpair_body); GETI(bpair_adr); GETI(bpair_num); GETI(gpair_geom); GETI(gpair_condim);
+  GETI(bpair_body); GETI(bpair_adr); GETI(bpair_num); GETI(bpair_plane); GETD(bpair_sphere);
+  GETI(gpair_geom); GETI(gpair_condim);
   GETD(gpair_friction); GETD(gpair_solref); GETD(gpair_solimp); GETD(gpair_margin);
   if (!ok) {
     dxo_model_free(m);
@@ -1125,6 +1127,47 @@ static void collide_capsules(const dxo_model* m, dxo_data* d, int gp, int g1, in
   add_contact(d, m, gp, g1, g2, pos, n, dist);
 }
 
+/* separating-axis test of the geoms' oriented bounding boxes (geom-frame AABBs);
+ * conservative, so it only removes pairs MPR would reject. */
+static int obb_overlap(const dxo_model* m, const dxo_data* d, int g1, int g2, double margin, double* fl) {
+  double ca[3], cb[3];
+  const double* a1 = m->geom_aabb + 6 * g1;
+  const double* a2 = m->geom_aabb + 6 * g2;
+  const double* Ra = d->geom_xmat + 9 * g1;
+  const double* Rb = d->geom_xmat + 9 * g2;
+  matvec3(ca, Ra, a1); add3(ca, ca, d->geom_xpos + 3 * g1);
+  matvec3(cb, Rb, a2); add3(cb, cb, d->geom_xpos + 3 * g2);
+  const double* ea = a1 + 3;
+  const double* eb = a2 + 3;
+  double t0[3], t[3], R[9], AR[9];
+  sub3(t0, cb, ca);
+  for (int i = 0; i < 3; i++) {
+    t[i] = Ra[i] * t0[0] + Ra[3 + i] * t0[1] + Ra[6 + i] * t0[2];
+    for (int j = 0; j < 3; j++) {
+      R[3 * i + j] = Ra[i] * Rb[j] + Ra[3 + i] * Rb[3 + j] + Ra[6 + i] * Rb[6 + j];
+      AR[3 * i + j] = fabs(R[3 * i + j]) + 1e-6;
+    }
+  }
+  *fl += 150;
+  for (int i = 0; i < 3; i++)
+    if (fabs(t[i]) > ea[i] + eb[0] * AR[3 * i] + eb[1] * AR[3 * i + 1] + eb[2] * AR[3 * i + 2] + margin) return 0;
+  for (int j = 0; j < 3; j++) {
+    double tj = t[0] * R[j] + t[1] * R[3 + j] + t[2] * R[6 + j];
+    if (fabs(tj) > ea[0] * AR[j] + ea[1] * AR[3 + j] + ea[2] * AR[6 + j] + eb[j] + margin) return 0;
+  }
+  for (int i = 0; i < 3; i++) {
+    int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+    for (int j = 0; j < 3; j++) {
+      int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      double ra = ea[i1] * AR[3 * i2 + j] + ea[i2] * AR[3 * i1 + j];
+      double rb = eb[j1] * AR[3 * i + j2] + eb[j2] * AR[3 * i + j1];
+      double tt = t[i2] * R[3 * i1 + j] - t[i1] * R[3 * i2 + j];
+      if (fabs(tt) > ra + rb + margin) return 0;
+    }
+  }
+  return 1;
+}
+
 static int sphere_overlap(const double* c1, double r1, const double* c2, double r2, double margin) {
   double t[3];
   sub3(t, c1, c2);
@@ -1137,17 +1180,27 @@ static void collision(const dxo_model* m, dxo_data* d) {
   if (m->disable_contact) return;
   for (int bp = 0; bp < m->nbpair; bp++) {
     int b1 = m->bpair_body[2 * bp], b2 = m->bpair_body[2 * bp + 1];
-    const double* s1 = m->body_bsphere + 4 * b1;
-    const double* s2 = m->body_bsphere + 4 * b2;
+    const double* s1 = m->bpair_sphere + 8 * bp;
+    const double* s2 = s1 + 4;
     double maxmargin = 0;
     for (int gp = m->bpair_adr[bp]; gp < m->bpair_adr[bp] + m->bpair_num[bp]; gp++)
       if (m->gpair_margin[gp] > maxmargin) maxmargin = m->gpair_margin[gp];
-    if (s1[3] >= 0 && s2[3] >= 0) {
-      double c1[3], c2[3];
-      matvec3(c1, d->xmat + 9 * b1, s1); add3(c1, c1, d->xpos + 3 * b1);
+    if (s2[3] >= 0) {
+      double c2[3];
       matvec3(c2, d->xmat + 9 * b2, s2); add3(c2, c2, d->xpos + 3 * b2);
-      d->flops[DXO_ST_COL] += 40;
-      if (!sphere_overlap(c1, s1[3], c2, s2[3], maxmargin)) continue;
+      d->flops[DXO_ST_COL] += 20;
+      int pg = m->bpair_plane[bp];
+      if (pg >= 0) {
+        const double* pm = d->geom_xmat + 9 * pg;
+        double n[3] = {pm[2], pm[5], pm[8]}, r[3];
+        sub3(r, c2, d->geom_xpos + 3 * pg);
+        if (dot3(r, n) > s2[3] + maxmargin) continue;
+      } else if (s1[3] >= 0) {
+        double c1[3];
+        matvec3(c1, d->xmat + 9 * b1, s1); add3(c1, c1, d->xpos + 3 * b1);
+        d->flops[DXO_ST_COL] += 20;
+        if (!sphere_overlap(c1, s1[3], c2, s2[3], maxmargin)) continue;
+      }
     }
     for (int gp = m->bpair_adr[bp]; gp < m->bpair_adr[bp] + m->bpair_num[bp]; gp++) {
       int g1 = m->gpair_geom[2 * gp], g2 = m->gpair_geom[2 * gp + 1];
@@ -1172,6 +1225,7 @@ static void collision(const dxo_model* m, dxo_data* d) {
       matvec3(c1, d->geom_xmat + 9 * g1, gs1); add3(c1, c1, d->geom_xpos + 3 * g1);
       d->flops[DXO_ST_COL] += 20;
       if (!sphere_overlap(c1, gs1[3], c2, gs2[3], margin)) continue;
+      if (!obb_overlap(m, d, g1, g2, margin, &d->flops[DXO_ST_COL])) continue;
       if (t1 == GEOM_CAPSULE && t2 == GEOM_CAPSULE) collide_capsules(m, d, gp, g1, g2, margin);
       else collide_convex(m, d, gp, g1, g2, margin);
     }
