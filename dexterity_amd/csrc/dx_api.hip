@@ -355,28 +355,28 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   if (it != m->dev_models.end()) { *out = it->second; return 0; }
   DevModel d = m->dm;
   std::vector<void*>& allocs = m->dev_allocs[device];
-  auto upf = [&](const char* name, const float** dst) -> int {
+  auto upf = [&](const char* name, const void** dst) -> int {
     auto& v = m->hf[name];
     size_t n = std::max<size_t>(v.size(), 1);
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, n * 4));
     allocs.push_back(p);
     if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
-    *dst = (const float*)p;
+    *dst = p;
     return 0;
   };
-  auto upi = [&](const char* name, const int** dst) -> int {
+  auto upi = [&](const char* name, const void** dst) -> int {
     auto& v = m->hi[name];
     size_t n = std::max<size_t>(v.size(), 1);
     void* p = nullptr;
     HIPCHK(hipMalloc(&p, n * 4));
     allocs.push_back(p);
     if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * 4, hipMemcpyHostToDevice));
-    *dst = (const int*)p;
+    *dst = p;
     return 0;
   };
-#define UF(field) if (int rc = upf(#field, &d.field)) return rc
-#define UI(field) if (int rc = upi(#field, &d.field)) return rc
+#define UF(field) { const void* p_; if (int rc = upf(#field, &p_)) return rc; d.field = (decltype(d.field))p_; }
+#define UI(field) { const void* p_; if (int rc = upi(#field, &p_)) return rc; d.field = (decltype(d.field))p_; }
   UI(body_parent); UI(body_rootidx); UI(body_jntnum); UI(body_jntadr); UI(body_dofnum); UI(body_dofadr);
   UI(lvl_adr); UI(lvl_body); UI(root_body);
   UF(body_pos); UF(body_quat); UF(body_ipos); UF(body_imat); UF(body_mass); UF(body_inertia);
@@ -403,7 +403,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   HIPCHK(hipMalloc(&p, m->body_chain.size() * 8));
   allocs.push_back(p);
   HIPCHK(hipMemcpy(p, m->body_chain.data(), m->body_chain.size() * 8, hipMemcpyHostToDevice));
-  d.body_chain = (const uint64_t*)p;
+  d.body_chain = (decltype(d.body_chain))p;
   m->dev_models[device] = d;
   *out = d;
   return 0;

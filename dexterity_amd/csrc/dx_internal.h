@@ -17,44 +17,52 @@ enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7
 enum { DXJ_FREE = 0, DXJ_HINGE = 3 };
 enum { DXR_FRIC = 0, DXR_LIMJ = 1, DXR_LIMT = 2, DXR_CON = 3, DXR_CONFL = 4 };
 
+// Model arrays live in global memory; on the device the pointers carry that address
+// space so accesses compile to global/scalar loads rather than generic flat loads.
+#ifdef __HIP_DEVICE_COMPILE__
+#define DXG __attribute__((address_space(1)))
+#else
+#define DXG
+#endif
+
 struct DevModel {
   int nq, nv, nbody, njnt, ngeom, nsite, nu, ntendon, nwrap, nbpair, ngpair;
   int iterations, disable_contact, any_damping, nlevel, nroot, nfric, nlimj, nlimt;
   float timestep, tolerance, impratio, meaninertia;
   float gravity[3];
   // bodies
-  const int *body_parent, *body_rootidx, *body_jntnum, *body_jntadr, *body_dofnum, *body_dofadr;
-  const int *lvl_adr, *lvl_body, *root_body;
-  const uint64_t* body_chain;  // dofs on the path body -> root
-  const float *body_pos, *body_quat, *body_ipos, *body_imat, *body_mass, *body_inertia;
-  const float *body_bsphere, *body_invweight0;
+  const DXG int *body_parent, *body_rootidx, *body_jntnum, *body_jntadr, *body_dofnum, *body_dofadr;
+  const DXG int *lvl_adr, *lvl_body, *root_body;
+  const DXG uint64_t* body_chain;  // dofs on the path body -> root
+  const DXG float *body_pos, *body_quat, *body_ipos, *body_imat, *body_mass, *body_inertia;
+  const DXG float *body_bsphere, *body_invweight0;
   // joints / dofs
-  const int *jnt_type, *jnt_bodyid, *jnt_qposadr, *jnt_dofadr;
-  const float *jnt_pos, *jnt_axis, *jnt_range, *jnt_margin, *jnt_solref, *jnt_solimp, *qpos0;
-  const int *limj_jnt;  // limited hinge joints
-  const int *dof_bodyid, *dof_parentid, *dof_jntid, *fric_dof, *dof_fricrow;
-  const float *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref, *dof_solimp,
+  const DXG int *jnt_type, *jnt_bodyid, *jnt_qposadr, *jnt_dofadr;
+  const DXG float *jnt_pos, *jnt_axis, *jnt_range, *jnt_margin, *jnt_solref, *jnt_solimp, *qpos0;
+  const DXG int *limj_jnt;  // limited hinge joints
+  const DXG int *dof_bodyid, *dof_parentid, *dof_jntid, *fric_dof, *dof_fricrow;
+  const DXG float *dof_armature, *dof_damping, *dof_frictionloss, *dof_solref, *dof_solimp,
       *dof_invweight0;
   // geoms / meshes
-  const int *geom_type, *geom_bodyid, *geom_dataid;
-  const float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere, *geom_bsphere_b, *geom_obb_b;
-  const int *mesh_vertadr, *mesh_vertnum;
-  const float* mesh_vert;
+  const DXG int *geom_type, *geom_bodyid, *geom_dataid;
+  const DXG float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere, *geom_bsphere_b, *geom_obb_b;
+  const DXG int *mesh_vertadr, *mesh_vertnum;
+  const DXG float* mesh_vert;
   // sites
-  const int* site_bodyid;
-  const float *site_pos, *site_mat;
+  const DXG int* site_bodyid;
+  const DXG float *site_pos, *site_mat;
   // tendons (fixed) and actuators
-  const int *tendon_adr, *tendon_num, *wrap_dof, *wrap_qadr, *limt_ten;
-  const float *tendon_range, *tendon_margin, *tendon_solref, *tendon_solimp, *tendon_invweight0,
+  const DXG int *tendon_adr, *tendon_num, *wrap_dof, *wrap_qadr, *limt_ten;
+  const DXG float *tendon_range, *tendon_margin, *tendon_solref, *tendon_solimp, *tendon_invweight0,
       *wrap_coef, *tendon_J;
-  const int *actuator_trntype, *actuator_trnid, *actuator_biastype, *actuator_ctrllimited,
+  const DXG int *actuator_trntype, *actuator_trnid, *actuator_biastype, *actuator_ctrllimited,
       *actuator_forcelimited;
-  const float *actuator_gear, *actuator_gainprm, *actuator_biasprm, *actuator_ctrlrange,
+  const DXG float *actuator_gear, *actuator_gainprm, *actuator_biasprm, *actuator_ctrlrange,
       *actuator_forcerange;
   // collision pairs
-  const int *bpair_body, *bpair_adr, *bpair_num, *bpair_plane, *gpair_geom, *gpair_condim;
-  const float* bpair_sphere;  // [nbpair][8]: sphere of side 1, side 2 (body frames)
-  const float *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
+  const DXG int *bpair_body, *bpair_adr, *bpair_num, *bpair_plane, *gpair_geom, *gpair_condim;
+  const DXG float* bpair_sphere;  // [nbpair][8]: sphere of side 1, side 2 (body frames)
+  const DXG float *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
 };
 
 struct DevBatch {

@@ -203,7 +203,7 @@ enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NI
 // ------------------------------------------------------------------------ //
 // position stage
 // ------------------------------------------------------------------------ //
-__device__ void kinematics(const Ctx& c) {
+__device__ __forceinline__ void kinematics(const Ctx& c) {
   const DevModel& m = c.m;
   float* qpos = c.f(c.L.qpos);
   float* xpos = c.f(c.L.xpos);
@@ -272,7 +272,7 @@ __device__ void kinematics(const Ctx& c) {
   }
 }
 
-__device__ void com_pos(const Ctx& c) {
+__device__ __forceinline__ void com_pos(const Ctx& c) {
   const DevModel& m = c.m;
   float* xipos = c.f(c.L.xipos);
   float* xmat = c.f(c.L.xmat);
@@ -345,7 +345,7 @@ __device__ void com_pos(const Ctx& c) {
   SYNC();
 }
 
-__device__ void tendon_lengths(const Ctx& c) {
+__device__ __forceinline__ void tendon_lengths(const Ctx& c) {
   const DevModel& m = c.m;
   float* qpos = c.f(c.L.qpos);
   float* tl = c.f(c.L.ten_len);
@@ -364,7 +364,7 @@ __device__ void tendon_lengths(const Ctx& c) {
   }
 }
 
-__device__ void crb_mass(const Ctx& c) {
+__device__ __forceinline__ void crb_mass(const Ctx& c) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float* crb = c.f(c.L.scr);
@@ -400,7 +400,7 @@ __device__ void crb_mass(const Ctx& c) {
 // lower triangle; entry t of a w x w trailing triangle maps to (ii, jj) through
 // the LDS table tri[t] = ii << 8 | jj (built once per launch), so the update is
 // branch-free and balanced over the 64 lanes.  Two barriers per column.
-__device__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
+__device__ __forceinline__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
   for (int k = 0; k < n; k++) {
     float d = sqrtf(fmaxf(A[k * n + k], 1e-30f));
     float inv = 1.0f / d;
@@ -419,7 +419,7 @@ __device__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
 }
 // Solve (L L^T) x = b; x holds b on entry (LDS).  Lane i keeps x_i in a register;
 // the dependent chain uses readlane broadcasts and no barriers.  n <= 64.
-__device__ void wave_chol_solve(const float* A, float* x, int n) {
+__device__ __forceinline__ void wave_chol_solve(const float* A, float* x, int n) {
   float xi = LANE < n ? x[LANE] : 0.f;
   for (int k = 0; k < n; k++) {
     float lik = LANE > k && LANE < n ? A[LANE * n + k] : 0.f;
@@ -447,7 +447,7 @@ struct Shape {
   const float* vert;
 };
 
-__device__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
+__device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
   const DevModel& m = c.m;
   int b = m.geom_bodyid[g];
   const float* xp = c.f(c.L.xpos) + 3 * b;
@@ -458,7 +458,7 @@ __device__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
   matmul3(mat, xm, m.geom_mat + 9 * g);
 }
 
-__device__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
+__device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
   const DevModel& m = c.m;
   s.type = m.geom_type[g];
   geom_pose(c, g, s.pos, s.mat);
@@ -476,7 +476,7 @@ __device__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
   s.margin = half_margin;
 }
 
-__device__ void support(const Shape& s, const float* dir, float* out) {
+__device__ __forceinline__ void support(const Shape& s, const float* dir, float* out) {
   float ld[3];
   mattvec3(ld, s.mat, dir);
   float lp[3] = {0, 0, 0};
@@ -516,19 +516,19 @@ __device__ __forceinline__ void mpr_support(const Shape& A, const Shape& B, cons
   sub3(p.v, p.a, p.b);
 }
 __device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-10f; }
-__device__ void portal_dir(const MPoint* P, float* dir) {
+__device__ __forceinline__ void portal_dir(const MPoint* P, float* dir) {
   float a[3], b[3];
   sub3(a, P[2].v, P[1].v);
   sub3(b, P[3].v, P[1].v);
   cross3(dir, a, b);
   normalize3(dir);
 }
-__device__ bool portal_reach_tol(const MPoint* P, const MPoint& v4, const float* dir, float tol) {
+__device__ __forceinline__ bool portal_reach_tol(const MPoint* P, const MPoint& v4, const float* dir, float tol) {
   float dv4 = dot3(v4.v, dir);
   float d1 = dv4 - dot3(P[1].v, dir), d2 = dv4 - dot3(P[2].v, dir), d3 = dv4 - dot3(P[3].v, dir);
   return fminf(d1, fminf(d2, d3)) <= tol;
 }
-__device__ void expand_portal(MPoint* P, const MPoint& v4) {
+__device__ __forceinline__ void expand_portal(MPoint* P, const MPoint& v4) {
   float v4v0[3];
   cross3(v4v0, v4.v, P[0].v);
   if (dot3(P[1].v, v4v0) > 0) {
@@ -539,7 +539,7 @@ __device__ void expand_portal(MPoint* P, const MPoint& v4) {
     else P[1] = v4;
   }
 }
-__device__ float tri_origin_dist2(const float* a, const float* b, const float* c, float* q) {
+__device__ __forceinline__ float tri_origin_dist2(const float* a, const float* b, const float* c, float* q) {
   float ab[3], ac[3], ap[3];
   sub3(ab, b, a); sub3(ac, c, a);
   ap[0] = -a[0]; ap[1] = -a[1]; ap[2] = -a[2];
@@ -574,7 +574,7 @@ __device__ float tri_origin_dist2(const float* a, const float* b, const float* c
   for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
   return dot3(q, q);
 }
-__device__ void find_pos(const MPoint* P, float* pos) {
+__device__ __forceinline__ void find_pos(const MPoint* P, float* pos) {
   float dir[3];
   portal_dir(P, dir);
   float b[4], t[3];
@@ -598,7 +598,7 @@ __device__ void find_pos(const MPoint* P, float* pos) {
 }
 
 // MPR penetration on A - B (libccd structure, see oracle mpr_penetration).
-__device__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+__device__ __forceinline__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
   const float tol = 1e-6f;
   const int maxit = 50;
   MPoint P[4];
@@ -688,7 +688,7 @@ __device__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, fl
 // Wave-cooperative support point: every lane runs the same (uniform) MPR control
 // flow; for mesh hulls the 64 lanes scan the vertices (staged in LDS) and an
 // argmax reduction picks the first maximal vertex, as the serial loop would.
-__device__ void support_wave(const Shape& s, const float* dir, float* out) {
+__device__ __forceinline__ void support_wave(const Shape& s, const float* dir, float* out) {
   float ld[3];
   mattvec3(ld, s.mat, dir);
   float lp[3] = {0, 0, 0};
@@ -728,7 +728,7 @@ __device__ __forceinline__ void mpr_support_wave(const Shape& A, const Shape& B,
 }
 
 // MPR penetration on A - B with wave-parallel support (see oracle mpr_penetration).
-__device__ bool mpr_wave(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+__device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
   const float tol = 1e-6f;
   const int maxit = 50;
   MPoint P[4];
@@ -824,7 +824,7 @@ __device__ __forceinline__ bool sphere_overlap(const float* c1, float r1, const 
 
 // Separating-axis test of two oriented boxes (Gottschalk's 15 axes), inflated by margin.
 // obb: [centre(3) in body frame, R(9) body<-box, half extents(3)].
-__device__ bool obb_overlap(const float* o1, const float* xp1, const float* xm1, const float* o2,
+__device__ __forceinline__ bool obb_overlap(const float* o1, const float* xp1, const float* xm1, const float* o2,
                             const float* xp2, const float* xm2, float margin) {
   float ca[3], cb[3], Ra[9], Rb[9];
   matvec3(ca, xm1, o1);
@@ -867,7 +867,7 @@ __device__ bool obb_overlap(const float* o1, const float* xp1, const float* xm1,
 }
 
 // Appends one contact record (called by a single lane).
-__device__ void write_contact(float* con, int slot, const float* pos, const float* n, float dist, int gp) {
+__device__ __forceinline__ void write_contact(float* con, int slot, const float* pos, const float* n, float dist, int gp) {
   float* r = con + DX_CON_STRIDE * slot;
   r[0] = pos[0]; r[1] = pos[1]; r[2] = pos[2];
   // frame: normal, tangent ([3P] mju_makeFrame)
@@ -888,14 +888,14 @@ __device__ void write_contact(float* con, int slot, const float* pos, const floa
 
 // Copies a mesh hull's vertices into LDS staging (returns the LDS pointer or the
 // global one when it does not fit).
-__device__ const float* stage_hull(const float* src, int nvert, float* dst, int cap) {
+__device__ __forceinline__ const float* stage_hull(const float* src, int nvert, float* dst, int cap) {
   if (3 * nvert > cap) return src;
   for (int k = LANE; k < 3 * nvert; k += DX_WAVE) dst[k] = src[k];
   return dst;
 }
 
 // Narrowphase of one geom pair by the whole wave; appends up to 4 contacts.
-__device__ int narrowphase_wave(const Ctx& c, int gp, float* con, int ncon) {
+__device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con, int ncon) {
   const DevModel& m = c.m;
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
@@ -1012,7 +1012,7 @@ __device__ int narrowphase_wave(const Ctx& c, int gp, float* con, int ncon) {
 // spheres, lanes over every geom pair of the surviving body pairs) -> narrowphase
 // (whole wave per pair).  Writes contact records into LDS.
 // watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
-__device__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
+__device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
   const DevModel& m = c.m;
   int* I = c.I;
   int* cand = (int*)c.f(c.L.H);  // H is free during collision
@@ -1146,7 +1146,7 @@ __device__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
 // ------------------------------------------------------------------------ //
 // constraints
 // ------------------------------------------------------------------------ //
-__device__ float impedance(const float* solimp, float violation) {
+__device__ __forceinline__ float impedance(const float* solimp, float violation) {
   float d0 = fminf(0.9999f, fmaxf(0.0001f, solimp[0]));
   float dmax = fminf(0.9999f, fmaxf(0.0001f, solimp[1]));
   float width = solimp[2], mid = solimp[3], power = solimp[4];
@@ -1161,7 +1161,7 @@ __device__ float impedance(const float* solimp, float violation) {
 }
 
 // row parameters -> D, aref, Rf.  vel = J*qvel.
-__device__ void row_params(const Ctx& c, int r, float pos, float margin, float floss, float diag,
+__device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float margin, float floss, float diag,
                            const float* solref, const float* solimp, float vel, float rscale, bool fric) {
   const DevModel& m = c.m;
   float imp = impedance(solimp, pos - margin);
@@ -1179,7 +1179,7 @@ __device__ void row_params(const Ctx& c, int r, float pos, float margin, float f
 }
 
 // sparse contact jacobian (frame rows) -> cj_idx / cj_val; then all rows
-__device__ void make_constraint(const Ctx& c) {
+__device__ __forceinline__ void make_constraint(const Ctx& c) {
   const DevModel& m = c.m;
   int nv = m.nv;
   int* I = c.I;
@@ -1356,7 +1356,7 @@ __device__ void make_constraint(const Ctx& c) {
 // ------------------------------------------------------------------------ //
 // velocity stage: comVel, RNE (+ applied wrench), passive, actuation
 // ------------------------------------------------------------------------ //
-__device__ void velocity_stage(const Ctx& c, const float* xfrc) {
+__device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float* qvel = c.f(c.L.qvel);
@@ -1479,7 +1479,7 @@ __device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf,
 }
 
 // y = M x (lanes over rows)
-__device__ void mat_vec(const float* M, const float* x, float* y, int n) {
+__device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y, int n) {
   for (int i = LANE; i < n; i += DX_WAVE) {
     float s = 0;
     for (int k = 0; k < n; k++) s += M[i * n + k] * x[k];
@@ -1488,7 +1488,7 @@ __device__ void mat_vec(const float* M, const float* x, float* y, int n) {
 }
 
 // J x for every row -> out[r]; uses cq as contact-frame scratch
-__device__ void jac_vec(const Ctx& c, const float* x, float* out) {
+__device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out) {
   const DevModel& m = c.m;
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
@@ -1528,7 +1528,7 @@ __device__ void jac_vec(const Ctx& c, const float* x, float* out) {
 }
 
 // cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
-__device__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
+__device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
   const DevModel& m = c.m;
   int nv = m.nv;
   const float* qs = c.f(c.L.qfrc_smooth);
@@ -1549,7 +1549,7 @@ __device__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
 }
 
 // jar = J qacc - aref, Ma = M qacc; returns cost
-__device__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
+__device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
   int nv = c.m.nv;
   mat_vec(c.f(c.L.M), qacc, Ma, nv);
   float* jar = c.f(c.L.efc_jar);
@@ -1563,7 +1563,7 @@ __device__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
 
 // out[d] = sum_r J[r][d] * w[r] computed as J^T applied to the per-row force of the
 // current jar (force mode) -- lane per dof, deterministic.
-__device__ void jac_t_force(const Ctx& c, float* out) {
+__device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
   const DevModel& m = c.m;
   int nv = m.nv;
   int nefc = c.I[I_NEFC];
@@ -1641,7 +1641,7 @@ __device__ void jac_t_force(const Ctx& c, float* out) {
 }
 
 // H = M + J^T D_active J  (at the current jar)
-__device__ void build_hessian(const Ctx& c) {
+__device__ __forceinline__ void build_hessian(const Ctx& c) {
   const DevModel& m = c.m;
   int nv = m.nv;
   int nefc = c.I[I_NEFC];
@@ -1737,7 +1737,7 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
   return jar < 0 ? 1 : 0;
 }
 
-__device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
+__device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float* Mdir = c.f(c.L.v4);
@@ -1787,7 +1787,7 @@ __device__ float line_search(const Ctx& c, const float* qacc, const float* Ma, c
   return alpha;
 }
 
-__device__ void solve(const Ctx& c) {
+__device__ __forceinline__ void solve(const Ctx& c) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float* qacc = c.f(c.L.qacc);
@@ -1864,7 +1864,7 @@ __device__ void solve(const Ctx& c) {
 // ------------------------------------------------------------------------ //
 // forward + Euler
 // ------------------------------------------------------------------------ //
-__device__ void position_stage(const Ctx& c) {
+__device__ __forceinline__ void position_stage(const Ctx& c) {
   kinematics(c);
   com_pos(c);
   stage_mark(c, ST_KIN);
@@ -1876,7 +1876,7 @@ __device__ void position_stage(const Ctx& c) {
   stage_mark(c, ST_CON);
 }
 
-__device__ void forward(const Ctx& c, const float* xfrc) {
+__device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   const DevModel& m = c.m;
   int nv = m.nv;
   position_stage(c);
@@ -1905,7 +1905,7 @@ __device__ void forward(const Ctx& c, const float* xfrc) {
   stage_mark(c, ST_QFRC);
 }
 
-__device__ void euler(const Ctx& c, float* time) {
+__device__ __forceinline__ void euler(const Ctx& c, float* time) {
   const DevModel& m = c.m;
   int nv = m.nv;
   float h = m.timestep;
@@ -1955,7 +1955,7 @@ __device__ void euler(const Ctx& c, float* time) {
 }
 
 // observation pass at the new state: kinematics, com, velocities, sites, watch contact
-__device__ void observe(const Ctx& c, const DevBatch& B, int env) {
+__device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env) {
   const DevModel& m = c.m;
   kinematics(c);
   com_pos(c);
