@@ -11,7 +11,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libdx.so")
+LIB_PATH = os.environ.get("DX_LIB") or os.path.join(_HERE, "libdx.so")  # DX_LIB: A/B-test a variant build
 
 # dx_field
 QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
@@ -19,7 +19,7 @@ SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND = 6, 7, 8, 
 INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND)
 
 EXPORTS = (
-    "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_field_width",
+    "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_model_lds_bytes", "dx_field_width",
     "dx_batch_create", "dx_batch_destroy", "dx_batch_nenv", "dx_reset",
     "dx_set_field", "dx_get_field", "dx_field_ptr", "dx_set_xfrc", "dx_set_ground_geom",
     "dx_set_watch", "dx_step", "dx_forward", "dx_stream", "dx_sync",
@@ -27,10 +27,14 @@ EXPORTS = (
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
+    "dx_debug_poison_lds",
 )
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
-          "qfrc_constraint", "euler", "observe", "io")
+          "qfrc_constraint", "euler", "observe", "io", "np_setup", "np_mpr", "np_prim")
+COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
+            26: "mpr_maxit"}
+NSTAGE = 32
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
 TASK_REORIENT = 0
 
@@ -55,6 +59,7 @@ def load(path: str = LIB_PATH):
     L.dx_model_load.argtypes = [ctypes.c_char_p, sz]
     L.dx_model_free.argtypes = [vp]
     L.dx_model_sizes.argtypes = [vp, ctypes.POINTER(i32)]
+    L.dx_model_lds_bytes.argtypes = [vp]
     L.dx_field_width.argtypes = [vp, ctypes.c_int]
     L.dx_batch_create.restype = vp
     L.dx_batch_create.argtypes = [vp, i32, i32]
@@ -92,6 +97,7 @@ def load(path: str = LIB_PATH):
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.dx_stage_timing.argtypes = [vp, ctypes.c_int]
     L.dx_stage_read.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), i32]
+    L.dx_debug_poison_lds.argtypes = [i32]
     _lib = L
     return L
 

@@ -274,34 +274,66 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   d.any_damping = 0;
   for (int i = 0; i < nv; i++)
     if (damp[i] > 0) d.any_damping = 1;
-  // LDS layout
+  // LDS layout (4-byte words).  Persistent arrays first, then a union whose
+  // contents change with the stage (dx_step.hip forward()):
+  //   A  kinematic block      xpos xmat xipos rcom cdof   kinematics .. make_constraint
+  //   B1 com temporaries      cinert cvel cdof_dot scr xanchor xaxis xquat
+  //                                                       kinematics .. velocity stage
+  //   B2 smooth-solve transpose (packed nv x nv)          smooth solve
+  //   B3 candidate lists + hull staging                   collision
+  //   B4 constraint rows + contact jacobians              make_constraint .. qfrc_constraint
+  //   H  Newton Hessian / Euler transpose over A          solve, euler
+  // The union keeps one environment in < 20 KB for the Shadow scene, so eight
+  // 64-lane workgroups (two waves per SIMD) fit in a CU's 160 KB.
   Lds& L = m->lds;
   int off = 0;
   auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
+  auto r4 = [](int n) { return (n + 3) & ~3; };
+  const int ntri = nv * (nv + 1) / 2;
+  L.ints = take(16);
   L.qpos = take(d.nq); L.qvel = take(nv); L.ctrl = take(std::max(d.nu, 1)); L.qacc = take(nv);
   L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv); L.qfrc_con = take(nv);
   L.v1 = take(nv); L.v2 = take(nv); L.v3 = take(nv); L.v4 = take(nv); L.v5 = take(nv);
-  L.xpos = take(3 * nb); L.xquat = take(4 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
-  L.xanchor = take(3 * std::max(d.njnt, 1)); L.xaxis = take(3 * std::max(d.njnt, 1));
-  L.rcom = take(3 * std::max(d.nroot, 1)); L.cinert = take(10 * nb); L.cdof = take(6 * nv);
-  L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.scr = take(12 * nb);
-  L.M = take(nv * nv);
-  L.cand_max = std::max(nv * nv, 768);
-  L.H = take(L.cand_max);
+  L.M = take(ntri);
   L.ten_len = take(std::max(d.ntendon, 1)); L.act_len = take(std::max(d.nu, 1));
   L.act_force = take(std::max(d.nu, 1));
   L.con = take(DX_NCON_MAX * DX_CON_STRIDE);
-  L.cj_idx = take(DX_NCON_MAX * DX_DOFMAX);
+  L.nefc_max = d.nfric + 2 * d.nlimj + 2 * d.nlimt + 4 * DX_NCON_MAX;
+  L.efc_fl = take(std::max(d.nfric, 1)); L.efc_Rf = take(std::max(d.nfric, 1));
+  L.tri = nv > 32 ? take((ntri + 1) / 2) : 0;
+  const int U0 = off;
+  L.xpos = take(3 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
+  L.rcom = take(3 * std::max(d.nroot, 1)); L.cdof = take(6 * nv);
+  const int B0 = off;
+  L.cinert = take(10 * nb); L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.scr = take(12 * nb);
+  L.xanchor = take(3 * std::max(d.njnt, 1)); L.xaxis = take(3 * std::max(d.njnt, 1));
+  L.xquat = take(4 * nb);
+  int end = off;
+  L.tsm = B0;
+  end = std::max(end, B0 + r4(ntri));
+  // staging must hold the two largest hulls of any geom pair
+  auto& gtype = m->hi["geom_type"];
+  auto& gdata = m->hi["geom_dataid"];
+  auto& mvn = m->hi["mesh_vertnum"];
+  auto& gpg = m->hi["gpair_geom"];
+  auto hullw = [&](int g) { return gtype[g] == DXG_MESH ? 3 * mvn[gdata[g]] : 0; };
+  int stage_need = 0;
+  for (int p = 0; p < d.ngpair; p++) stage_need = std::max(stage_need, hullw(gpg[2 * p]) + hullw(gpg[2 * p + 1]));
+  L.cand_max = 768;
+  L.cand = B0;
+  L.stage = B0 + L.cand_max;
+  end = std::max(end, L.stage + r4(std::max(stage_need, 1)));
+  off = std::max(B0, U0 + r4(ntri));
+  L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
+  L.efc_jar = take(L.nefc_max); L.efc_jv = take(L.nefc_max);
+  L.cj_idx = take((DX_NCON_MAX * DX_DOFMAX + 3) / 4);  // uint8 dof ids
   L.cj_val = take(DX_NCON_MAX * 3 * DX_DOFMAX);
   L.cq = take(3 * DX_NCON_MAX);
   L.cw = take(3 * DX_NCON_MAX);
-  L.nefc_max = d.nfric + 2 * d.nlimj + 2 * d.nlimt + 4 * DX_NCON_MAX;
-  L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
-  L.efc_fl = take(L.nefc_max); L.efc_Rf = take(L.nefc_max); L.efc_jar = take(L.nefc_max);
-  L.efc_jv = take(L.nefc_max);
-  L.tri = take((nv * (nv + 1) / 2 + 1) / 2);
-  L.ints = take(16);
-  L.total = off;
+  end = std::max(end, off);
+  L.H = U0;
+  L.total = end;
+  L.stage_cap = L.total - L.stage;
   m->ncon_max = DX_NCON_MAX;
   m->nefc_max = L.nefc_max;
   if (L.total * 4 > 160 * 1024) {
@@ -331,6 +363,11 @@ extern "C" int dx_model_sizes(const dx_model* m, int32_t out[12]) {
                m->ncon_max, m->nefc_max};
   memcpy(out, v, sizeof(v));
   return 0;
+}
+
+extern "C" int dx_model_lds_bytes(const dx_model* m) {
+  if (!m) return fail(DX_EINVAL, "null model");
+  return m->lds.total * 4;
 }
 
 extern "C" int dx_field_width(const dx_model* m, int field) {
@@ -875,11 +912,31 @@ extern "C" int dx_env_pack_outputs(dx_env* e, float* dst_dev) {
   return 0;
 }
 
+// Fills every CU's LDS with NaN bit patterns (test hook: the step kernel must not
+// depend on LDS contents left by earlier workgroups).
+__global__ void dx_poison_lds_kernel(int nwords) {
+  extern __shared__ unsigned int lds_words[];
+  for (int k = threadIdx.x; k < nwords; k += blockDim.x) lds_words[k] = 0x7fc00000u | (k & 0xff);
+  __syncthreads();
+}
+
+extern "C" int dx_debug_poison_lds(int32_t device) {
+  HIPCHK(hipSetDevice(device));
+  const int bytes = 64 * 1024;
+  hipLaunchKernelGGL(dx_poison_lds_kernel, dim3(256 * 16), dim3(256), bytes, nullptr, bytes / 4);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
 extern "C" int dx_stage_timing(dx_batch* b, int enable) {
   if (!b) return fail(DX_EINVAL, "null batch");
+  HIPCHK(hipSetDevice(b->device));
+  size_t bytes = (size_t)b->nenv * DX_NSTAGE * 8;  // per-env accumulators: no atomics
   if (enable && !b->db.stage_acc) {
     void* p = nullptr;
-    if (int rc = balloc(b, &p, DX_NSTAGE * 8)) return rc;
+    if (int rc = balloc(b, &p, bytes)) return rc;
+    HIPCHK(hipMemsetAsync(p, 0, bytes, b->stream));
     b->db.stage_acc = (unsigned long long*)p;
   } else if (!enable) {
     b->db.stage_acc = nullptr;
@@ -891,8 +948,16 @@ extern "C" int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n) {
   if (!b || !out) return fail(DX_EINVAL, "null argument");
   if (!b->db.stage_acc) return fail(DX_EINVAL, "stage timing not enabled");
   HIPCHK(hipSetDevice(b->device));
-  HIPCHK(hipMemcpyAsync(out, b->db.stage_acc, std::min(n, DX_NSTAGE) * 8, hipMemcpyDeviceToHost, b->stream));
-  HIPCHK(hipMemsetAsync(b->db.stage_acc, 0, DX_NSTAGE * 8, b->stream));
+  size_t cnt = (size_t)b->nenv * DX_NSTAGE;
+  std::vector<uint64_t> h(cnt);
+  HIPCHK(hipMemcpyAsync(h.data(), b->db.stage_acc, cnt * 8, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipMemsetAsync(b->db.stage_acc, 0, cnt * 8, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  for (int k = 0; k < std::min(n, DX_NSTAGE); k++) {
+    uint64_t t = 0;
+    for (int e = 0; e < b->nenv; e++) t += h[(size_t)e * DX_NSTAGE + k];
+    out[k] = t;
+  }
   HIPCHK(hipStreamSynchronize(b->stream));
   return 0;
 }

@@ -17,10 +17,11 @@ enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7
 enum { DXJ_FREE = 0, DXJ_HINGE = 3 };
 enum { DXR_FRIC = 0, DXR_LIMJ = 1, DXR_LIMT = 2, DXR_CON = 3, DXR_CONFL = 4 };
 
-// Model arrays live in global memory; on the device the pointers carry that address
-// space so accesses compile to global/scalar loads rather than generic flat loads.
+// Model arrays are read-only for a launch; on the device the pointers carry the
+// constant address space, so uniform accesses compile to scalar (s_load) loads
+// and divergent ones to global loads -- never generic flat loads.
 #ifdef __HIP_DEVICE_COMPILE__
-#define DXG __attribute__((address_space(1)))
+#define DXG __attribute__((address_space(4)))
 #else
 #define DXG
 #endif
@@ -78,7 +79,7 @@ struct DevBatch {
   int* dbg_nefc;
   unsigned long long* stage_acc;  // [DX_NSTAGE] s_memtime cycles per stage (null: off)
 };
-#define DX_NSTAGE 24
+#define DX_NSTAGE 32
 
 // Offsets (in 4-byte words) of every per-env LDS array.
 struct Lds {
@@ -88,9 +89,11 @@ struct Lds {
   int M, H, ten_len, act_len, act_force;
   int con, cj_idx, cj_val, cq, cw;
   int efc_meta, efc_D, efc_aref, efc_fl, efc_Rf, efc_jar, efc_jv;
-  int tri;   // ushort lower-triangle index table
+  int tri;   // ushort lower-triangle index table (nv > 32 only)
   int ints;  // misc int scalars
-  int nefc_max, cand_max;
+  int tsm;   // smooth-solve Cholesky transpose
+  int cand, stage;  // collision candidate lists, hull staging
+  int nefc_max, cand_max, stage_cap;
   int total;
 };
 

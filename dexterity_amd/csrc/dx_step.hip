@@ -22,21 +22,14 @@
 #include <math.h>
 
 #define LANE ((int)threadIdx.x)
-#define SYNC() __syncthreads()
+// A workgroup is exactly one wavefront, and a wavefront's LDS instructions execute
+// in issue order, so cross-lane LDS hand-offs need only a compiler-level barrier
+// (no s_barrier, and no s_waitcnt on outstanding global stores).
+#define SYNC() __builtin_amdgcn_wave_barrier()
 
 // ------------------------------------------------------------------------ //
 // wave helpers
 // ------------------------------------------------------------------------ //
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
 // DPP row reductions (gfx9 family): quad_perm, row_half_mirror, row_mirror, then
 // row_bcast15 / row_bcast31 carry the partial results up to lane 63.
 template <int CTRL, int ROWMASK>
@@ -46,6 +39,26 @@ __device__ __forceinline__ float dpp_f(float x) {
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ int dpp_i(int x) {
   return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xF, false);
+}
+// Sums: quad, half-row, row sums by DPP, then rows carried up to lane 63 (each lane
+// contributes exactly once), broadcast with readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1, 0xF>(v);
+  v += dpp_f<0x4E, 0xF>(v);
+  v += dpp_f<0x141, 0xF>(v);
+  v += dpp_f<0x140, 0xF>(v);
+  v += dpp_f<0x142, 0xA>(v);
+  v += dpp_f<0x143, 0xC>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+  v += dpp_i<0xB1, 0xF>(v);
+  v += dpp_i<0x4E, 0xF>(v);
+  v += dpp_i<0x141, 0xF>(v);
+  v += dpp_i<0x140, 0xF>(v);
+  v += dpp_i<0x142, 0xA>(v);
+  v += dpp_i<0x143, 0xC>(v);
+  return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ float wave_max_f(float m) {
   m = fmaxf(m, dpp_f<0xB1, 0xF>(m));
@@ -187,15 +200,21 @@ struct Ctx {
 // Per-stage cycle accounting (runtime-gated by DevBatch::stage_acc, lane 0 only).
 enum {
   ST_KIN = 0, ST_CRB, ST_BROAD, ST_MID, ST_NARROW, ST_CON, ST_VEL, ST_SMOOTH, ST_NEWTON_EVAL,
-  ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO
+  ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO,
+  ST_NP_SETUP, ST_NP_MPR, ST_NP_PRIM,
+  CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
+  CNT_MPR_MAXIT  // event counters, not cycles
 };
 __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
   if (c.stage_acc && LANE == 0) {
     unsigned long long t = __builtin_amdgcn_s_memtime();
     unsigned long long* last = (unsigned long long*)(c.I + 10);
-    atomicAdd(c.stage_acc + k, t - *last);
+    c.stage_acc[k] += t - *last;  // this env's own slots
     *last = t;
   }
+}
+__device__ __forceinline__ void stage_count(const Ctx& c, int k) {
+  if (c.stage_acc && LANE == 0) c.stage_acc[k] += 1;
 }
 // misc int slots
 enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
@@ -364,6 +383,10 @@ __device__ __forceinline__ void tendon_lengths(const Ctx& c) {
   }
 }
 
+// Symmetric nv x nv matrices (M, the Newton Hessian, Cholesky factors) are stored
+// as packed lower triangles, row-major: (i, j <= i) -> ti(i) + j.
+__device__ __forceinline__ int ti(int i) { return (i * (i + 1)) >> 1; }
+
 __device__ __forceinline__ void crb_mass(const Ctx& c) {
   const DevModel& m = c.m;
   int nv = m.nv;
@@ -372,7 +395,7 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
   float* M = c.f(c.L.M);
   float* cdof = c.f(c.L.cdof);
   for (int k = LANE; k < 10 * m.nbody; k += DX_WAVE) crb[k] = cinert[k];
-  for (int k = LANE; k < nv * nv; k += DX_WAVE) M[k] = 0;
+  for (int k = LANE; k < ti(nv); k += DX_WAVE) M[k] = 0;
   SYNC();
   for (int lv = m.nlevel - 1; lv > 0; lv--) {
     for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
@@ -386,11 +409,9 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
     float f[6];
     mul_inert(f, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
     for (int j = i; j >= 0; j = m.dof_parentid[j]) {
-      float v = dot6(cdof + 6 * j, f);
-      M[i * nv + j] = v;
-      M[j * nv + i] = v;
+      M[ti(i) + j] = dot6(cdof + 6 * j, f);  // ancestors j < i
     }
-    M[i * nv + i] += m.dof_armature[i];
+    M[ti(i) + i] += m.dof_armature[i];
   }
   SYNC();
 }
@@ -402,17 +423,17 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
 // branch-free and balanced over the 64 lanes.  Two barriers per column.
 __device__ __forceinline__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
   for (int k = 0; k < n; k++) {
-    float d = sqrtf(fmaxf(A[k * n + k], 1e-30f));
+    float d = sqrtf(fmaxf(A[ti(k) + k], 1e-30f));
     float inv = 1.0f / d;
-    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) A[i * n + k] *= inv;
+    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) A[ti(i) + k] *= inv;
     SYNC();
-    if (LANE == 0) A[k * n + k] = d;
+    if (LANE == 0) A[ti(k) + k] = d;
     int w = n - k - 1;
     int tot = w * (w + 1) / 2;
     for (int t = LANE; t < tot; t += DX_WAVE) {
       int e = tri[t];
       int i = k + 1 + (e >> 8), j = k + 1 + (e & 255);
-      A[i * n + j] -= A[i * n + k] * A[j * n + k];
+      A[ti(i) + j] -= A[ti(i) + k] * A[ti(j) + k];
     }
     SYNC();
   }
@@ -422,14 +443,14 @@ __device__ __forceinline__ void wave_cholesky(float* A, int n, const unsigned sh
 __device__ __forceinline__ void wave_chol_solve(const float* A, float* x, int n) {
   float xi = LANE < n ? x[LANE] : 0.f;
   for (int k = 0; k < n; k++) {
-    float lik = LANE > k && LANE < n ? A[LANE * n + k] : 0.f;
-    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[k * n + k];
+    float lik = LANE > k && LANE < n ? A[ti(LANE) + k] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[ti(k) + k];
     if (LANE == k) xi = v;
     xi -= lik * v;
   }
   for (int k = n - 1; k >= 0; k--) {
-    float lki = LANE < k ? A[k * n + LANE] : 0.f;
-    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[k * n + k];
+    float lki = LANE < k ? A[ti(k) + LANE] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[ti(k) + k];
     if (LANE == k) xi = v;
     xi -= lki * v;
   }
@@ -438,13 +459,93 @@ __device__ __forceinline__ void wave_chol_solve(const float* A, float* x, int n)
   SYNC();
 }
 
+// Register Cholesky solve for n <= 32: lane i holds row i of A in r[0..31].
+// Right-looking like wave_cholesky (same per-element update order); the column
+// broadcast is a v_readlane instead of an LDS round trip + barrier.  No per-lane
+// predicates in the hot loops (they made the compiler keep 32 exec masks live):
+// rows are loaded unconditionally (entries above the diagonal, and the rows of
+// lanes >= n, hold garbage that never reaches rows < n because every broadcast
+// reads a lane < n), the diagonal lives in dinv (set with v_writelane), and the
+// substitutions deposit results with v_writelane.  The back substitution needs
+// columns of L: one LDS transpose through T (packed, may alias A).
+// A (+ hs*dadd on the diagonal, if dadd) -> x = A^-1 x.
+__device__ __forceinline__ float rl(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+// llvm.amdgcn.writelane (no clang builtin in this toolchain)
+extern "C" __device__ int dx_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ float wl(float v, float s, int k) {  // v with lane k := s
+  return __int_as_float(dx_writelane_i32(__float_as_int(s), k, __float_as_int(v)));
+}
+__device__ __forceinline__ void reg_chol_solve32(const float* A, int n, const DXG float* dadd, float hs,
+                                                 float* x, float* T) {
+  // All 32 steps run regardless of n (no n-dependent branches: the compiler would
+  // hoist 32 loop-invariant masks out of the Newton loop and spill them).  Lanes
+  // and columns >= n only ever see finite LDS words (the kernel zeroes its LDS
+  // block at entry) and multiply into zeros.
+  constexpr int NB = 32;
+  const int i = LANE;
+  const float* Ai = A + ti(min(i, n - 1));
+  float r[NB];
+#pragma unroll
+  for (int k = 0; k < NB; k++) r[k] = Ai[k];
+  float add = (dadd && i < n) ? hs * dadd[i] : 0.f;
+  float b = i < n ? x[i] : 0.f;
+  SYNC();  // A may alias T
+  float dinv = 0.f;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    float d = sqrtf(fmaxf(rl(r[k], k) + rl(add, k), 1e-30f));
+    float inv = 1.0f / d;
+    dinv = wl(dinv, inv, k);
+    float lik = r[k] * inv;
+    r[k] = lik;
+#pragma unroll
+    for (int j = k + 1; j < NB; j++) r[j] = fmaf(-lik, rl(lik, j), r[j]);
+  }
+  // strictly-lower row -> T (packed), and zero the rest of r
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    bool low = k < i && i < n;
+    r[k] = low ? r[k] : 0.f;
+    if (low) T[ti(i) + k] = r[k];
+  }
+  // forward: L y = b
+  float y = 0.f;
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    float yk = rl(b, k) * rl(dinv, k);
+    y = wl(y, yk, k);
+    b = fmaf(-r[k], yk, b);
+  }
+  SYNC();
+  // column i of L (below the diagonal) -> r; rows >= n of T are never written
+  const int ic = min(i, n - 1);
+#pragma unroll
+  for (int k = 0; k < NB; k++) {
+    float v = T[ti(k) + ic];
+    r[k] = ic < k ? v : 0.f;
+  }
+  // backward: L^T x = y  (y is 0 on lanes >= n, so steps k >= n add 0 * finite)
+  float xo = 0.f;
+#pragma unroll
+  for (int k = NB - 1; k >= 0; k--) {
+    float xk = rl(y, k) * rl(dinv, k);
+    xo = wl(xo, xk, k);
+    y = fmaf(-r[k], xk, y);
+  }
+  if (i < n) x[i] = xo;
+  SYNC();
+}
+
 // ------------------------------------------------------------------------ //
 // collision
 // ------------------------------------------------------------------------ //
 struct Shape {
   int type, nvert;
+  int voff;  // LDS word offset of the staged hull vertices (meshes)
   float pos[3], mat[9], size[3], center[3], margin;
-  const float* vert;
+  const DXG float* vert;  // hull vertices in global memory
 };
 
 __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
@@ -465,6 +566,7 @@ __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margi
   s.size[0] = m.geom_size[3 * g]; s.size[1] = m.geom_size[3 * g + 1]; s.size[2] = m.geom_size[3 * g + 2];
   s.vert = nullptr;
   s.nvert = 0;
+  s.voff = 0;
   if (s.type == DXG_MESH) {
     int mid = m.geom_dataid[g];
     s.vert = m.mesh_vert + 3 * m.mesh_vertadr[mid];
@@ -476,45 +578,8 @@ __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margi
   s.margin = half_margin;
 }
 
-__device__ __forceinline__ void support(const Shape& s, const float* dir, float* out) {
-  float ld[3];
-  mattvec3(ld, s.mat, dir);
-  float lp[3] = {0, 0, 0};
-  if (s.type == DXG_BOX) {
-    for (int k = 0; k < 3; k++) lp[k] = ld[k] >= 0 ? s.size[k] : -s.size[k];
-  } else if (s.type == DXG_MESH) {
-    float best = -3.0e38f;
-    int bi = 0;
-    for (int i = 0; i < s.nvert; i++) {
-      const float* v = s.vert + 3 * i;
-      float d = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
-      if (d > best) { best = d; bi = i; }
-    }
-    lp[0] = s.vert[3 * bi]; lp[1] = s.vert[3 * bi + 1]; lp[2] = s.vert[3 * bi + 2];
-  } else if (s.type == DXG_SPHERE || s.type == DXG_CAPSULE) {
-    float n = norm3(ld);
-    if (n > 1e-20f) { float sc = s.size[0] / n; lp[0] = ld[0] * sc; lp[1] = ld[1] * sc; lp[2] = ld[2] * sc; }
-    if (s.type == DXG_CAPSULE) lp[2] += ld[2] >= 0 ? s.size[1] : -s.size[1];
-  }
-  matvec3(out, s.mat, lp);
-  out[0] += s.pos[0]; out[1] += s.pos[1]; out[2] += s.pos[2];
-  if (s.margin > 0) {
-    float n = norm3(dir);
-    if (n > 1e-20f) {
-      float sc = s.margin / n;
-      out[0] += dir[0] * sc; out[1] += dir[1] * sc; out[2] += dir[2] * sc;
-    }
-  }
-}
-
 struct MPoint { float v[3], a[3], b[3]; };
 
-__device__ __forceinline__ void mpr_support(const Shape& A, const Shape& B, const float* dir, MPoint& p) {
-  float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support(A, dir, p.a);
-  support(B, nd, p.b);
-  sub3(p.v, p.a, p.b);
-}
 __device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-10f; }
 __device__ __forceinline__ void portal_dir(const MPoint* P, float* dir) {
   float a[3], b[3];
@@ -597,111 +662,35 @@ __device__ __forceinline__ void find_pos(const MPoint* P, float* pos) {
   for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
 }
 
-// MPR penetration on A - B (libccd structure, see oracle mpr_penetration).
-__device__ __forceinline__ bool mpr_penetration(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
-  const float tol = 1e-6f;
-  const int maxit = 50;
-  MPoint P[4];
-  sub3(P[0].v, A.center, B.center);
-  for (int k = 0; k < 3; k++) { P[0].a[k] = A.center[k]; P[0].b[k] = B.center[k]; }
-  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-9f;
-  float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
-  normalize3(dir);
-  mpr_support(A, B, dir, P[1]);
-  float dt = dot3(P[1].v, dir);
-  if (fzero(dt) || dt < 0) return false;
-  cross3(dir, P[0].v, P[1].v);
-  if (fzero(dot3(dir, dir))) {
-    if (fzero(P[1].v[0]) && fzero(P[1].v[1]) && fzero(P[1].v[2])) {
-      depth = 0;
-      normal[0] = 0; normal[1] = 0; normal[2] = 1;
-    } else {
-      depth = norm3(P[1].v);
-      for (int k = 0; k < 3; k++) normal[k] = P[1].v[k];
-      normalize3(normal);
-    }
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P[1].a[k] + P[1].b[k]);
-    return true;
-  }
-  normalize3(dir);
-  mpr_support(A, B, dir, P[2]);
-  dt = dot3(P[2].v, dir);
-  if (fzero(dt) || dt < 0) return false;
-  float va[3], vb[3];
-  sub3(va, P[1].v, P[0].v);
-  sub3(vb, P[2].v, P[0].v);
-  cross3(dir, va, vb);
-  normalize3(dir);
-  if (dot3(dir, P[0].v) > 0) {
-    MPoint t = P[1]; P[1] = P[2]; P[2] = t;
-    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
-  }
-  for (int it = 0;; it++) {
-    if (it > 1000) return false;
-    mpr_support(A, B, dir, P[3]);
-    dt = dot3(P[3].v, dir);
-    if (fzero(dt) || dt < 0) return false;
-    bool cont = false;
-    cross3(va, P[1].v, P[3].v);
-    dt = dot3(va, P[0].v);
-    if (dt < 0 && !fzero(dt)) { P[2] = P[3]; cont = true; }
-    if (!cont) {
-      cross3(va, P[3].v, P[2].v);
-      dt = dot3(va, P[0].v);
-      if (dt < 0 && !fzero(dt)) { P[1] = P[3]; cont = true; }
-    }
-    if (!cont) break;
-    sub3(va, P[1].v, P[0].v);
-    sub3(vb, P[2].v, P[0].v);
-    cross3(dir, va, vb);
-    normalize3(dir);
-  }
-  for (int it = 0;; it++) {
-    portal_dir(P, dir);
-    if (dot3(dir, P[1].v) >= 0) break;
-    MPoint v4;
-    mpr_support(A, B, dir, v4);
-    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P, v4, dir, tol) || it > maxit) return false;
-    expand_portal(P, v4);
-  }
-  for (int it = 0;; it++) {
-    portal_dir(P, dir);
-    MPoint v4;
-    mpr_support(A, B, dir, v4);
-    if (portal_reach_tol(P, v4, dir, tol) || it > maxit) {
-      float cl[3];
-      float d2 = tri_origin_dist2(P[1].v, P[2].v, P[3].v, cl);
-      depth = sqrtf(d2);
-      if (depth > 1e-20f) {
-        float s = 1.0f / depth;
-        normal[0] = cl[0] * s; normal[1] = cl[1] * s; normal[2] = cl[2] * s;
-      } else {
-        normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
-      }
-      find_pos(P, pos);
-      return true;
-    }
-    expand_portal(P, v4);
-  }
-}
-
 // Wave-cooperative support point: every lane runs the same (uniform) MPR control
 // flow; for mesh hulls the 64 lanes scan the vertices (staged in LDS) and an
 // argmax reduction picks the first maximal vertex, as the serial loop would.
-__device__ __forceinline__ void support_wave(const Shape& s, const float* dir, float* out) {
+__device__ __forceinline__ void support_wave(const Ctx& c, const Shape& s, const float* dir, float* out) {
   float ld[3];
   mattvec3(ld, s.mat, dir);
   float lp[3] = {0, 0, 0};
   if (s.type == DXG_MESH) {
+    // lane t scans vertices t, t+64, ... (4 loads in flight per pass); strict '>'
+    // keeps each lane's first maximum, the reduction the lowest index among lanes.
+    const float* V = c.S + s.voff;
+    const int nvert = s.nvert;
     float best = -3.0e38f;
     int bi = 0x7fffffff;
-    for (int i = LANE; i < s.nvert; i += DX_WAVE) {
-      const float* v = s.vert + 3 * i;
-      float d = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
-      if (d > best) { best = d; bi = i; }
+    for (int base = 0; base < nvert; base += 4 * DX_WAVE) {
+      float d[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        int i = base + u * DX_WAVE + LANE;
+        const float* v = V + 3 * (i < nvert ? i : 0);
+        float dd = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
+        d[u] = i < nvert ? dd : -3.0e38f;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (d[u] > best) { best = d[u]; bi = base + u * DX_WAVE + LANE; }
     }
     bi = wave_argmax_first(best, bi);
-    lp[0] = s.vert[3 * bi]; lp[1] = s.vert[3 * bi + 1]; lp[2] = s.vert[3 * bi + 2];
+    lp[0] = V[3 * bi]; lp[1] = V[3 * bi + 1]; lp[2] = V[3 * bi + 2];
   } else if (s.type == DXG_BOX) {
     for (int k = 0; k < 3; k++) lp[k] = ld[k] >= 0 ? s.size[k] : -s.size[k];
   } else if (s.type == DXG_SPHERE || s.type == DXG_CAPSULE) {
@@ -720,15 +709,16 @@ __device__ __forceinline__ void support_wave(const Shape& s, const float* dir, f
   }
 }
 
-__device__ __forceinline__ void mpr_support_wave(const Shape& A, const Shape& B, const float* dir, MPoint& p) {
+__device__ __forceinline__ void mpr_support_wave(const Ctx& c, const Shape& A, const Shape& B, const float* dir, MPoint& p) {
+  stage_count(c, CNT_SUPPORT);
   float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_wave(A, dir, p.a);
-  support_wave(B, nd, p.b);
+  support_wave(c, A, dir, p.a);
+  support_wave(c, B, nd, p.b);
   sub3(p.v, p.a, p.b);
 }
 
 // MPR penetration on A - B with wave-parallel support (see oracle mpr_penetration).
-__device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+__device__ __forceinline__ bool mpr_wave(const Ctx& c, const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
   const float tol = 1e-6f;
   const int maxit = 50;
   MPoint P[4];
@@ -737,7 +727,7 @@ __device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& 
   if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-9f;
   float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
   normalize3(dir);
-  mpr_support_wave(A, B, dir, P[1]);
+  mpr_support_wave(c, A, B, dir, P[1]);
   float dt = dot3(P[1].v, dir);
   if (fzero(dt) || dt < 0) return false;
   cross3(dir, P[0].v, P[1].v);
@@ -754,7 +744,7 @@ __device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& 
     return true;
   }
   normalize3(dir);
-  mpr_support_wave(A, B, dir, P[2]);
+  mpr_support_wave(c, A, B, dir, P[2]);
   dt = dot3(P[2].v, dir);
   if (fzero(dt) || dt < 0) return false;
   float va[3], vb[3];
@@ -768,7 +758,7 @@ __device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& 
   }
   for (int it = 0;; it++) {
     if (it > 1000) return false;
-    mpr_support_wave(A, B, dir, P[3]);
+    mpr_support_wave(c, A, B, dir, P[3]);
     dt = dot3(P[3].v, dir);
     if (fzero(dt) || dt < 0) return false;
     bool cont = false;
@@ -790,14 +780,16 @@ __device__ __forceinline__ bool mpr_wave(const Shape& A, const Shape& B, float& 
     portal_dir(P, dir);
     if (dot3(dir, P[1].v) >= 0) break;
     MPoint v4;
-    mpr_support_wave(A, B, dir, v4);
+    mpr_support_wave(c, A, B, dir, v4);
+    if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
     if (dot3(v4.v, dir) < 0 || portal_reach_tol(P, v4, dir, tol) || it > maxit) return false;
     expand_portal(P, v4);
   }
   for (int it = 0;; it++) {
     portal_dir(P, dir);
     MPoint v4;
-    mpr_support_wave(A, B, dir, v4);
+    mpr_support_wave(c, A, B, dir, v4);
+    if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
     if (portal_reach_tol(P, v4, dir, tol) || it > maxit) {
       float cl[3];
       float d2 = tri_origin_dist2(P[1].v, P[2].v, P[3].v, cl);
@@ -886,12 +878,27 @@ __device__ __forceinline__ void write_contact(float* con, int slot, const float*
   r[13] = __int_as_float(gp);
 }
 
-// Copies a mesh hull's vertices into LDS staging (returns the LDS pointer or the
-// global one when it does not fit).
-__device__ __forceinline__ const float* stage_hull(const float* src, int nvert, float* dst, int cap) {
-  if (3 * nvert > cap) return src;
-  for (int k = LANE; k < 3 * nvert; k += DX_WAVE) dst[k] = src[k];
-  return dst;
+// Copies a mesh hull's vertices into LDS at word offset `off` (8 global loads in
+// flight per lane).  The host sizes the staging area for the largest pair of hulls
+// among the model's geom pairs (dx_api.hip), so the support scan always reads LDS.
+__device__ __forceinline__ void stage_hull(const Ctx& c, Shape& s, int off) {
+  s.voff = off;
+  float* dst = c.S + off;
+  const DXG float* src = s.vert;
+  const int n = 3 * s.nvert;
+  for (int base = 0; base < n; base += 8 * DX_WAVE) {
+    float t[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      int k = base + u * DX_WAVE + LANE;
+      t[u] = src[k < n ? k : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      int k = base + u * DX_WAVE + LANE;
+      if (k < n) dst[k] = t[u];
+    }
+  }
 }
 
 // Narrowphase of one geom pair by the whole wave; appends up to 4 contacts.
@@ -932,19 +939,24 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
         float pos[3] = {v[0] - 0.5f * dist * n[0], v[1] - 0.5f * dist * n[1], v[2] - 0.5f * dist * n[2]};
         write_contact(con, ncon + rank, pos, n, dist, gp);
       }
+      stage_count(c, CNT_PLANE_BOX);
+      stage_mark(c, ST_NP_PRIM);
       return ncon + min(4, __popcll(mask));
     }
     Shape s;
     make_shape(c, g2, 0, s);
-    if (s.type == DXG_MESH) s.vert = stage_hull(s.vert, s.nvert, c.f(c.L.cj_val), 3 * DX_NCON_MAX * DX_DOFMAX);
+    if (s.type == DXG_MESH) stage_hull(c, s, c.L.stage);
     SYNC();
+    stage_mark(c, ST_NP_SETUP);
+    stage_count(c, CNT_PLANE_CONVEX);
     float nd[3] = {-n[0], -n[1], -n[2]};
     float sp[3];
-    support_wave(s, nd, sp);
+    support_wave(c, s, nd, sp);
     SYNC();
     float r[3];
     sub3(r, sp, pp);
     float dist = dot3(r, n);
+    stage_mark(c, ST_NP_PRIM);
     if (dist > margin) return ncon;
     if (LANE == 0 && ncon < DX_NCON_MAX) {
       float pos[3] = {sp[0] - 0.5f * dist * n[0], sp[1] - 0.5f * dist * n[1], sp[2] - 0.5f * dist * n[2]};
@@ -978,6 +990,8 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
     sub3(diff, q2, q1);
     float len = norm3(diff);
     float dist = len - r1 - r2;
+    stage_count(c, CNT_CAPSULE);
+    stage_mark(c, ST_NP_PRIM);
     if (dist > margin) return ncon;
     float n[3];
     if (len > 1e-20f) { n[0] = diff[0] / len; n[1] = diff[1] / len; n[2] = diff[2] / len; }
@@ -992,19 +1006,21 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
   Shape A, B;
   make_shape(c, g1, 0.5f * margin, A);
   make_shape(c, g2, 0.5f * margin, B);
-  float* stg = c.f(c.L.cj_val);
-  int cap = 3 * DX_NCON_MAX * DX_DOFMAX;
   int used = 0;
-  if (A.type == DXG_MESH && 3 * A.nvert <= cap) { A.vert = stage_hull(A.vert, A.nvert, stg, cap); used = 3 * A.nvert; }
-  if (B.type == DXG_MESH) B.vert = stage_hull(B.vert, B.nvert, stg + used, cap - used);
+  if (A.type == DXG_MESH) { stage_hull(c, A, c.L.stage); used = 3 * A.nvert; }
+  if (B.type == DXG_MESH) stage_hull(c, B, c.L.stage + used);
   SYNC();
+  stage_mark(c, ST_NP_SETUP);
+  stage_count(c, CNT_MPR);
   float depth, nrm[3], pos[3];
   int out = ncon;
-  if (mpr_wave(A, B, depth, nrm, pos)) {
+  if (mpr_wave(c, A, B, depth, nrm, pos)) {
+    stage_count(c, CNT_MPR_HIT);
     if (LANE == 0 && ncon < DX_NCON_MAX) write_contact(con, ncon, pos, nrm, margin - depth, gp);
     out = ncon + 1;
   }
   SYNC();
+  stage_mark(c, ST_NP_MPR);
   return out;
 }
 
@@ -1015,7 +1031,7 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
 __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
   const DevModel& m = c.m;
   int* I = c.I;
-  int* cand = (int*)c.f(c.L.H);  // H is free during collision
+  int* cand = (int*)c.f(c.L.cand);
   int cmax = c.L.cand_max;
   if (LANE == 0) { I[I_NCON] = 0; I[I_NCAND] = 0; }
   SYNC();
@@ -1172,8 +1188,10 @@ __device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float
   float R = fmaxf(1e-15f, (1 - imp) / imp * diag);
   R = fmaxf(1e-15f, R * rscale);
   c.f(c.L.efc_D)[r] = 1.0f / R;
-  c.f(c.L.efc_fl)[r] = floss;
-  c.f(c.L.efc_Rf)[r] = R * floss;
+  if (fric) {  // friction rows come first: efc_fl / efc_Rf hold only [0, nfric)
+    c.f(c.L.efc_fl)[r] = floss;
+    c.f(c.L.efc_Rf)[r] = R * floss;
+  }
   float viol = fric ? 0.f : pos - margin;
   c.f(c.L.efc_aref)[r] = -B * vel - K * imp * viol;
 }
@@ -1264,7 +1282,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   float* con = c.f(c.L.con);
   float* cdof = c.f(c.L.cdof);
   float* rcom = c.f(c.L.rcom);
-  int* cj_idx = (int*)c.f(c.L.cj_idx);
+  unsigned char* cj_idx = (unsigned char*)c.f(c.L.cj_idx);
   float* cj_val = c.f(c.L.cj_val);
   float* cq = c.f(c.L.cq);
   for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
@@ -1287,7 +1305,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       float t[3];
       cross3(t, cd, off);
       float jp[3] = {cd[3] + t[0], cd[4] + t[1], cd[5] + t[2]};
-      cj_idx[ci * DX_DOFMAX + nnz] = d;
+      cj_idx[ci * DX_DOFMAX + nnz] = (unsigned char)d;
       for (int k = 0; k < 3; k++) {
         float v = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
         cj_val[(ci * 3 + k) * DX_DOFMAX + nnz] = v;
@@ -1296,10 +1314,6 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       nnz++;
     }
     if (sup) I[I_OVF] |= 4;
-    for (int q = nnz; q < DX_DOFMAX; q++) {
-      cj_idx[ci * DX_DOFMAX + q] = -1;
-      for (int k = 0; k < 3; k++) cj_val[(ci * 3 + k) * DX_DOFMAX + q] = 0;
-    }
     for (int k = 0; k < 3; k++) cq[3 * ci + k] = vel[k];  // frame velocities (J qvel)
     r[14] = __int_as_float(nnz);
   }
@@ -1482,7 +1496,9 @@ __device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf,
 __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y, int n) {
   for (int i = LANE; i < n; i += DX_WAVE) {
     float s = 0;
-    for (int k = 0; k < n; k++) s += M[i * n + k] * x[k];
+    const float* row = M + ti(i);
+    for (int k = 0; k <= i; k++) s += row[k] * x[k];
+    for (int k = i + 1; k < n; k++) s += M[ti(k) + i] * x[k];
     y[i] = s;
   }
 }
@@ -1493,7 +1509,7 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
   const int* meta = (const int*)c.f(c.L.efc_meta);
-  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
   float* cq = c.f(c.L.cq);
   const float* con = c.f(c.L.con);
@@ -1543,7 +1559,8 @@ __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, con
   const float* jar = c.f(c.L.efc_jar);
   for (int r = LANE; r < nefc; r += DX_WAVE) {
     float f, hw;
-    g += row_cost(meta[r] & 15, D[r], fl[r], Rf[r], jar[r], f, hw);
+    bool fr = r < m.nfric;
+    g += row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r], f, hw);
   }
   return wave_sum(g);
 }
@@ -1599,7 +1616,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     cw[3 * ci] = fc[0]; cw[3 * ci + 1] = fc[1]; cw[3 * ci + 2] = fc[2];
   }
   SYNC();
-  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
   for (int d = LANE; d < nv; d += DX_WAVE) {
     float s = 0;
@@ -1653,7 +1670,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   const float* fl = c.f(c.L.efc_fl);
   const float* Rf = c.f(c.L.efc_Rf);
   const float* jar = c.f(c.L.efc_jar);
-  for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
+  for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
   SYNC();
   // unit rows (friction, joint limits) -> diagonal; lane per dof
   for (int d = LANE; d < nv; d += DX_WAVE) {
@@ -1668,7 +1685,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
       row_cost(type, D[r], 0, 0, jar[r], f, hw);
       s += hw;
     }
-    H[d * nv + d] += s;
+    H[ti(d) + d] += s;
   }
   SYNC();
   // tendon limit rows: dense outer products, lanes over entries
@@ -1680,15 +1697,13 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
     row_cost(type, D[r], 0, 0, jar[r], f, hw);
     if (hw == 0) continue;
     const float* tj = m.tendon_J + id * nv;
-    for (int k = LANE; k < nv * nv; k += DX_WAVE) {
-      int i = k / nv, j = k % nv;
-      H[k] += hw * tj[i] * tj[j];
-    }
+    for (int i = LANE; i < nv; i += DX_WAVE)
+      for (int j = 0; j <= i; j++) H[ti(i) + j] += hw * tj[i] * tj[j];
     SYNC();
   }
   // contacts: W = sum_active_edges D c c^T in frame space; H[idx_a][idx_b] += J^T W J
   const float* con = c.f(c.L.con);
-  const int* cj_idx = (const int*)c.f(c.L.cj_idx);
+  const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
   for (int ci = 0; ci < ncon; ci++) {
     const float* r = con + DX_CON_STRIDE * ci;
@@ -1717,6 +1732,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
     if (W[0] == 0 && W[4] == 0 && W[8] == 0) continue;
     for (int t = LANE; t < nnz * nnz; t += DX_WAVE) {
       int a = t / nnz, b = t % nnz;
+      if (b > a) continue;  // cj_idx ascending: lower triangle only
       float ja[3], jb[3];
       for (int k = 0; k < 3; k++) {
         ja[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + a];
@@ -1725,7 +1741,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
       float s = 0;
       for (int p = 0; p < 3; p++)
         for (int q = 0; q < 3; q++) s += ja[p] * W[3 * p + q] * jb[q];
-      H[cj_idx[ci * DX_DOFMAX + a] * nv + cj_idx[ci * DX_DOFMAX + b]] += s;
+      H[ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b]] += s;
     }
     SYNC();
   }
@@ -1762,7 +1778,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
       float j = jv[r];
       if (j == 0) continue;
       float f, hw;
-      row_cost(meta[r] & 15, D[r], fl[r], Rf[r], jar[r] + alpha * j, f, hw);
+      bool fr = r < m.nfric;
+      row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r] + alpha * j, f, hw);
       g -= f * j;
       h += hw * j * j;
     }
@@ -1781,7 +1798,8 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   int ch = 0;
   for (int r = LANE; r < nefc; r += DX_WAVE) {
     int type = meta[r] & 15;
-    ch += row_zone(type, Rf[r], jar[r]) != row_zone(type, Rf[r], jar[r] + alpha * jv[r]);
+    float rf = r < m.nfric ? Rf[r] : 0.f;
+    ch += row_zone(type, rf, jar[r]) != row_zone(type, rf, jar[r] + alpha * jv[r]);
   }
   *changed = wave_sum_i(ch);
   return alpha;
@@ -1834,10 +1852,14 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     build_hessian(c);
     stage_mark(c, ST_NEWTON_HESS);
     float* H = c.f(c.L.H);
-    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
     for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
     SYNC();
-    wave_chol_solve(H, dir, nv);
+    if (nv <= 32) {
+      reg_chol_solve32(H, nv, nullptr, 0.f, dir, H);
+    } else {
+      wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
+      wave_chol_solve(H, dir, nv);
+    }
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float alpha = line_search(c, qacc, Ma, dir, &changed);
@@ -1864,35 +1886,43 @@ __device__ __forceinline__ void solve(const Ctx& c) {
 // ------------------------------------------------------------------------ //
 // forward + Euler
 // ------------------------------------------------------------------------ //
-__device__ __forceinline__ void position_stage(const Ctx& c) {
+
+__device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
+  const DevModel& m = c.m;
+  int nv = m.nv;
+  // Stage order (LDS phases, see dx_api.hip layout): kinematics/com/crb and the
+  // velocity stage use the com temporaries; the smooth solve reuses them for its
+  // transpose; collision reuses them for candidates + hull staging; the constraint
+  // rows and contact jacobians overwrite those; the Newton Hessian overwrites the
+  // kinematic block.  Collision does not depend on velocities, so this order gives
+  // the same result as MuJoCo's mj_fwdPosition -> mj_fwdVelocity.
   kinematics(c);
   com_pos(c);
   stage_mark(c, ST_KIN);
   tendon_lengths(c);
   crb_mass(c);
   stage_mark(c, ST_CRB);
-  collision(c, 0, -1, -1);
-  make_constraint(c);
-  stage_mark(c, ST_CON);
-}
-
-__device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
-  const DevModel& m = c.m;
-  int nv = m.nv;
-  position_stage(c);
   velocity_stage(c, xfrc);
   stage_mark(c, ST_VEL);
-  // qacc_smooth = M^-1 qfrc_smooth via Cholesky in H
-  float* H = c.f(c.L.H);
+  // qacc_smooth = M^-1 qfrc_smooth (Cholesky)
+  float* H = c.f(c.L.tsm);
   const float* M = c.f(c.L.M);
-  for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
   float* a0 = c.f(c.L.qacc_smooth);
   const float* qs = c.f(c.L.qfrc_smooth);
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
-  SYNC();
-  wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
-  wave_chol_solve(H, a0, nv);
+  if (nv <= 32) {
+    SYNC();
+    reg_chol_solve32(M, nv, nullptr, 0.f, a0, H);
+  } else {
+    for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
+    SYNC();
+    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
+    wave_chol_solve(H, a0, nv);
+  }
   stage_mark(c, ST_SMOOTH);
+  collision(c, 0, -1, -1);
+  make_constraint(c);
+  stage_mark(c, ST_CON);
   solve(c);
   // qfrc_constraint = J^T f at the solution
   float* qc = c.f(c.L.qfrc_con);
@@ -1916,15 +1946,18 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
   if (m.any_damping) {
     float* H = c.f(c.L.H);
     const float* M = c.f(c.L.M);
-    for (int k = LANE; k < nv * nv; k += DX_WAVE) H[k] = M[k];
-    SYNC();
-    for (int i = LANE; i < nv; i += DX_WAVE) {
-      H[i * nv + i] += h * m.dof_damping[i];
-      acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
+    for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
+    if (nv <= 32) {
+      SYNC();
+      reg_chol_solve32(M, nv, m.dof_damping, h, acc, H);
+    } else {
+      for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
+      SYNC();
+      for (int i = LANE; i < nv; i += DX_WAVE) H[ti(i) + i] += h * m.dof_damping[i];
+      SYNC();
+      wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
+      wave_chol_solve(H, acc, nv);
     }
-    SYNC();
-    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
-    wave_chol_solve(H, acc, nv);
   } else {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
     SYNC();
@@ -1995,6 +2028,11 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
     vo[0] = cv[3] + wx[0]; vo[1] = cv[4] + wx[1]; vo[2] = cv[5] + wx[2];
     vo[3] = cv[0]; vo[4] = cv[1]; vo[5] = cv[2];
   }
+  // body poses out before the watch pass reuses the com-temporary LDS block
+  const float* xq = c.f(c.L.xquat);
+  for (int k = LANE; k < 3 * m.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * m.nbody + k] = xpos[k];
+  for (int k = LANE; k < 4 * m.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * m.nbody + k] = xq[k];
+  SYNC();
   if (B.watch_geom >= 0 && B.watch) {
     collision(c, 1, B.watch_geom, B.watch_body);
     int n = c.I[I_NCON];
@@ -2010,13 +2048,20 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
 // kernels
 // ------------------------------------------------------------------------ //
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
-extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
   extern __shared__ float smem[];
   int env = blockIdx.x;
   if (env >= B.nenv) return;
   int* I = (int*)(smem + L.ints);
-  Ctx c{m, L, smem, I, B.stage_acc};
-  if (B.stage_acc && LANE == 0) *(unsigned long long*)(I + 10) = __builtin_amdgcn_s_memtime();
+  Ctx c{m, L, smem, I, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr};
+  // Zero the whole per-env LDS block once: reg_chol_solve32 reads a few words past
+  // its packed triangles (padding lanes/columns, multiplied by exact zeros), and
+  // those must be finite rather than whatever an earlier workgroup left behind.
+#ifndef DX_SKIP_LDS_ZERO  // (defined only by the test that shows why this is needed)
+  for (int k = LANE; k < L.total; k += DX_WAVE) smem[k] = 0.f;
+#endif
+  SYNC();
+  if (c.stage_acc && LANE == 0) *(unsigned long long*)(I + 10) = __builtin_amdgcn_s_memtime();
   float* qpos = c.f(L.qpos);
   float* qvel = c.f(L.qvel);
   float* ctrl = c.f(L.ctrl);
@@ -2028,7 +2073,7 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
   }
   for (int i = LANE; i < m.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * m.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
-  {
+  if (m.nv > 32) {
     // lower-triangle index table for wave_cholesky: t -> (i << 8 | j), row-major
     unsigned short* tri = (unsigned short*)c.f(L.tri);
     int T = m.nv * (m.nv + 1) / 2;
@@ -2058,7 +2103,10 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
       B.dbg_qacc_smooth[(size_t)env * m.nv + i] = c.f(L.qacc_smooth)[i];
       B.dbg_qfrc_smooth[(size_t)env * m.nv + i] = c.f(L.qfrc_smooth)[i];
     }
-    for (int k = LANE; k < m.nv * m.nv; k += DX_WAVE) B.dbg_M[(size_t)env * m.nv * m.nv + k] = c.f(L.M)[k];
+    for (int k = LANE; k < m.nv * m.nv; k += DX_WAVE) {
+      int i = k / m.nv, j = k % m.nv;
+      B.dbg_M[(size_t)env * m.nv * m.nv + k] = c.f(L.M)[i >= j ? ti(i) + j : ti(j) + i];
+    }
     int n = I[I_NCON];
     for (int k = LANE; k < DX_NCON_MAX * 16; k += DX_WAVE) {
       int ci = k / 16, e = k % 16;
@@ -2090,10 +2138,6 @@ extern "C" __global__ void __launch_bounds__(64) dx_step_kernel(DevModel m, DevB
     B.qvel[(size_t)env * m.nv + i] = qvel[i];
     B.qacc_ws[(size_t)env * m.nv + i] = ws[i];
   }
-  float* xpos = c.f(L.xpos);
-  float* xquat = c.f(L.xquat);
-  for (int k = LANE; k < 3 * m.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * m.nbody + k] = xpos[k];
-  for (int k = LANE; k < 4 * m.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * m.nbody + k] = xquat[k];
   if (LANE == 0) B.time[env] = time;
 }
 

@@ -33,6 +33,7 @@ class Model:
         _lib.check(L.dx_model_sizes(self.ptr, sizes))
         (self.nq, self.nv, self.nbody, self.njnt, self.ngeom, self.nsite, self.nu,
          self.ntendon, self.nbpair, self.ngpair, self.ncon_max, self.nefc_max) = list(sizes)
+        self.lds_bytes = _lib.check(L.dx_model_lds_bytes(self.ptr))
 
     @staticmethod
     def from_file(path: str) -> "Model":

@@ -79,6 +79,8 @@ dx_model* dx_model_load(const void* blob, size_t nbytes);
 void dx_model_free(dx_model* m);
 /* Sizes: out[0..11] = nq nv nbody njnt ngeom nsite nu ntendon nbpair ngpair ncon_max nefc_max */
 int dx_model_sizes(const dx_model* m, int32_t out[12]);
+/* Bytes of LDS one environment (one 64-lane workgroup) of dx_step uses. */
+int dx_model_lds_bytes(const dx_model* m);
 /* Width (in 4-byte words per environment) of a dx_field. */
 int dx_field_width(const dx_model* m, int field);
 
@@ -172,6 +174,8 @@ int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
  * out[k] = summed s_memtime cycles of stage k over all envs since the last read. */
 int dx_stage_timing(dx_batch* b, int enable);
 int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n);
+/* Test hook: overwrites the LDS of every CU on `device` with NaN patterns. */
+int dx_debug_poison_lds(int32_t device);
 
 const char* dx_last_error(void);
 int dx_abi_version(void);

@@ -236,6 +236,24 @@ def test_deterministic_replay(gpu, reorient_setup):
         np.testing.assert_array_equal(a, b)
 
 
+def test_independent_of_stale_lds(gpu, reorient_setup):
+    """Results must not depend on LDS contents left by earlier workgroups: a run
+    after every CU's LDS was filled with NaN patterns is bit-identical."""
+    cm, xfrc, om, states, model = reorient_setup
+    L = _lib.load()
+    outs = []
+    for poison in (False, True):
+        phys = _load_states(gpu, model, xfrc, states)
+        if poison:
+            _lib.check(L.dx_debug_poison_lds(0))
+        phys.step(5)
+        q = phys.qpos
+        assert np.all(np.isfinite(q))
+        outs.append((q, phys.qvel, phys.get(_lib.NITER)))
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
 def test_env_step_rewards_match_host_restatement(gpu):
     from dexterity_amd import manipulation
     from oracle import task_ref

@@ -19,15 +19,17 @@ for i in range(10):
     env.step(env.sample_actions(i), device_action=True)
 env.physics.sync()
 _lib.check(L.dx_stage_timing(env.physics.ptr, 1))
-buf = (ctypes.c_uint64 * 24)()
-_lib.check(L.dx_stage_read(env.physics.ptr, buf, 24))
+buf = (ctypes.c_uint64 * _lib.NSTAGE)()
+_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE))
 t = time.perf_counter()
 for i in range(steps):
     env.step(env.sample_actions(100 + i), device_action=True)
 env.physics.sync()
 dt = time.perf_counter() - t
-_lib.check(L.dx_stage_read(env.physics.ptr, buf, 24))
+_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE))
 cyc = np.array(list(buf), dtype=np.float64)
+cnt = {name: cyc[k] / (B * steps * 5) for k, name in _lib.COUNTERS.items()}
+cyc[list(_lib.COUNTERS)] = 0
 tot = cyc.sum()
 per = cyc / (B * steps * 5)
 out = {}
@@ -35,6 +37,7 @@ print(f"B={B} steps={steps}: {dt/steps*1e3:.2f} ms/step; total cycles per env-su
 for k, name in enumerate(_lib.STAGES):
     print(f"  {name:20s} {100*cyc[k]/tot:6.2f}%  {per[k]:12.0f} cyc/env-substep")
     out[name] = per[k]
+print("narrowphase calls per env-substep", {k: round(v, 3) for k, v in cnt.items()})
 niter = env.physics.get(_lib.NITER)[:, 0]
 ncon = env.physics.get(_lib.NCON)[:, 0]
 print("niter hist", np.bincount(niter), "ncon mean", ncon.mean(), "max", ncon.max())
