@@ -109,23 +109,23 @@ def main():
 
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    from dexterity_amd import _lib, manipulation
+    from dexterity_amd import _lib, distributed, manipulation
 
     B = args.envs_per_gpu
-    env = manipulation.load("reorient", "state_dense", seed=12345 + rank, num_envs=B, device=local)
+    env = manipulation.load("reorient", "state_dense", seed=distributed.rank_seed(12345, rank), num_envs=B,
+                            device=local)
     L = _lib.load()
     obs_w = env.obs_dim + 3
     if world > 1:
-        shard = torch.empty((B, obs_w), dtype=torch.float32, device=f"cuda:{local}")
-        gathered = torch.empty((world * B, obs_w), dtype=torch.float32, device=f"cuda:{local}")
+        collator = distributed.OutputCollator(B, obs_w, device=f"cuda:{local}")
 
     def one_step(i):
         a = env.sample_actions(i)
         env.step(a, device_action=True)
         if world > 1:
-            _lib.check(L.dx_env_pack_outputs(env.ptr, ctypes.c_void_p(shard.data_ptr())))
+            _lib.check(L.dx_env_pack_outputs(env.ptr, ctypes.c_void_p(collator.shard.data_ptr())))
             env.physics.sync()
-            dist.all_gather_into_tensor(gathered, shard)
+            collator.gather()
 
     env.reset()
     for i in range(args.warmup):
@@ -148,9 +148,7 @@ def main():
     _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(kt), ctypes.byref(kn)))
     _lib.check(L.dx_timing_enable(env.physics.ptr, 0))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = distributed.max_over_ranks(elapsed, f"cuda:{local}")
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
     kernel_ms = kt.value / max(1, kn.value)

@@ -579,30 +579,43 @@ __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margi
 }
 
 struct MPoint { float v[3], a[3], b[3]; };
+// dst = c ? src : dst, as value selects (a conditional struct copy lets the optimizer
+// merge the copies into one with a selected destination pointer, which pins the
+// points in scratch memory).
+__device__ __forceinline__ void msel(MPoint& dst, const MPoint& src, bool c) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    dst.v[k] = c ? src.v[k] : dst.v[k];
+    dst.a[k] = c ? src.a[k] : dst.a[k];
+    dst.b[k] = c ? src.b[k] : dst.b[k];
+  }
+}
 
 __device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-10f; }
-__device__ __forceinline__ void portal_dir(const MPoint* P, float* dir) {
+// The portal points are four separate MPoint variables (not an array): an array of
+// structs with conditional element copies stayed an alloca in scratch memory.
+__device__ __forceinline__ void portal_dir(const MPoint& P1, const MPoint& P2, const MPoint& P3, float* dir) {
   float a[3], b[3];
-  sub3(a, P[2].v, P[1].v);
-  sub3(b, P[3].v, P[1].v);
+  sub3(a, P2.v, P1.v);
+  sub3(b, P3.v, P1.v);
   cross3(dir, a, b);
   normalize3(dir);
 }
-__device__ __forceinline__ bool portal_reach_tol(const MPoint* P, const MPoint& v4, const float* dir, float tol) {
+__device__ __forceinline__ bool portal_reach_tol(const MPoint& P1, const MPoint& P2, const MPoint& P3,
+                                                 const MPoint& v4, const float* dir, float tol) {
   float dv4 = dot3(v4.v, dir);
-  float d1 = dv4 - dot3(P[1].v, dir), d2 = dv4 - dot3(P[2].v, dir), d3 = dv4 - dot3(P[3].v, dir);
+  float d1 = dv4 - dot3(P1.v, dir), d2 = dv4 - dot3(P2.v, dir), d3 = dv4 - dot3(P3.v, dir);
   return fminf(d1, fminf(d2, d3)) <= tol;
 }
-__device__ __forceinline__ void expand_portal(MPoint* P, const MPoint& v4) {
+__device__ __forceinline__ void expand_portal(const MPoint& P0, MPoint& P1, MPoint& P2, MPoint& P3,
+                                              const MPoint& v4) {
   float v4v0[3];
-  cross3(v4v0, v4.v, P[0].v);
-  if (dot3(P[1].v, v4v0) > 0) {
-    if (dot3(P[2].v, v4v0) > 0) P[1] = v4;
-    else P[3] = v4;
-  } else {
-    if (dot3(P[3].v, v4v0) > 0) P[2] = v4;
-    else P[1] = v4;
-  }
+  cross3(v4v0, v4.v, P0.v);
+  bool c1 = dot3(P1.v, v4v0) > 0, c2 = dot3(P2.v, v4v0) > 0, c3 = dot3(P3.v, v4v0) > 0;
+  bool to1 = c1 ? c2 : !c3, to2 = !c1 && c3, to3 = c1 && !c2;
+  msel(P1, v4, to1);
+  msel(P2, v4, to2);
+  msel(P3, v4, to3);
 }
 __device__ __forceinline__ float tri_origin_dist2(const float* a, const float* b, const float* c, float* q) {
   float ab[3], ac[3], ap[3];
@@ -639,27 +652,29 @@ __device__ __forceinline__ float tri_origin_dist2(const float* a, const float* b
   for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
   return dot3(q, q);
 }
-__device__ __forceinline__ void find_pos(const MPoint* P, float* pos) {
+__device__ __forceinline__ void find_pos(const MPoint& P0, const MPoint& P1, const MPoint& P2, const MPoint& P3,
+                                         float* pos) {
   float dir[3];
-  portal_dir(P, dir);
-  float b[4], t[3];
-  cross3(t, P[2].v, P[3].v); b[0] = dot3(P[1].v, t);
-  cross3(t, P[2].v, P[0].v); b[1] = dot3(P[3].v, t);
-  cross3(t, P[1].v, P[3].v); b[2] = dot3(P[0].v, t);
-  cross3(t, P[1].v, P[0].v); b[3] = dot3(P[2].v, t);
-  float sum = b[0] + b[1] + b[2] + b[3];
+  portal_dir(P1, P2, P3, dir);
+  float b0, b1, b2, b3, t[3];
+  cross3(t, P2.v, P3.v); b0 = dot3(P1.v, t);
+  cross3(t, P2.v, P0.v); b1 = dot3(P3.v, t);
+  cross3(t, P1.v, P3.v); b2 = dot3(P0.v, t);
+  cross3(t, P1.v, P0.v); b3 = dot3(P2.v, t);
+  float sum = b0 + b1 + b2 + b3;
   if (sum <= 0) {
-    b[0] = 0;
-    cross3(t, P[3].v, dir); b[1] = dot3(P[2].v, t);
-    cross3(t, P[1].v, dir); b[2] = dot3(P[3].v, t);
-    cross3(t, P[2].v, dir); b[3] = dot3(P[1].v, t);
-    sum = b[1] + b[2] + b[3];
+    b0 = 0;
+    cross3(t, P3.v, dir); b1 = dot3(P2.v, t);
+    cross3(t, P1.v, dir); b2 = dot3(P3.v, t);
+    cross3(t, P2.v, dir); b3 = dot3(P1.v, t);
+    sum = b1 + b2 + b3;
   }
   float inv = 1.0f / sum;
-  float p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
-  for (int i = 0; i < 4; i++)
-    for (int k = 0; k < 3; k++) { p1[k] += b[i] * P[i].a[k]; p2[k] += b[i] * P[i].b[k]; }
-  for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p1[k] + p2[k]) * inv;
+  for (int k = 0; k < 3; k++) {
+    float p1 = b0 * P0.a[k] + b1 * P1.a[k] + b2 * P2.a[k] + b3 * P3.a[k];
+    float p2 = b0 * P0.b[k] + b1 * P1.b[k] + b2 * P2.b[k] + b3 * P3.b[k];
+    pos[k] = 0.5f * (p1 + p2) * inv;
+  }
 }
 
 // Wave-cooperative support point: every lane runs the same (uniform) MPR control
@@ -721,78 +736,79 @@ __device__ __forceinline__ void mpr_support_wave(const Ctx& c, const Shape& A, c
 __device__ __forceinline__ bool mpr_wave(const Ctx& c, const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
   const float tol = 1e-6f;
   const int maxit = 50;
-  MPoint P[4];
-  sub3(P[0].v, A.center, B.center);
-  for (int k = 0; k < 3; k++) { P[0].a[k] = A.center[k]; P[0].b[k] = B.center[k]; }
-  if (fzero(P[0].v[0]) && fzero(P[0].v[1]) && fzero(P[0].v[2])) P[0].v[0] += 1e-9f;
-  float dir[3] = {-P[0].v[0], -P[0].v[1], -P[0].v[2]};
+  MPoint P0, P1, P2, P3;
+  sub3(P0.v, A.center, B.center);
+  for (int k = 0; k < 3; k++) { P0.a[k] = A.center[k]; P0.b[k] = B.center[k]; }
+  if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-9f;
+  float dir[3] = {-P0.v[0], -P0.v[1], -P0.v[2]};
   normalize3(dir);
-  mpr_support_wave(c, A, B, dir, P[1]);
-  float dt = dot3(P[1].v, dir);
+  mpr_support_wave(c, A, B, dir, P1);
+  float dt = dot3(P1.v, dir);
   if (fzero(dt) || dt < 0) return false;
-  cross3(dir, P[0].v, P[1].v);
+  cross3(dir, P0.v, P1.v);
   if (fzero(dot3(dir, dir))) {
-    if (fzero(P[1].v[0]) && fzero(P[1].v[1]) && fzero(P[1].v[2])) {
+    if (fzero(P1.v[0]) && fzero(P1.v[1]) && fzero(P1.v[2])) {
       depth = 0;
       normal[0] = 0; normal[1] = 0; normal[2] = 1;
     } else {
-      depth = norm3(P[1].v);
-      for (int k = 0; k < 3; k++) normal[k] = P[1].v[k];
+      depth = norm3(P1.v);
+      for (int k = 0; k < 3; k++) normal[k] = P1.v[k];
       normalize3(normal);
     }
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P[1].a[k] + P[1].b[k]);
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P1.a[k] + P1.b[k]);
     return true;
   }
   normalize3(dir);
-  mpr_support_wave(c, A, B, dir, P[2]);
-  dt = dot3(P[2].v, dir);
+  mpr_support_wave(c, A, B, dir, P2);
+  dt = dot3(P2.v, dir);
   if (fzero(dt) || dt < 0) return false;
   float va[3], vb[3];
-  sub3(va, P[1].v, P[0].v);
-  sub3(vb, P[2].v, P[0].v);
+  sub3(va, P1.v, P0.v);
+  sub3(vb, P2.v, P0.v);
   cross3(dir, va, vb);
   normalize3(dir);
-  if (dot3(dir, P[0].v) > 0) {
-    MPoint t = P[1]; P[1] = P[2]; P[2] = t;
+  if (dot3(dir, P0.v) > 0) {
+    MPoint t = P1;
+    msel(P1, P2, true);
+    msel(P2, t, true);
     dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
   }
   for (int it = 0;; it++) {
     if (it > 1000) return false;
-    mpr_support_wave(c, A, B, dir, P[3]);
-    dt = dot3(P[3].v, dir);
+    mpr_support_wave(c, A, B, dir, P3);
+    dt = dot3(P3.v, dir);
     if (fzero(dt) || dt < 0) return false;
-    bool cont = false;
-    cross3(va, P[1].v, P[3].v);
-    dt = dot3(va, P[0].v);
-    if (dt < 0 && !fzero(dt)) { P[2] = P[3]; cont = true; }
-    if (!cont) {
-      cross3(va, P[3].v, P[2].v);
-      dt = dot3(va, P[0].v);
-      if (dt < 0 && !fzero(dt)) { P[1] = P[3]; cont = true; }
-    }
-    if (!cont) break;
-    sub3(va, P[1].v, P[0].v);
-    sub3(vb, P[2].v, P[0].v);
+    cross3(va, P1.v, P3.v);
+    dt = dot3(va, P0.v);
+    bool r2 = dt < 0 && !fzero(dt);
+    cross3(va, P3.v, P2.v);
+    dt = dot3(va, P0.v);
+    bool r1 = !r2 && dt < 0 && !fzero(dt);
+    msel(P2, P3, r2);
+    msel(P1, P3, r1);
+    if (!r1 && !r2) break;
+    sub3(va, P1.v, P0.v);
+    sub3(vb, P2.v, P0.v);
     cross3(dir, va, vb);
     normalize3(dir);
   }
   for (int it = 0;; it++) {
-    portal_dir(P, dir);
-    if (dot3(dir, P[1].v) >= 0) break;
+    portal_dir(P1, P2, P3, dir);
+    if (dot3(dir, P1.v) >= 0) break;
     MPoint v4;
     mpr_support_wave(c, A, B, dir, v4);
     if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
-    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P, v4, dir, tol) || it > maxit) return false;
-    expand_portal(P, v4);
+    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P1, P2, P3, v4, dir, tol) || it > maxit) return false;
+    expand_portal(P0, P1, P2, P3, v4);
   }
   for (int it = 0;; it++) {
-    portal_dir(P, dir);
+    portal_dir(P1, P2, P3, dir);
     MPoint v4;
     mpr_support_wave(c, A, B, dir, v4);
     if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
-    if (portal_reach_tol(P, v4, dir, tol) || it > maxit) {
+    if (portal_reach_tol(P1, P2, P3, v4, dir, tol) || it > maxit) {
       float cl[3];
-      float d2 = tri_origin_dist2(P[1].v, P[2].v, P[3].v, cl);
+      float d2 = tri_origin_dist2(P1.v, P2.v, P3.v, cl);
       depth = sqrtf(d2);
       if (depth > 1e-20f) {
         float s = 1.0f / depth;
@@ -800,10 +816,10 @@ __device__ __forceinline__ bool mpr_wave(const Ctx& c, const Shape& A, const Sha
       } else {
         normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
       }
-      find_pos(P, pos);
+      find_pos(P0, P1, P2, P3, pos);
       return true;
     }
-    expand_portal(P, v4);
+    expand_portal(P0, P1, P2, P3, v4);
   }
 }
 
