@@ -33,7 +33,7 @@ STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constra
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
           "qfrc_constraint", "euler", "observe", "io", "np_setup", "np_mpr", "np_prim")
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
-            26: "mpr_maxit"}
+            26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc"}
 NSTAGE = 32
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
 TASK_REORIENT = 0

@@ -348,10 +348,10 @@ extern "C" void dx_model_free(dx_model* m) {
   if (!m) return;
   for (auto& kv : m->dev_allocs) {
     int cur;
-    hipGetDevice(&cur);
-    hipSetDevice(kv.first);
-    for (void* p : kv.second) hipFree(p);
-    hipSetDevice(cur);
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(kv.first);
+    for (void* p : kv.second) (void)hipFree(p);
+    (void)hipSetDevice(cur);
   }
   delete m;
 }
@@ -519,10 +519,10 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
 
 extern "C" void dx_batch_destroy(dx_batch* b) {
   if (!b) return;
-  hipSetDevice(b->device);
-  hipStreamSynchronize(b->stream);
-  for (void* p : b->allocs) hipFree(p);
-  hipStreamDestroy(b->stream);
+  (void)hipSetDevice(b->device);
+  (void)hipStreamSynchronize(b->stream);
+  for (void* p : b->allocs) (void)hipFree(p);
+  (void)hipStreamDestroy(b->stream);
   delete b;
 }
 
@@ -861,14 +861,14 @@ static void timing_begin(dx_batch* b, hipEvent_t* start) {
   auto it = g_timing.find(b);
   *start = nullptr;
   if (it == g_timing.end() || !it->second.on) return;
-  hipEventCreate(start);
-  hipEventRecord(*start, b->stream);
+  (void)hipEventCreate(start);
+  (void)hipEventRecord(*start, b->stream);
 }
 static void timing_end(dx_batch* b, hipEvent_t start) {
   if (!start) return;
   hipEvent_t stop;
-  hipEventCreate(&stop);
-  hipEventRecord(stop, b->stream);
+  (void)hipEventCreate(&stop);
+  (void)hipEventRecord(stop, b->stream);
   g_timing[b].ev.emplace_back(start, stop);
 }
 
@@ -888,8 +888,8 @@ extern "C" int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count) {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
     tot += ms;
-    hipEventDestroy(p.first);
-    hipEventDestroy(p.second);
+    (void)hipEventDestroy(p.first);
+    (void)hipEventDestroy(p.second);
   }
   *total_ms = tot;
   *count = (int32_t)st.ev.size();

@@ -203,7 +203,7 @@ enum {
   ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO,
   ST_NP_SETUP, ST_NP_MPR, ST_NP_PRIM,
   CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
-  CNT_MPR_MAXIT  // event counters, not cycles
+  CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC  // event counters, not cycles
 };
 __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
   if (c.stage_acc && LANE == 0) {
@@ -213,8 +213,8 @@ __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
     *last = t;
   }
 }
-__device__ __forceinline__ void stage_count(const Ctx& c, int k) {
-  if (c.stage_acc && LANE == 0) c.stage_acc[k] += 1;
+__device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
+  if (c.stage_acc && LANE == 0) c.stage_acc[k] += n;
 }
 // misc int slots
 enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
@@ -1789,6 +1789,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   const float* jar = c.f(c.L.efc_jar);
   float lo = 0, hi = -1, alpha = 0, g0 = 0;
   for (int it = 0; it < 40; it++) {
+    stage_count(c, CNT_LS_IT);
     float g = 0, h = 0;
     for (int r = LANE; r < nefc; r += DX_WAVE) {
       float j = jv[r];
@@ -1855,7 +1856,10 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   }
   int it = 0;
   stage_mark(c, ST_NEWTON_EVAL);
+  stage_count(c, CNT_SOLVE);
+  stage_count(c, CNT_NEFC, nefc);
   for (; it < m.iterations; it++) {
+    stage_count(c, CNT_NEWTON_IT);
     jac_t_force(c, grad);  // grad <- J^T f
     float gn = 0;
     for (int i = LANE; i < nv; i += DX_WAVE) {
