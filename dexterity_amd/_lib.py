@@ -27,7 +27,7 @@ EXPORTS = (
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
-    "dx_debug_poison_lds",
+    "dx_debug_poison_lds", "dx_hull_support",
 )
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
@@ -61,6 +61,7 @@ def load(path: str = LIB_PATH):
     L.dx_model_sizes.argtypes = [vp, ctypes.POINTER(i32)]
     L.dx_model_lds_bytes.argtypes = [vp]
     L.dx_field_width.argtypes = [vp, ctypes.c_int]
+    L.dx_hull_support.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32)]
     L.dx_batch_create.restype = vp
     L.dx_batch_create.argtypes = [vp, i32, i32]
     L.dx_batch_destroy.argtypes = [vp]

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
@@ -109,6 +110,116 @@ static void quat2mat_h(float* R, const float* q) {
   R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
   R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
   R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+
+
+// ------------------------------------------------------------------------ //
+// direction-binned hulls (support-point acceleration, exact)
+// ------------------------------------------------------------------------ //
+// A hull with more than 64 vertices gets a cube map of n x n cells per face over
+// the local direction sphere (cell rule: dx_step.hip hull_cell).  Each cell stores
+// the vertices that can be a support point for some direction in the cell, sorted
+// by vertex index and padded to the mesh's capacity `cap` (a multiple of 16, at
+// most 64), so the device scans one cell with one 16-lane pass and one memory round
+// trip.  A vertex is dropped only if a single other vertex beats it by more than
+// 1e-5 R at all four corner directions of the (slightly enlarged) cell, hence at
+// every direction of the cell: every maximiser -- ties included -- of every
+// direction in the cell is kept, and the lowest-index maximiser over the cell's list
+// is the vertex the full scan returns (the oracle's rule).
+static void cell_corners(int face, int n, int iu, int iv, double eps, double c[4][3]) {
+  int ax = face >> 1;
+  double sgn = (face & 1) ? -1.0 : 1.0;
+  double u0 = -1 + 2.0 * iu / n - eps, u1 = -1 + 2.0 * (iu + 1) / n + eps;
+  double v0 = -1 + 2.0 * iv / n - eps, v1 = -1 + 2.0 * (iv + 1) / n + eps;
+  double us[4] = {u0, u1, u1, u0}, vs[4] = {v0, v0, v1, v1};
+  for (int k = 0; k < 4; k++) {
+    c[k][ax] = sgn;
+    c[k][(ax + 1) % 3] = us[k];
+    c[k][(ax + 2) % 3] = vs[k];
+  }
+}
+
+static void hull_cell_candidates(const std::vector<double>& V, int nv, double R, const double c[4][3],
+                                 std::vector<int>& out) {
+  std::vector<double> D(4 * nv), S(nv);
+  for (int i = 0; i < nv; i++) {
+    for (int k = 0; k < 4; k++)
+      D[4 * i + k] = V[3 * i] * c[k][0] + V[3 * i + 1] * c[k][1] + V[3 * i + 2] * c[k][2];
+    S[i] = D[4 * i] + D[4 * i + 1] + D[4 * i + 2] + D[4 * i + 3];
+  }
+  std::vector<int> order(nv);
+  for (int i = 0; i < nv; i++) order[i] = i;
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return S[a] > S[b]; });
+  double cn[4];
+  for (int k = 0; k < 4; k++) cn[k] = std::sqrt(c[k][0] * c[k][0] + c[k][1] * c[k][1] + c[k][2] * c[k][2]);
+  const double tol = 1e-5 * R;
+  out.clear();
+  for (int v = 0; v < nv; v++) {
+    bool dominated = false;
+    for (int w : order) {
+      if (S[w] <= S[v]) break;  // a dominator beats v at every corner, so also in the sum
+      bool all = true;
+      for (int k = 0; k < 4 && all; k++) all = D[4 * w + k] - D[4 * v + k] > tol * cn[k];
+      if (all) { dominated = true; break; }
+    }
+    if (!dominated) out.push_back(v);
+  }
+}
+
+static void build_hull_bins(dx_model* m) {
+  auto& mv = m->hf["mesh_vert"];
+  auto& adr = m->hi["mesh_vertadr"];
+  auto& num = m->hi["mesh_vertnum"];
+  int nmesh = (int)num.size();
+  std::vector<int> bn(std::max(nmesh, 1), 0), bcap(std::max(nmesh, 1), 0), badr(std::max(nmesh, 1), 0);
+  std::vector<float> b4;
+  static const int kN[] = {4, 6, 8, 12, 16};
+  for (int i = 0; i < nmesh; i++) {
+    int nv = num[i];
+    if (nv <= 64) continue;
+    std::vector<double> V(3 * nv);
+    double R = 0;
+    for (int j = 0; j < nv; j++) {
+      for (int k = 0; k < 3; k++) V[3 * j + k] = mv[3 * (adr[i] + j) + k];
+      R = std::max(R, std::sqrt(V[3 * j] * V[3 * j] + V[3 * j + 1] * V[3 * j + 1] + V[3 * j + 2] * V[3 * j + 2]));
+    }
+    for (int n : kN) {
+      std::vector<std::vector<int>> cells(6 * n * n);
+      int cap = 0;
+      for (int f = 0; f < 6 && cap <= 64; f++)
+        for (int iu = 0; iu < n && cap <= 64; iu++)
+          for (int iv = 0; iv < n && cap <= 64; iv++) {
+            double c[4][3];
+            cell_corners(f, n, iu, iv, 1e-3, c);
+            auto& L = cells[(f * n + iu) * n + iv];
+            hull_cell_candidates(V, nv, R, c, L);
+            cap = std::max(cap, (int)L.size());
+          }
+      if (cap > 64) continue;
+      cap = (cap + 15) & ~15;
+      bn[i] = n;
+      bcap[i] = cap;
+      badr[i] = (int)(b4.size() / 4);
+      for (auto& L : cells) {
+        for (int s = 0; s < cap; s++) {
+          float e[4] = {0.f, 0.f, 0.f, 0.f};
+          int idx = -1;
+          if (s < (int)L.size()) {
+            idx = L[s];
+            for (int k = 0; k < 3; k++) e[k] = mv[3 * (adr[i] + idx) + k];
+          }
+          memcpy(&e[3], &idx, 4);
+          b4.insert(b4.end(), e, e + 4);
+        }
+      }
+      break;
+    }
+  }
+  if (b4.empty()) b4.assign(4, 0.f);
+  m->hf["mesh_bin4"] = b4;
+  m->hi["mesh_binn"] = bn;
+  m->hi["mesh_bincap"] = bcap;
+  m->hi["mesh_binadr"] = badr;
 }
 
 static const char* kFloatArrays[] = {
@@ -210,6 +321,49 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   mats("body_iquat", "body_imat", nb);
   mats("geom_quat", "geom_mat", d.ngeom);
   mats("site_quat", "site_mat", d.nsite);
+  {
+    auto& mv = m->hf["mesh_vert"];
+    std::vector<float> v4(4 * std::max<size_t>(mv.size() / 3, 1), 0.f);
+    for (size_t i = 0; i < mv.size() / 3; i++)
+      for (int k = 0; k < 3; k++) v4[4 * i + k] = mv[3 * i + k];
+    m->hf["mesh_vert4"] = v4;
+  }
+  build_hull_bins(m);
+  // per-geom shape records and per-pair records for the narrowphase setup: one or two
+  // memory round trips instead of a chain of dependent table lookups
+  {
+    auto& gt = m->hi["geom_type"]; auto& gb = m->hi["geom_bodyid"]; auto& gdid = m->hi["geom_dataid"];
+    auto& gs = m->hf["geom_size"]; auto& gp = m->hf["geom_pos"]; auto& gm = m->hf["geom_mat"];
+    auto& gc = m->hf["geom_center"];
+    auto& vadr = m->hi["mesh_vertadr"]; auto& vnum = m->hi["mesh_vertnum"];
+    auto& bn = m->hi["mesh_binn"]; auto& bc = m->hi["mesh_bincap"]; auto& ba = m->hi["mesh_binadr"];
+    int ng = (int)gt.size();
+    std::vector<float> rec(32 * std::max(ng, 1), 0.f);
+    for (int g = 0; g < ng; g++) {
+      float* r = rec.data() + 32 * g;
+      int iv[8] = {gt[g], gb[g], 0, 0, 0, 0, 0, 0};
+      if (gt[g] == DXG_MESH) {
+        int mid = gdid[g];
+        iv[2] = vnum[mid]; iv[3] = bn[mid]; iv[4] = bc[mid]; iv[5] = vadr[mid]; iv[6] = ba[mid];
+      }
+      memcpy(r, iv, sizeof(iv));
+      for (int k = 0; k < 3; k++) { r[8 + k] = gs[3 * g + k]; r[12 + k] = gp[3 * g + k]; r[25 + k] = gc[3 * g + k]; }
+      for (int k = 0; k < 9; k++) r[16 + k] = gm[9 * g + k];
+    }
+    m->hf["geom_rec"] = rec;
+    auto& pg = m->hi["gpair_geom"]; auto& pm = m->hf["gpair_margin"];
+    int np = (int)pm.size();
+    std::vector<float> prec(4 * std::max(np, 1), 0.f);
+    for (int k = 0; k < np; k++) {
+      int g1 = pg[2 * k], g2 = pg[2 * k + 1];
+      int prim = gt[g1] == DXG_PLANE || (gt[g1] == DXG_CAPSULE && gt[g2] == DXG_CAPSULE);
+      int iv[2] = {g1, g2};
+      memcpy(&prec[4 * k], iv, 8);
+      prec[4 * k + 2] = pm[k];
+      memcpy(&prec[4 * k + 3], &prim, 4);
+    }
+    m->hf["gpair_rec"] = prec;
+  }
   // geom bounding spheres with centres in the body frame (mid-phase cull)
   {
     std::vector<float> gb(4 * std::max(d.ngeom, 1), 0.f);
@@ -311,18 +465,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   int end = off;
   L.tsm = B0;
   end = std::max(end, B0 + r4(ntri));
-  // staging must hold the two largest hulls of any geom pair
-  auto& gtype = m->hi["geom_type"];
-  auto& gdata = m->hi["geom_dataid"];
-  auto& mvn = m->hi["mesh_vertnum"];
-  auto& gpg = m->hi["gpair_geom"];
-  auto hullw = [&](int g) { return gtype[g] == DXG_MESH ? 3 * mvn[gdata[g]] : 0; };
-  int stage_need = 0;
-  for (int p = 0; p < d.ngpair; p++) stage_need = std::max(stage_need, hullw(gpg[2 * p]) + hullw(gpg[2 * p + 1]));
   L.cand_max = 768;
   L.cand = B0;
-  L.stage = B0 + L.cand_max;
-  end = std::max(end, L.stage + r4(std::max(stage_need, 1)));
+  end = std::max(end, L.cand + L.cand_max);
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_jar = take(L.nefc_max); L.efc_jv = take(L.nefc_max);
@@ -333,7 +478,6 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, off);
   L.H = U0;
   L.total = end;
-  L.stage_cap = L.total - L.stage;
   m->ncon_max = DX_NCON_MAX;
   m->nefc_max = L.nefc_max;
   if (L.total * 4 > 160 * 1024) {
@@ -362,6 +506,51 @@ extern "C" int dx_model_sizes(const dx_model* m, int32_t out[12]) {
   int v[12] = {d.nq, d.nv, d.nbody, d.njnt, d.ngeom, d.nsite, d.nu, d.ntendon, d.nbpair, d.ngpair,
                m->ncon_max, m->nefc_max};
   memcpy(out, v, sizeof(v));
+  return 0;
+}
+
+// Host twin of the device's binned support scan (test hook): the vertex index the
+// kernel's support_grp returns for hull `mesh` along local direction dir, plus the
+// mesh's cube-map resolution and cell capacity (0, 0 when the hull is not binned).
+extern "C" int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[3], int32_t info[3]) {
+  if (!m || !dir || !info) return fail(DX_EINVAL, "null argument");
+  auto& num = m->hi.at("mesh_vertnum");
+  if (mesh < 0 || mesh >= (int)num.size()) return fail(DX_EINVAL, "mesh out of range");
+  int n = m->hi.at("mesh_binn")[mesh], cap = m->hi.at("mesh_bincap")[mesh];
+  const float* b4 = m->hf.at("mesh_bin4").data() + 4 * (size_t)m->hi.at("mesh_binadr")[mesh];
+  const float* mv = m->hf.at("mesh_vert").data() + 3 * (size_t)m->hi.at("mesh_vertadr")[mesh];
+  int best = -1;
+  float bd = -3.0e38f;
+  int cell = -1;
+  if (n > 0) {
+    float ax0 = std::fabs(dir[0]), ax1 = std::fabs(dir[1]), ax2 = std::fabs(dir[2]);
+    int ax = (ax0 >= ax1 && ax0 >= ax2) ? 0 : (ax1 >= ax2 ? 1 : 2);
+    float a = dir[ax], u = dir[(ax + 1) % 3], v = dir[(ax + 2) % 3];
+    if (std::fabs(a) > 1e-30f) {
+      float inv = 1.0f / std::fabs(a);
+      int iu = std::min(std::max((int)((u * inv + 1.0f) * 0.5f * (float)n), 0), n - 1);
+      int iv = std::min(std::max((int)((v * inv + 1.0f) * 0.5f * (float)n), 0), n - 1);
+      cell = ((2 * ax + (a < 0 ? 1 : 0)) * n + iu) * n + iv;
+    }
+  }
+  if (cell >= 0) {
+    for (int s = 0; s < cap; s++) {
+      const float* e = b4 + 4 * ((size_t)cell * cap + s);
+      int idx;
+      memcpy(&idx, e + 3, 4);
+      if (idx < 0) continue;
+      float d = e[0] * dir[0] + e[1] * dir[1] + e[2] * dir[2];
+      if (d > bd) { bd = d; best = idx; }
+    }
+  } else {
+    for (int i = 0; i < num[mesh]; i++) {
+      float d = mv[3 * i] * dir[0] + mv[3 * i + 1] * dir[1] + mv[3 * i + 2] * dir[2];
+      if (d > bd) { bd = d; best = i; }
+    }
+  }
+  info[0] = best;
+  info[1] = n;
+  info[2] = cap;
   return 0;
 }
 
@@ -424,7 +613,9 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UF(dof_armature); UF(dof_damping); UF(dof_frictionloss); UF(dof_solref); UF(dof_solimp); UF(dof_invweight0);
   UI(geom_type); UI(geom_bodyid); UI(geom_dataid);
   UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere); UF(geom_bsphere_b); UF(geom_obb_b);
-  UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert);
+  UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert4);
+  UI(mesh_binn); UI(mesh_bincap); UI(mesh_binadr); UF(mesh_bin4);
+  UF(geom_rec); UF(gpair_rec);
   UI(site_bodyid); UF(site_pos); UF(site_mat);
   UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
   UF(tendon_range); UF(tendon_margin); UF(tendon_solref); UF(tendon_solimp); UF(tendon_invweight0);

@@ -48,7 +48,15 @@ struct DevModel {
   const DXG int *geom_type, *geom_bodyid, *geom_dataid;
   const DXG float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere, *geom_bsphere_b, *geom_obb_b;
   const DXG int *mesh_vertadr, *mesh_vertnum;
-  const DXG float* mesh_vert;
+  const DXG float4* mesh_vert4;  // hull vertices padded to (x, y, z, 0)
+  // direction-binned hulls (dx_api.hip build_hull_bins): cube map of binn x binn cells
+  // per face, bincap float4 (x, y, z, vertex index bits; -1 = padding) per cell
+  const DXG int *mesh_binn, *mesh_bincap, *mesh_binadr;
+  const DXG float4* mesh_bin4;
+  // narrowphase setup records: geom_rec [ngeom][8] float4 = {type, body, nvert, bin_n,
+  // bin_cap, vert4 offset, bin4 offset, -}{size, -}{pos, -}{mat 9, center 3, -};
+  // gpair_rec [ngpair] = {g1, g2, margin, primitive-pair flag}
+  const DXG float4 *geom_rec, *gpair_rec;
   // sites
   const DXG int* site_bodyid;
   const DXG float *site_pos, *site_mat;
@@ -92,8 +100,8 @@ struct Lds {
   int tri;   // ushort lower-triangle index table (nv > 32 only)
   int ints;  // misc int scalars
   int tsm;   // smooth-solve Cholesky transpose
-  int cand, stage;  // collision candidate lists, hull staging
-  int nefc_max, cand_max, stage_cap;
+  int cand;  // collision candidate lists
+  int nefc_max, cand_max;
   int total;
 };
 

@@ -84,16 +84,24 @@ __device__ __forceinline__ int wave_argmax_first(float best, int bi) {
   return wave_min_i(best == vmax ? bi : 0x7fffffff);
 }
 
-// exclusive prefix sum over lanes
-__device__ __forceinline__ int wave_excl_scan(int v) {
-  int x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int y = __shfl_up(x, o, 64);
-    if (LANE >= o) x += y;
-  }
-  return x - v;
+// Inclusive prefix sum over the wave by DPP: Hillis-Steele within each 16-lane row
+// (row_shr 1, 2, 4, 8 with zero fill), then row_bcast:15 / row_bcast:31 carry the
+// row totals upwards.  No LDS round trip.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i0(int x) {  // lanes without a source read 0
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xF, false);
 }
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += dpp_i0<0x111, 0xF>(x);  // row_shr:1
+  x += dpp_i0<0x112, 0xF>(x);  // row_shr:2
+  x += dpp_i0<0x114, 0xF>(x);  // row_shr:4
+  x += dpp_i0<0x118, 0xF>(x);  // row_shr:8
+  x += dpp_i0<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_i0<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+// exclusive prefix sum over lanes
+__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan(v) - v; }
 
 // ------------------------------------------------------------------------ //
 // small math
@@ -543,9 +551,10 @@ __device__ __forceinline__ void reg_chol_solve32(const float* A, int n, const DX
 // ------------------------------------------------------------------------ //
 struct Shape {
   int type, nvert;
-  int voff;  // LDS word offset of the staged hull vertices (meshes)
+  int bin_n, bin_cap;  // direction-binned hull (bin_n > 0), see dx_api.hip build_hull_bins
   float pos[3], mat[9], size[3], center[3], margin;
-  const DXG float* vert;  // hull vertices in global memory
+  const DXG float4* vert4;  // hull vertices (x, y, z, 0) in global memory (L2-resident)
+  const DXG float4* bin4;   // this hull's cells
 };
 
 __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
@@ -564,13 +573,18 @@ __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margi
   s.type = m.geom_type[g];
   geom_pose(c, g, s.pos, s.mat);
   s.size[0] = m.geom_size[3 * g]; s.size[1] = m.geom_size[3 * g + 1]; s.size[2] = m.geom_size[3 * g + 2];
-  s.vert = nullptr;
+  s.vert4 = m.mesh_vert4;
+  s.bin4 = m.mesh_bin4;
   s.nvert = 0;
-  s.voff = 0;
+  s.bin_n = 0;
+  s.bin_cap = 0;
   if (s.type == DXG_MESH) {
     int mid = m.geom_dataid[g];
-    s.vert = m.mesh_vert + 3 * m.mesh_vertadr[mid];
+    s.vert4 = m.mesh_vert4 + m.mesh_vertadr[mid];
     s.nvert = m.mesh_vertnum[mid];
+    s.bin_n = m.mesh_binn[mid];
+    s.bin_cap = m.mesh_bincap[mid];
+    s.bin4 = m.mesh_bin4 + m.mesh_binadr[mid];
   }
   float t[3];
   matvec3(t, s.mat, m.geom_center + 3 * g);
@@ -677,42 +691,65 @@ __device__ __forceinline__ void find_pos(const MPoint& P0, const MPoint& P1, con
   }
 }
 
-// Wave-cooperative support point: every lane runs the same (uniform) MPR control
-// flow; for mesh hulls the 64 lanes scan the vertices (staged in LDS) and an
-// argmax reduction picks the first maximal vertex, as the serial loop would.
-__device__ __forceinline__ void support_wave(const Ctx& c, const Shape& s, const float* dir, float* out) {
-  float ld[3];
-  mattvec3(ld, s.mat, dir);
-  float lp[3] = {0, 0, 0};
-  if (s.type == DXG_MESH) {
-    // lane t scans vertices t, t+64, ... (4 loads in flight per pass); strict '>'
-    // keeps each lane's first maximum, the reduction the lowest index among lanes.
-    const float* V = c.S + s.voff;
-    const int nvert = s.nvert;
-    float best = -3.0e38f;
-    int bi = 0x7fffffff;
-    for (int base = 0; base < nvert; base += 4 * DX_WAVE) {
-      float d[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        int i = base + u * DX_WAVE + LANE;
-        const float* v = V + 3 * (i < nvert ? i : 0);
-        float dd = v[0] * ld[0] + v[1] * ld[1] + v[2] * ld[2];
-        d[u] = i < nvert ? dd : -3.0e38f;
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        if (d[u] > best) { best = d[u]; bi = base + u * DX_WAVE + LANE; }
-    }
-    bi = wave_argmax_first(best, bi);
-    lp[0] = V[3 * bi]; lp[1] = V[3 * bi + 1]; lp[2] = V[3 * bi + 2];
-  } else if (s.type == DXG_BOX) {
+// Shape of geom g from its record (two memory round trips: record, then body pose in LDS).
+__device__ __forceinline__ void make_shape_rec(const Ctx& c, int g, float half_margin, Shape& s) {
+  const DevModel& m = c.m;
+  const DXG float4* r = m.geom_rec + 8 * g;
+  float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4], r5 = r[5], r6 = r[6];
+  s.type = __float_as_int(r0.x);
+  int b = __float_as_int(r0.y);
+  s.nvert = __float_as_int(r0.z);
+  s.bin_n = __float_as_int(r0.w);
+  s.bin_cap = __float_as_int(r1.x);
+  s.vert4 = m.mesh_vert4 + __float_as_int(r1.y);
+  s.bin4 = m.mesh_bin4 + __float_as_int(r1.z);
+  s.size[0] = r2.x; s.size[1] = r2.y; s.size[2] = r2.z;
+  const float gpos[3] = {r3.x, r3.y, r3.z};
+  const float gmat[9] = {r4.x, r4.y, r4.z, r4.w, r5.x, r5.y, r5.z, r5.w, r6.x};
+  const float gc[3] = {r6.y, r6.z, r6.w};
+  const float* xp = c.f(c.L.xpos) + 3 * b;
+  const float* xm = c.f(c.L.xmat) + 9 * b;
+  float t[3];
+  matvec3(t, xm, gpos);
+  s.pos[0] = xp[0] + t[0]; s.pos[1] = xp[1] + t[1]; s.pos[2] = xp[2] + t[2];
+  matmul3(s.mat, xm, gmat);
+  matvec3(t, s.mat, gc);
+  s.center[0] = s.pos[0] + t[0]; s.center[1] = s.pos[1] + t[1]; s.center[2] = s.pos[2] + t[2];
+  s.margin = half_margin;
+}
+
+// Narrowphase runs four candidate pairs per wave, one per 16-lane group (a DPP
+// row).  Every lane of a group runs the same MPR control flow for its pair; the
+// groups diverge only through the exec mask.
+#define SL (LANE & 15)
+__device__ __forceinline__ float row_max_f(float m) {
+  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));   // quad_perm [1,0,3,2]
+  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));   // quad_perm [2,3,0,1]
+  m = fmaxf(m, dpp_f<0x141, 0xF>(m));  // row_half_mirror
+  m = fmaxf(m, dpp_f<0x140, 0xF>(m));  // row_mirror
+  return m;
+}
+__device__ __forceinline__ int row_min_i(int m) {
+  m = min(m, dpp_i<0xB1, 0xF>(m));
+  m = min(m, dpp_i<0x4E, 0xF>(m));
+  m = min(m, dpp_i<0x141, 0xF>(m));
+  m = min(m, dpp_i<0x140, 0xF>(m));
+  return m;
+}
+
+// Local-frame support of a primitive (box, sphere, capsule) in local direction ld.
+__device__ __forceinline__ void support_prim(const Shape& s, const float* ld, float* lp) {
+  lp[0] = lp[1] = lp[2] = 0;
+  if (s.type == DXG_BOX) {
     for (int k = 0; k < 3; k++) lp[k] = ld[k] >= 0 ? s.size[k] : -s.size[k];
   } else if (s.type == DXG_SPHERE || s.type == DXG_CAPSULE) {
     float n = norm3(ld);
     if (n > 1e-20f) { float sc = s.size[0] / n; lp[0] = ld[0] * sc; lp[1] = ld[1] * sc; lp[2] = ld[2] * sc; }
     if (s.type == DXG_CAPSULE) lp[2] += ld[2] >= 0 ? s.size[1] : -s.size[1];
   }
+}
+// local support -> world point, plus the shape's half margin along dir
+__device__ __forceinline__ void support_world(const Shape& s, const float* lp, const float* dir, float* out) {
   matvec3(out, s.mat, lp);
   out[0] += s.pos[0]; out[1] += s.pos[1]; out[2] += s.pos[2];
   if (s.margin > 0) {
@@ -723,104 +760,257 @@ __device__ __forceinline__ void support_wave(const Ctx& c, const Shape& s, const
     }
   }
 }
-
-__device__ __forceinline__ void mpr_support_wave(const Ctx& c, const Shape& A, const Shape& B, const float* dir, MPoint& p) {
-  stage_count(c, CNT_SUPPORT);
-  float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  support_wave(c, A, dir, p.a);
-  support_wave(c, B, nd, p.b);
-  sub3(p.v, p.a, p.b);
+// Hull scan state of one lane: its first maximal slot (strict '>') and coordinates.
+struct HullBest {
+  float d, x, y, z;
+  int i;
+};
+__device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i, bool ok) {
+  bool t = ok && d > h.d;
+  h.d = t ? d : h.d;
+  h.i = t ? i : h.i;
+  h.x = t ? v.x : h.x;
+  h.y = t ? v.y : h.y;
+  h.z = t ? v.z : h.z;
+}
+// Group reduction: lowest slot among the lanes holding the maximum.  Slots are in
+// ascending vertex-index order (whole hull, or a binned cell's sorted list), so this
+// is the vertex the oracle's serial scan returns; its coordinates come from the lane
+// that scanned it (slot s is scanned by group lane s % 16) through ds_bpermute.
+__device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
+  float vmax = row_max_f(h.d);
+  int bi = row_min_i(h.d == vmax ? h.i : 0x7fffffff);
+  int src = (LANE & 48) | (bi & 15);
+  lp[0] = __shfl(h.x, src, 64);
+  lp[1] = __shfl(h.y, src, 64);
+  lp[2] = __shfl(h.z, src, 64);
+}
+// Cube-map cell of local direction ld (host twin: dx_api.hip cell_corners).  Returns
+// -1 for a zero direction (then the whole hull is scanned, as the oracle does).
+__device__ __forceinline__ int hull_cell(const float* ld, int n) {
+  float ax0 = fabsf(ld[0]), ax1 = fabsf(ld[1]), ax2 = fabsf(ld[2]);
+  int ax = (ax0 >= ax1 && ax0 >= ax2) ? 0 : (ax1 >= ax2 ? 1 : 2);
+  float a = ax == 0 ? ld[0] : (ax == 1 ? ld[1] : ld[2]);
+  float u = ax == 0 ? ld[1] : (ax == 1 ? ld[2] : ld[0]);
+  float v = ax == 0 ? ld[2] : (ax == 1 ? ld[0] : ld[1]);
+  float aa = fabsf(a);
+  if (!(aa > 1e-30f)) return -1;
+  float inv = 1.0f / aa;
+  int iu = (int)((u * inv + 1.0f) * 0.5f * (float)n);
+  int iv = (int)((v * inv + 1.0f) * 0.5f * (float)n);
+  iu = min(max(iu, 0), n - 1);
+  iv = min(max(iv, 0), n - 1);
+  int face = 2 * ax + (a < 0 ? 1 : 0);
+  return (face * n + iu) * n + iv;
+}
+// The slots a support scan of `s` along local direction ld must visit.
+__device__ __forceinline__ void hull_span(const Shape& s, const float* ld, const DXG float4*& p, int& cnt) {
+  p = s.vert4;
+  cnt = s.nvert;
+  if (s.bin_n > 0) {
+    int cell = hull_cell(ld, s.bin_n);
+    if (cell >= 0) {
+      p = s.bin4 + cell * s.bin_cap;
+      cnt = s.bin_cap;
+    }
+  }
 }
 
-// MPR penetration on A - B with wave-parallel support (see oracle mpr_penetration).
-__device__ __forceinline__ bool mpr_wave(const Ctx& c, const Shape& A, const Shape& B, float& depth, float* normal, float* pos) {
+// Support points of A along dir and of B along -dir, by one 16-lane group.  Both
+// hulls (or their direction cells, <= 64 slots) are scanned in the same pass from L2:
+// eight float4 loads in flight per lane, one memory round trip.
+__device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, const float* dir, float* outA,
+                                             float* outB) {
+  float nd[3] = {-dir[0], -dir[1], -dir[2]};
+  float la[3], lb[3];
+  mattvec3(la, A.mat, dir);
+  mattvec3(lb, B.mat, nd);
+  const DXG float4 *VA, *VB;
+  int nA, nB;  // 0 unless a hull
+  hull_span(A, la, VA, nA);
+  hull_span(B, lb, VB, nB);
+  HullBest hA = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff}, hB = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+  const int n = max(nA, nB);
+  for (int base = 0; base < n; base += 64) {
+    float4 va[4], vb[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int i = base + u * 16 + SL;
+      va[u] = VA[i < nA ? i : 0];
+      vb[u] = VB[i < nB ? i : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      int i = base + u * 16 + SL;
+      hull_take(hA, va[u], va[u].x * la[0] + va[u].y * la[1] + va[u].z * la[2], i,
+                i < nA && __float_as_int(va[u].w) >= 0);
+      hull_take(hB, vb[u], vb[u].x * lb[0] + vb[u].y * lb[1] + vb[u].z * lb[2], i,
+                i < nB && __float_as_int(vb[u].w) >= 0);
+    }
+  }
+  float pa[3], pb[3];
+  if (nA > 0) hull_reduce(hA, pa); else support_prim(A, la, pa);
+  if (nB > 0) hull_reduce(hB, pb); else support_prim(B, lb, pb);
+  support_world(A, pa, dir, outA);
+  support_world(B, pb, nd, outB);
+}
+// Support of one shape along dir (group-cooperative for hulls).
+__device__ __forceinline__ void support_grp(const Shape& s, const float* dir, float* out) {
+  float ld[3], lp[3];
+  mattvec3(ld, s.mat, dir);
+  if (s.type == DXG_MESH) {
+    const DXG float4* V;
+    int cnt;
+    hull_span(s, ld, V, cnt);
+    HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+    for (int base = 0; base < cnt; base += 64) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        int i = base + u * 16 + SL;
+        v[u] = V[i < cnt ? i : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        int i = base + u * 16 + SL;
+        hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], i,
+                  i < cnt && __float_as_int(v[u].w) >= 0);
+      }
+    }
+    hull_reduce(h, lp);
+  } else {
+    support_prim(s, ld, lp);
+  }
+  support_world(s, lp, dir, out);
+}
+
+struct NpStats { int support, mpr, hit, plane_box, plane_convex, capsule, maxit; };
+
+// MPR penetration on A - B (libccd ccdMPRPenetration structure, see the oracle's
+// mpr_penetration) as a resumable state machine: one support evaluation per
+// mpr_step, so the four 16-lane groups of a wave -- each on its own pair and in its
+// own MPR phase -- share every support pass.
+//   phase 0: P1          phase 1: P2          phase 2: portal discovery (P3)
+//   phase 3: portal refinement towards the origin
+//   phase 4: refinement of the penetration (contact) portal
+struct MprState {
+  MPoint P0, P1, P2, P3;
+  float dir[3];
+  int phase, it;
+};
+__device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprState& S) {
+  sub3(S.P0.v, A.center, B.center);
+  for (int k = 0; k < 3; k++) { S.P0.a[k] = A.center[k]; S.P0.b[k] = B.center[k]; }
+  if (fzero(S.P0.v[0]) && fzero(S.P0.v[1]) && fzero(S.P0.v[2])) S.P0.v[0] += 1e-9f;
+  S.P1 = S.P0; S.P2 = S.P0; S.P3 = S.P0;
+  S.dir[0] = -S.P0.v[0]; S.dir[1] = -S.P0.v[1]; S.dir[2] = -S.P0.v[2];
+  normalize3(S.dir);
+  S.phase = 0;
+  S.it = 0;
+}
+// Returns 0: running, 1: separated (no contact), 2: penetration (depth/normal/pos set).
+__device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState& S, float& depth, float* normal,
+                                        float* pos, NpStats& st) {
   const float tol = 1e-6f;
   const int maxit = 50;
-  MPoint P0, P1, P2, P3;
-  sub3(P0.v, A.center, B.center);
-  for (int k = 0; k < 3; k++) { P0.a[k] = A.center[k]; P0.b[k] = B.center[k]; }
-  if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-9f;
-  float dir[3] = {-P0.v[0], -P0.v[1], -P0.v[2]};
-  normalize3(dir);
-  mpr_support_wave(c, A, B, dir, P1);
-  float dt = dot3(P1.v, dir);
-  if (fzero(dt) || dt < 0) return false;
-  cross3(dir, P0.v, P1.v);
-  if (fzero(dot3(dir, dir))) {
-    if (fzero(P1.v[0]) && fzero(P1.v[1]) && fzero(P1.v[2])) {
-      depth = 0;
-      normal[0] = 0; normal[1] = 0; normal[2] = 1;
-    } else {
-      depth = norm3(P1.v);
-      for (int k = 0; k < 3; k++) normal[k] = P1.v[k];
-      normalize3(normal);
+  MPoint p;
+  float* dir = S.dir;
+  support_pair(A, B, dir, p.a, p.b);
+  sub3(p.v, p.a, p.b);
+  st.support++;
+  if (S.phase == 0) {
+    S.P1 = p;
+    float dt = dot3(S.P1.v, dir);
+    if (fzero(dt) || dt < 0) return 1;
+    cross3(dir, S.P0.v, S.P1.v);
+    if (fzero(dot3(dir, dir))) {
+      if (fzero(S.P1.v[0]) && fzero(S.P1.v[1]) && fzero(S.P1.v[2])) {
+        depth = 0;
+        normal[0] = 0; normal[1] = 0; normal[2] = 1;
+      } else {
+        depth = norm3(S.P1.v);
+        for (int k = 0; k < 3; k++) normal[k] = S.P1.v[k];
+        normalize3(normal);
+      }
+      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (S.P1.a[k] + S.P1.b[k]);
+      return 2;
     }
-    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (P1.a[k] + P1.b[k]);
-    return true;
+    normalize3(dir);
+    S.phase = 1;
+    return 0;
   }
-  normalize3(dir);
-  mpr_support_wave(c, A, B, dir, P2);
-  dt = dot3(P2.v, dir);
-  if (fzero(dt) || dt < 0) return false;
-  float va[3], vb[3];
-  sub3(va, P1.v, P0.v);
-  sub3(vb, P2.v, P0.v);
-  cross3(dir, va, vb);
-  normalize3(dir);
-  if (dot3(dir, P0.v) > 0) {
-    MPoint t = P1;
-    msel(P1, P2, true);
-    msel(P2, t, true);
-    dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
-  }
-  for (int it = 0;; it++) {
-    if (it > 1000) return false;
-    mpr_support_wave(c, A, B, dir, P3);
-    dt = dot3(P3.v, dir);
-    if (fzero(dt) || dt < 0) return false;
-    cross3(va, P1.v, P3.v);
-    dt = dot3(va, P0.v);
-    bool r2 = dt < 0 && !fzero(dt);
-    cross3(va, P3.v, P2.v);
-    dt = dot3(va, P0.v);
-    bool r1 = !r2 && dt < 0 && !fzero(dt);
-    msel(P2, P3, r2);
-    msel(P1, P3, r1);
-    if (!r1 && !r2) break;
-    sub3(va, P1.v, P0.v);
-    sub3(vb, P2.v, P0.v);
+  if (S.phase == 1) {
+    S.P2 = p;
+    float dt = dot3(S.P2.v, dir);
+    if (fzero(dt) || dt < 0) return 1;
+    float va[3], vb[3];
+    sub3(va, S.P1.v, S.P0.v);
+    sub3(vb, S.P2.v, S.P0.v);
     cross3(dir, va, vb);
     normalize3(dir);
-  }
-  for (int it = 0;; it++) {
-    portal_dir(P1, P2, P3, dir);
-    if (dot3(dir, P1.v) >= 0) break;
-    MPoint v4;
-    mpr_support_wave(c, A, B, dir, v4);
-    if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
-    if (dot3(v4.v, dir) < 0 || portal_reach_tol(P1, P2, P3, v4, dir, tol) || it > maxit) return false;
-    expand_portal(P0, P1, P2, P3, v4);
-  }
-  for (int it = 0;; it++) {
-    portal_dir(P1, P2, P3, dir);
-    MPoint v4;
-    mpr_support_wave(c, A, B, dir, v4);
-    if (it > maxit) stage_count(c, CNT_MPR_MAXIT);
-    if (portal_reach_tol(P1, P2, P3, v4, dir, tol) || it > maxit) {
-      float cl[3];
-      float d2 = tri_origin_dist2(P1.v, P2.v, P3.v, cl);
-      depth = sqrtf(d2);
-      if (depth > 1e-20f) {
-        float s = 1.0f / depth;
-        normal[0] = cl[0] * s; normal[1] = cl[1] * s; normal[2] = cl[2] * s;
-      } else {
-        normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
-      }
-      find_pos(P0, P1, P2, P3, pos);
-      return true;
+    if (dot3(dir, S.P0.v) > 0) {
+      MPoint t = S.P1;
+      msel(S.P1, S.P2, true);
+      msel(S.P2, t, true);
+      dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
     }
-    expand_portal(P0, P1, P2, P3, v4);
+    S.phase = 2;
+    S.it = 0;
+    return 0;
   }
+  if (S.phase == 2) {
+    if (S.it > 1000) return 1;
+    S.P3 = p;
+    float dt = dot3(S.P3.v, dir);
+    if (fzero(dt) || dt < 0) return 1;
+    float va[3], vb[3];
+    cross3(va, S.P1.v, S.P3.v);
+    dt = dot3(va, S.P0.v);
+    bool r2 = dt < 0 && !fzero(dt);
+    cross3(va, S.P3.v, S.P2.v);
+    dt = dot3(va, S.P0.v);
+    bool r1 = !r2 && dt < 0 && !fzero(dt);
+    msel(S.P2, S.P3, r2);
+    msel(S.P1, S.P3, r1);
+    S.it++;
+    if (r1 || r2) {
+      sub3(va, S.P1.v, S.P0.v);
+      sub3(vb, S.P2.v, S.P0.v);
+      cross3(dir, va, vb);
+      normalize3(dir);
+    } else {
+      portal_dir(S.P1, S.P2, S.P3, dir);
+      S.phase = dot3(dir, S.P1.v) >= 0 ? 4 : 3;
+      S.it = 0;
+    }
+    return 0;
+  }
+  if (S.it > maxit) st.maxit++;
+  if (S.phase == 3) {
+    if (dot3(p.v, dir) < 0 || portal_reach_tol(S.P1, S.P2, S.P3, p, dir, tol) || S.it > maxit) return 1;
+    expand_portal(S.P0, S.P1, S.P2, S.P3, p);
+    S.it++;
+    portal_dir(S.P1, S.P2, S.P3, dir);
+    if (dot3(dir, S.P1.v) >= 0) { S.phase = 4; S.it = 0; }
+    return 0;
+  }
+  if (portal_reach_tol(S.P1, S.P2, S.P3, p, dir, tol) || S.it > maxit) {
+    float cl[3];
+    float d2 = tri_origin_dist2(S.P1.v, S.P2.v, S.P3.v, cl);
+    depth = sqrtf(d2);
+    if (depth > 1e-20f) {
+      float sc = 1.0f / depth;
+      normal[0] = cl[0] * sc; normal[1] = cl[1] * sc; normal[2] = cl[2] * sc;
+    } else {
+      normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
+    }
+    find_pos(S.P0, S.P1, S.P2, S.P3, pos);
+    return 2;
+  }
+  expand_portal(S.P0, S.P1, S.P2, S.P3, p);
+  S.it++;
+  portal_dir(S.P1, S.P2, S.P3, dir);
+  return 0;
 }
 
 __device__ __forceinline__ bool sphere_overlap(const float* c1, float r1, const float* c2, float r2, float margin) {
@@ -894,54 +1084,50 @@ __device__ __forceinline__ void write_contact(float* con, int slot, const float*
   r[13] = __int_as_float(gp);
 }
 
-// Copies a mesh hull's vertices into LDS at word offset `off` (8 global loads in
-// flight per lane).  The host sizes the staging area for the largest pair of hulls
-// among the model's geom pairs (dx_api.hip), so the support scan always reads LDS.
-__device__ __forceinline__ void stage_hull(const Ctx& c, Shape& s, int off) {
-  s.voff = off;
-  float* dst = c.S + off;
-  const DXG float* src = s.vert;
-  const int n = 3 * s.nvert;
-  for (int base = 0; base < n; base += 8 * DX_WAVE) {
-    float t[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      int k = base + u * DX_WAVE + LANE;
-      t[u] = src[k < n ? k : 0];
-    }
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      int k = base + u * DX_WAVE + LANE;
-      if (k < n) dst[k] = t[u];
-    }
-  }
-}
+// One lane's share of a group's narrowphase result: `wr` lanes write a contact at
+// (group offset + rank).
+struct NpOut {
+  bool wr;
+  int rank;
+  float pos[3], n[3], dist;
+};
 
-// Narrowphase of one geom pair by the whole wave; appends up to 4 contacts.
-__device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con, int ncon) {
+// True for pairs the primitive routines handle (plane-*, capsule-capsule); the rest
+// (box/mesh/sphere/capsule vs box/mesh) go through MPR.
+__device__ __forceinline__ bool pair_is_prim(const DevModel& m, int gp) {
+  int t1 = m.geom_type[m.gpair_geom[2 * gp]], t2 = m.geom_type[m.gpair_geom[2 * gp + 1]];
+  return t1 == DXG_PLANE || (t1 == DXG_CAPSULE && t2 == DXG_CAPSULE);
+}
+// Primitive narrowphase of one geom pair by one 16-lane group; returns the group's
+// contact count (group-uniform, at most 4).
+__device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, NpStats& st) {
   const DevModel& m = c.m;
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   float margin = m.gpair_margin[gp];
+  o.wr = false;
+  o.rank = 0;
   if (t1 == DXG_PLANE) {
     float pp[3], pm[9];
     geom_pose(c, g1, pp, pm);
     float n[3] = {pm[2], pm[5], pm[8]};
+    for (int k = 0; k < 3; k++) o.n[k] = n[k];
     if (t2 == DXG_BOX) {
+      st.plane_box++;
       float bp[3], bm[9];
       geom_pose(c, g2, bp, bm);
-      const float* sz = m.geom_size + 3 * g2;
+      const float sz[3] = {m.geom_size[3 * g2], m.geom_size[3 * g2 + 1], m.geom_size[3 * g2 + 2]};
       float rel[3];
       sub3(rel, bp, pp);
       float cdist = dot3(rel, n);
       float ext = 0;
       for (int k = 0; k < 3; k++) ext += fabsf(bm[k] * n[0] + bm[3 + k] * n[1] + bm[6 + k] * n[2]) * sz[k];
-      if (cdist > margin + ext) return ncon;
-      // corners i = 0..7 on lanes 0..7; keep the first 4 (in corner order) within the margin
+      if (cdist > margin + ext) return 0;
+      // corners i = 0..7 on group lanes 0..7; keep the first 4 (in corner order) within the margin
       bool hit = false;
-      float v[3], dist = 0;
-      if (LANE < 8) {
-        int i = LANE;
+      float v[3] = {0, 0, 0}, dist = 0;
+      if (SL < 8) {
+        int i = SL;
         float s0 = (i & 1) ? sz[0] : -sz[0], s1 = (i & 2) ? sz[1] : -sz[1], s2 = (i & 4) ? sz[2] : -sz[2];
         for (int k = 0; k < 3; k++) v[k] = bp[k] + bm[3 * k] * s0 + bm[3 * k + 1] * s1 + bm[3 * k + 2] * s2;
         float r[3];
@@ -949,38 +1135,31 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
         dist = dot3(r, n);
         hit = dist <= margin;
       }
-      uint64_t mask = __ballot(hit);
-      int rank = __popcll(mask & ((1ull << LANE) - 1ull));
-      if (hit && rank < 4 && ncon + rank < DX_NCON_MAX) {
-        float pos[3] = {v[0] - 0.5f * dist * n[0], v[1] - 0.5f * dist * n[1], v[2] - 0.5f * dist * n[2]};
-        write_contact(con, ncon + rank, pos, n, dist, gp);
-      }
-      stage_count(c, CNT_PLANE_BOX);
-      stage_mark(c, ST_NP_PRIM);
-      return ncon + min(4, __popcll(mask));
+      unsigned gm = (unsigned)((__ballot(hit) >> (LANE & 48)) & 0xFFFFull);
+      int rank = __popc(gm & ((1u << SL) - 1u));
+      o.wr = hit && rank < 4;
+      o.rank = rank;
+      o.dist = dist;
+      for (int k = 0; k < 3; k++) o.pos[k] = v[k] - 0.5f * dist * n[k];
+      return min(4, __popc(gm));
     }
+    st.plane_convex++;
     Shape s;
     make_shape(c, g2, 0, s);
-    if (s.type == DXG_MESH) stage_hull(c, s, c.L.stage);
-    SYNC();
-    stage_mark(c, ST_NP_SETUP);
-    stage_count(c, CNT_PLANE_CONVEX);
     float nd[3] = {-n[0], -n[1], -n[2]};
     float sp[3];
-    support_wave(c, s, nd, sp);
-    SYNC();
+    support_grp(s, nd, sp);
     float r[3];
     sub3(r, sp, pp);
     float dist = dot3(r, n);
-    stage_mark(c, ST_NP_PRIM);
-    if (dist > margin) return ncon;
-    if (LANE == 0 && ncon < DX_NCON_MAX) {
-      float pos[3] = {sp[0] - 0.5f * dist * n[0], sp[1] - 0.5f * dist * n[1], sp[2] - 0.5f * dist * n[2]};
-      write_contact(con, ncon, pos, n, dist, gp);
-    }
-    return ncon + 1;
+    if (dist > margin) return 0;
+    o.wr = SL == 0;
+    o.dist = dist;
+    for (int k = 0; k < 3; k++) o.pos[k] = sp[k] - 0.5f * dist * n[k];
+    return 1;
   }
   if (t1 == DXG_CAPSULE && t2 == DXG_CAPSULE) {
+    st.capsule++;
     float p1[3], m1[9], p2[3], m2[9];
     geom_pose(c, g1, p1, m1);
     geom_pose(c, g2, p2, m2);
@@ -1006,38 +1185,16 @@ __device__ __forceinline__ int narrowphase_wave(const Ctx& c, int gp, float* con
     sub3(diff, q2, q1);
     float len = norm3(diff);
     float dist = len - r1 - r2;
-    stage_count(c, CNT_CAPSULE);
-    stage_mark(c, ST_NP_PRIM);
-    if (dist > margin) return ncon;
+    if (dist > margin) return 0;
     float n[3];
     if (len > 1e-20f) { n[0] = diff[0] / len; n[1] = diff[1] / len; n[2] = diff[2] / len; }
     else { n[0] = 1; n[1] = 0; n[2] = 0; }
-    if (LANE == 0 && ncon < DX_NCON_MAX) {
-      float pos[3];
-      for (int k = 0; k < 3; k++) pos[k] = q1[k] + n[k] * (r1 + 0.5f * dist);
-      write_contact(con, ncon, pos, n, dist, gp);
-    }
-    return ncon + 1;
+    o.wr = SL == 0;
+    o.dist = dist;
+    for (int k = 0; k < 3; k++) { o.n[k] = n[k]; o.pos[k] = q1[k] + n[k] * (r1 + 0.5f * dist); }
+    return 1;
   }
-  Shape A, B;
-  make_shape(c, g1, 0.5f * margin, A);
-  make_shape(c, g2, 0.5f * margin, B);
-  int used = 0;
-  if (A.type == DXG_MESH) { stage_hull(c, A, c.L.stage); used = 3 * A.nvert; }
-  if (B.type == DXG_MESH) stage_hull(c, B, c.L.stage + used);
-  SYNC();
-  stage_mark(c, ST_NP_SETUP);
-  stage_count(c, CNT_MPR);
-  float depth, nrm[3], pos[3];
-  int out = ncon;
-  if (mpr_wave(c, A, B, depth, nrm, pos)) {
-    stage_count(c, CNT_MPR_HIT);
-    if (LANE == 0 && ncon < DX_NCON_MAX) write_contact(con, ncon, pos, nrm, margin - depth, gp);
-    out = ncon + 1;
-  }
-  SYNC();
-  stage_mark(c, ST_NP_MPR);
-  return out;
+  return 0;
 }
 
 // broadphase (body spheres, lanes over body pairs) -> flattened mid-phase (geom
@@ -1090,13 +1247,14 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     }
     uint64_t mask = __ballot(keep);
     int pos = __popcll(mask & ((1ull << LANE) - 1ull));
-    int off = wave_excl_scan(cnt);
+    int inc = wave_incl_scan(cnt);
+    int off = inc - cnt;
     if (keep && nbc + pos < half) {
       cand[nbc + pos] = bp;
       pref[nbc + pos] = ngp + off;
     }
     nbc += __popcll(mask);
-    ngp += wave_sum_i(cnt);
+    ngp += __builtin_amdgcn_readlane(inc, 63);
   }
   if (nbc > half) { nbc = half; if (LANE == 0) I[I_OVF] |= 1; }
   if (LANE == 0) pref[nbc] = ngp;
@@ -1158,13 +1316,101 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   if (LANE == 0) I[I_NCAND] = ng;
   SYNC();
   stage_mark(c, ST_MID);
-  // 3. narrowphase: whole wave per candidate, in candidate order (deterministic)
+  // 3. narrowphase.  Candidate q belongs to 16-lane group q % 4 (static round robin)
+  // and every group walks its own candidates in this one loop, so a group never
+  // waits for another group's pair.  Contacts are written unordered together with
+  // their key (candidate, rank) and put into candidate order below, which gives the
+  // list of the serial loop.
   float* con = c.f(c.L.con);
   int ncon = 0;
-  for (int q = 0; q < ng; q++) {
-    int gp = __builtin_amdgcn_readfirstlane(gcand[q]);
-    ncon = narrowphase_wave(c, gp, con, ncon);
+  NpStats st = {0, 0, 0, 0, 0, 0, 0};
+  {
+    const int grp = LANE >> 4;
+    int q = grp;
+    bool fresh = true;
+    int gp = 0;
+    float margin = 0;
+    Shape A, B;
+    MprState M;
+    for (;;) {
+      bool act = q < ng;
+      if (__ballot(act) == 0) break;
+      NpOut o;
+      o.wr = false;
+      o.rank = 0;
+      int cnt = 0;
+      bool done = false;
+      if (act) {
+        bool stepping = !fresh;
+        if (fresh) {
+          gp = gcand[q];
+          float4 pr = m.gpair_rec[gp];
+          if (__float_as_int(pr.w)) {
+            cnt = narrowphase_prim(c, gp, o, st);
+            done = true;
+          } else {
+            st.mpr++;
+            margin = pr.z;
+            make_shape_rec(c, __float_as_int(pr.x), 0.5f * margin, A);
+            make_shape_rec(c, __float_as_int(pr.y), 0.5f * margin, B);
+            mpr_init(A, B, M);
+            fresh = false;
+            stepping = true;
+          }
+        }
+        if (stepping) {
+          float depth, nrm[3], pos[3];
+          int r = mpr_step(A, B, M, depth, nrm, pos, st);
+          if (r) {
+            done = true;
+            if (r == 2) {
+              st.hit++;
+              cnt = 1;
+              o.wr = SL == 0;
+              o.dist = margin - depth;
+              for (int k = 0; k < 3; k++) { o.n[k] = nrm[k]; o.pos[k] = pos[k]; }
+            }
+          }
+        }
+      }
+      int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
+      int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
+      int pre = grp == 0 ? 0 : grp == 1 ? c0 : grp == 2 ? c0 + c1 : c0 + c1 + c2;
+      int slot = ncon + pre + o.rank;
+      if (o.wr && slot < DX_NCON_MAX) {
+        write_contact(con, slot, o.pos, o.n, o.dist, gp);
+        con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
+      }
+      ncon += c0 + c1 + c2 + c3;
+      if (done) {
+        q += 4;
+        fresh = true;
+      }
+    }
   }
+  SYNC();
+  // candidate order: lane k ranks record k by its key, then moves it
+  {
+    int nk = min(ncon, DX_NCON_MAX);
+    int key = LANE < nk ? __float_as_int(con[DX_CON_STRIDE * LANE + 14]) : 0x7fffffff;
+    int rank = 0;
+    for (int j = 0; j < nk; j++) rank += __builtin_amdgcn_readlane(key, j) < key;
+    float rec[14];
+#pragma unroll
+    for (int e = 0; e < 14; e++) rec[e] = LANE < nk ? con[DX_CON_STRIDE * LANE + e] : 0.f;
+    SYNC();
+    if (LANE < nk) {
+#pragma unroll
+      for (int e = 0; e < 14; e++) con[DX_CON_STRIDE * rank + e] = rec[e];
+    }
+  }
+  if (c.stage_acc) {
+    bool lead = SL == 0;
+    int v[7] = {st.plane_box, st.plane_convex, st.capsule, st.mpr, st.support, st.hit, st.maxit};
+#pragma unroll
+    for (int k = 0; k < 7; k++) stage_count(c, CNT_PLANE_BOX + k, wave_sum_i(lead ? v[k] : 0));
+  }
+  stage_mark(c, ST_NP_MPR);
   if (ncon > DX_NCON_MAX) {
     if (LANE == 0) I[I_OVF] |= 2;
     ncon = DX_NCON_MAX;
@@ -1242,8 +1488,9 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       dist[1] = m.jnt_range[2 * j + 1] - q;
       cnt = (dist[0] < m.jnt_margin[j]) + (dist[1] < m.jnt_margin[j]);
     }
-    int off = wave_excl_scan(cnt);
-    int tot = wave_sum_i(cnt);
+    int inc = wave_incl_scan(cnt);
+    int off = inc - cnt;
+    int tot = __builtin_amdgcn_readlane(inc, 63);
     if (cnt) {
       int r = nrow + off;
       int d = m.jnt_dofadr[j];
@@ -1273,8 +1520,9 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       dist[1] = m.tendon_range[2 * t + 1] - tl[t];
       cnt = (dist[0] < m.tendon_margin[t]) + (dist[1] < m.tendon_margin[t]);
     }
-    int off = wave_excl_scan(cnt);
-    int tot = wave_sum_i(cnt);
+    int inc = wave_incl_scan(cnt);
+    int off = inc - cnt;
+    int tot = __builtin_amdgcn_readlane(inc, 63);
     if (cnt) {
       int r = nrow + off;
       float tv = 0;
@@ -1344,8 +1592,9 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       gp = __float_as_int(r[13]);
       nr = m.gpair_condim[gp] == 1 ? 1 : 4;
     }
-    int off = wave_excl_scan(nr);
-    int tot = wave_sum_i(nr);
+    int inc = wave_incl_scan(nr);
+    int off = inc - nr;
+    int tot = __builtin_amdgcn_readlane(inc, 63);
     if (nr) {
       int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
       int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];

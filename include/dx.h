@@ -81,6 +81,10 @@ void dx_model_free(dx_model* m);
 int dx_model_sizes(const dx_model* m, int32_t out[12]);
 /* Bytes of LDS one environment (one 64-lane workgroup) of dx_step uses. */
 int dx_model_lds_bytes(const dx_model* m);
+/* Test hook: index of the vertex the device's support scan returns for hull `mesh`
+   along local direction dir (direction-binned hulls); info =
+   [vertex, cube-map cells per face edge (0: not binned), cell capacity]. */
+int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[3], int32_t info[3]);
 /* Width (in 4-byte words per environment) of a dx_field. */
 int dx_field_width(const dx_model* m, int field);
 

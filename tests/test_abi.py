@@ -76,3 +76,46 @@ def test_null_arguments_are_rejected(lib):
     assert lib.dx_step(None, 1) < 0
     assert lib.dx_env_step(None, None) < 0
     assert lib.dx_set_field(None, 0, None, 0, 1) < 0
+
+
+@pytest.mark.parametrize("asset", ["shadow_reorient", "adroit_reach"])
+def test_binned_hull_support_matches_full_scan(lib, asset):
+    """Direction-binned hulls (dx_api.hip build_hull_bins) return the vertex the full
+    serial scan returns -- the first maximiser -- for random and axis-aligned
+    directions, including cell edges and faces.  A different index is accepted only
+    for a tie at fp32 resolution (two vertices whose fp64 dots differ by < 1e-6 R,
+    ordered differently by fp32 rounding)."""
+    from dexterity_amd.mjcf.compiler import CompiledModel
+    from dexterity_amd.physics import Model
+
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", f"{asset}.npz"))
+    model = Model(cm)
+    a = cm.arrays
+    nvert = np.asarray(a["mesh_vertnum"])
+    adr = np.asarray(a["mesh_vertadr"])
+    V = np.asarray(a["mesh_vert"], dtype=np.float64).reshape(-1, 3)
+    info = (ctypes.c_int32 * 3)()
+    d = (ctypes.c_float * 3)()
+    rng = np.random.RandomState(7)
+    checked = binned = 0
+    for mesh in np.nonzero(nvert > 64)[0]:
+        vv = V[adr[mesh]: adr[mesh] + nvert[mesh]]
+        R = np.linalg.norm(vv, axis=1).max()
+        dirs = rng.randn(400, 3).astype(np.float32)
+        dirs[::4, rng.randint(3)] = 0.0          # on cube-map cell edges
+        dirs[1::4] = np.round(dirs[1::4] * 2) / 2  # exact face / corner ratios
+        for dv in dirs:
+            d[:] = dv
+            assert lib.dx_hull_support(model.ptr, int(mesh), d, info) == 0
+            # not binned (a hull whose cells need > 64 slots, e.g. a face with > 64
+            # coplanar vertices): the device scans the whole hull
+            assert (info[1] > 0 and 0 < info[2] <= 64 and info[2] % 16 == 0) or info[1] == info[2] == 0
+            binned += info[1] > 0
+            dots = vv @ dv.astype(np.float64)
+            ref = int(np.argmax(dots))
+            tie = dots[info[0]] >= dots[ref] - 1e-6 * R * np.linalg.norm(dv)
+            assert info[0] == ref or tie, (mesh, dv)
+            checked += 1
+    assert checked > 0
+    if asset == "shadow_reorient":
+        assert binned == checked  # every large Shadow hull is binned
