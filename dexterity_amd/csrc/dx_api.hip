@@ -480,6 +480,11 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.total = end;
   m->ncon_max = DX_NCON_MAX;
   m->nefc_max = L.nefc_max;
+  if (L.nefc_max > 5 * 64) {  // line-search register slots (dx_step.hip DX_LS_SLOTS)
+    fail(DX_ELIMIT, "constraint row capacity exceeds 320");
+    delete m;
+    return nullptr;
+  }
   if (L.total * 4 > 160 * 1024) {
     fail(DX_ELIMIT, "per-env LDS footprint exceeds 160 KiB");
     delete m;

@@ -10,7 +10,9 @@
 #define DX_WAVE 64
 #define DX_NCON_MAX 32    // contacts kept per env per substep (MuJoCo pool: nconmax)
 #define DX_DOFMAX 16      // max dofs in a contact Jacobian (|chain(b1) xor chain(b2)|)
-#define DX_CON_STRIDE 16  // floats per contact record in LDS
+#define DX_CON_STRIDE 20  // words per contact record in LDS:
+// 0-2 pos, 3-11 frame (normal, tangents), 12 dist, 13 geom pair, 14 nnz | nrows << 8
+// (key while sorting), 15 first efc row, 16-17 friction (mu1, mu2), 18-19 dof support mask
 #define DX_MAX_NV 64      // dof bitmasks are uint64
 
 enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };

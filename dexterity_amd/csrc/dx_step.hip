@@ -21,7 +21,15 @@
 
 #include <math.h>
 
-#define LANE ((int)threadIdx.x)
+// The lane id is laundered through an empty volatile asm at every use: the compiler
+// can then neither hoist lane-dependent address arithmetic out of the substep loop
+// nor keep it alive across the stages (it did, and spilled those values to scratch).
+__device__ __forceinline__ int lane_id() {
+  int l = (int)threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+#define LANE (lane_id())
 // A workgroup is exactly one wavefront, and a wavefront's LDS instructions execute
 // in issue order, so cross-lane LDS hand-offs need only a compiler-level barrier
 // (no s_barrier, and no s_waitcnt on outstanding global stores).
@@ -1497,7 +1505,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       for (int side = 0; side < 2; side++) {
         if (dist[side] >= m.jnt_margin[j]) continue;
         if (r < c.L.nefc_max) {
-          meta[r] = DXR_LIMJ | (side << 4) | (j << 8);
+          meta[r] = DXR_LIMJ | (side << 4) | (d << 8);  // hinge: the joint's dof
           float v = side == 0 ? qvel[d] : -qvel[d];
           row_params(c, r, dist[side], m.jnt_margin[j], 0, m.dof_invweight0[d], m.jnt_solref + 2 * j,
                      m.jnt_solimp + 5 * j, v, 1.0f, false);
@@ -1579,7 +1587,13 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     }
     if (sup) I[I_OVF] |= 4;
     for (int k = 0; k < 3; k++) cq[3 * ci + k] = vel[k];  // frame velocities (J qvel)
-    r[14] = __int_as_float(nnz);
+    int nr = m.gpair_condim[gp] == 1 ? 1 : 4;
+    r[14] = __int_as_float(nnz | (nr << 8));
+    r[16] = m.gpair_friction[5 * gp];
+    r[17] = m.gpair_friction[5 * gp + 1];
+    uint64_t sp = c1 ^ c2;
+    r[18] = __int_as_float((int)(uint32_t)sp);
+    r[19] = __int_as_float((int)(uint32_t)(sp >> 32));
   }
   SYNC();
   for (int base = 0; base < ncon; base += DX_WAVE) {
@@ -1590,7 +1604,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     if (ci < ncon) {
       r = con + DX_CON_STRIDE * ci;
       gp = __float_as_int(r[13]);
-      nr = m.gpair_condim[gp] == 1 ? 1 : 4;
+      nr = __float_as_int(r[14]) >> 8;
     }
     int inc = wave_incl_scan(nr);
     int off = inc - nr;
@@ -1757,8 +1771,23 @@ __device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf,
   return 0.5f * D * jar * jar;
 }
 
-// y = M x (lanes over rows)
+// y = M x (lanes over rows).  For n <= 32 the row is gathered with 32 independent
+// LDS reads (one latency, not one per element); entries past n read zeros of the
+// packed triangle's padding only through x, which is 0 there.
 __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y, int n) {
+  if (n <= 32) {
+    const int i = min(LANE, n - 1);
+    float s = 0;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      int a = max(i, k), b = min(i, k);
+      float xk = k < n ? x[k] : 0.f;
+      float mk = k < n ? M[ti(a) + b] : 0.f;
+      s = fmaf(mk, xk, s);
+    }
+    if (LANE < n) y[LANE] = s;
+    return;
+  }
   for (int i = LANE; i < n; i += DX_WAVE) {
     float s = 0;
     const float* row = M + ti(i);
@@ -1768,7 +1797,8 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
   }
 }
 
-// J x for every row -> out[r]; uses cq as contact-frame scratch
+// J x for every row -> out[r]; uses cq as contact-frame scratch.  The contact
+// frame rows are gathered with DX_DOFMAX independent reads per lane.
 __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out) {
   const DevModel& m = c.m;
   int nefc = c.I[I_NEFC];
@@ -1779,10 +1809,15 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
   float* cq = c.f(c.L.cq);
   const float* con = c.f(c.L.con);
   for (int t = LANE; t < 3 * ncon; t += DX_WAVE) {
-    int ci = t / 3, k = t % 3;
-    int nnz = __float_as_int(con[DX_CON_STRIDE * ci + 14]);
+    int ci = t / 3, k = t - 3 * ci;
+    int nnz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
     float s = 0;
-    for (int q = 0; q < nnz; q++) s += cj_val[(ci * 3 + k) * DX_DOFMAX + q] * x[cj_idx[ci * DX_DOFMAX + q]];
+#pragma unroll
+    for (int q = 0; q < DX_DOFMAX; q++) {
+      float v = q < nnz ? cj_val[(ci * 3 + k) * DX_DOFMAX + q] : 0.f;
+      float xv = q < nnz ? x[cj_idx[ci * DX_DOFMAX + q]] : 0.f;
+      s = fmaf(v, xv, s);
+    }
     cq[t] = s;
   }
   SYNC();
@@ -1790,7 +1825,7 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
     int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
     float v;
     if (type == DXR_FRIC) v = x[id];
-    else if (type == DXR_LIMJ) v = aux == 0 ? x[m.jnt_dofadr[id]] : -x[m.jnt_dofadr[id]];
+    else if (type == DXR_LIMJ) v = aux == 0 ? x[id] : -x[id];
     else if (type == DXR_LIMT) {
       v = 0;
       for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++) v += m.wrap_coef[w] * x[m.wrap_dof[w]];
@@ -1799,8 +1834,7 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
       v = cq[3 * id];
     } else {
       int k = 1 + (aux >> 1);
-      int gp = __float_as_int(con[DX_CON_STRIDE * id + 13]);
-      float mu = m.gpair_friction[5 * gp + k - 1] * ((aux & 1) ? -1.f : 1.f);
+      float mu = con[DX_CON_STRIDE * id + 15 + k] * ((aux & 1) ? -1.f : 1.f);
       v = cq[3 * id] + mu * cq[3 * id + k];
     }
     out[r] = v;
@@ -1861,9 +1895,8 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
   for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
     const float* r = con + DX_CON_STRIDE * ci;
     int row0 = __float_as_int(r[15]);
-    int gp = __float_as_int(r[13]);
     float fc[3] = {0, 0, 0};
-    if (m.gpair_condim[gp] == 1) {
+    if ((__float_as_int(r[14]) >> 8) == 1) {
       float f, hw;
       if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); fc[0] = f; }
     } else {
@@ -1873,7 +1906,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
         float f, hw;
         row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
         int k = 1 + (e >> 1);
-        float mu = m.gpair_friction[5 * gp + k - 1] * ((e & 1) ? -1.f : 1.f);
+        float mu = r[15 + k] * ((e & 1) ? -1.f : 1.f);
         fc[0] += f;
         fc[k] += mu * f;
       }
@@ -1891,7 +1924,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     for (int r = m.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
       if (type == DXR_LIMJ) {
-        if (m.jnt_dofadr[id] != d) continue;
+        if (id != d) continue;
         float f, hw;
         row_cost(type, D[r], 0, 0, jar[r], f, hw);
         s += aux ? -f : f;
@@ -1908,9 +1941,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     uint64_t bit = 1ull << d;
     for (int ci = 0; ci < ncon; ci++) {
       const float* r = con + DX_CON_STRIDE * ci;
-      int gp = __float_as_int(r[13]);
-      int b1 = m.geom_bodyid[m.gpair_geom[2 * gp]], b2 = m.geom_bodyid[m.gpair_geom[2 * gp + 1]];
-      uint64_t sup = m.body_chain[b1] ^ m.body_chain[b2];
+      uint64_t sup = (uint64_t)(uint32_t)__float_as_int(r[18]) | ((uint64_t)(uint32_t)__float_as_int(r[19]) << 32);
       if (!(sup & bit)) continue;
       int q = __popcll(sup & (bit - 1));
       if (q >= DX_DOFMAX) continue;
@@ -1945,7 +1976,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
     for (int r = m.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, id = mt >> 8;
       if (type != DXR_LIMJ) { if (type == DXR_LIMT) continue; break; }
-      if (m.jnt_dofadr[id] != d) continue;
+      if (id != d) continue;
       float f, hw;
       row_cost(type, D[r], 0, 0, jar[r], f, hw);
       s += hw;
@@ -1973,10 +2004,9 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   for (int ci = 0; ci < ncon; ci++) {
     const float* r = con + DX_CON_STRIDE * ci;
     int row0 = __float_as_int(r[15]);
-    int gp = __float_as_int(r[13]);
-    int nnz = __float_as_int(r[14]);
+    int nnz = __float_as_int(r[14]) & 255;
     float W[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    if (m.gpair_condim[gp] == 1) {
+    if ((__float_as_int(r[14]) >> 8) == 1) {
       float f, hw;
       if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); W[0] = hw; }
     } else {
@@ -1987,7 +2017,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
         row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
         if (hw == 0) continue;
         int k = 1 + (e >> 1);
-        float mu = m.gpair_friction[5 * gp + k - 1] * ((e & 1) ? -1.f : 1.f);
+        float mu = r[15 + k] * ((e & 1) ? -1.f : 1.f);
         W[0] += hw;
         W[k] += hw * mu;
         W[3 * k] += hw * mu;
@@ -2018,6 +2048,10 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
   return jar < 0 ? 1 : 0;
 }
 
+// Exact line search along dir (1-D Newton with bracketing on the piecewise-quadratic
+// cost).  Every row's (type, D, friction, jar, J dir) is loaded into registers once
+// -- lane-owned rows r = LANE + 64 k -- so the iterations touch no LDS.
+#define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
   const DevModel& m = c.m;
   int nv = m.nv;
@@ -2031,23 +2065,38 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   qa = wave_sum(qa);
   qb = wave_sum(qb);
   int nefc = c.I[I_NEFC];
+  const int ns = (nefc + DX_WAVE - 1) / DX_WAVE;  // uniform
   const int* meta = (const int*)c.f(c.L.efc_meta);
-  const float* D = c.f(c.L.efc_D);
-  const float* fl = c.f(c.L.efc_fl);
-  const float* Rf = c.f(c.L.efc_Rf);
-  const float* jar = c.f(c.L.efc_jar);
+  const float* Dp = c.f(c.L.efc_D);
+  const float* flp = c.f(c.L.efc_fl);
+  const float* Rfp = c.f(c.L.efc_Rf);
+  const float* jarp = c.f(c.L.efc_jar);
+  int ty[DX_LS_SLOTS];
+  float D[DX_LS_SLOTS], fl[DX_LS_SLOTS], Rf[DX_LS_SLOTS], ja[DX_LS_SLOTS], jj[DX_LS_SLOTS];
+#pragma unroll
+  for (int k = 0; k < DX_LS_SLOTS; k++) {
+    int r = LANE + DX_WAVE * k;
+    bool ok = k < ns && r < nefc;
+    bool fr = ok && r < m.nfric;
+    ty[k] = ok ? (meta[r] & 15) : DXR_CON;
+    D[k] = ok ? Dp[r] : 0.f;
+    fl[k] = fr ? flp[r] : 0.f;
+    Rf[k] = fr ? Rfp[r] : 0.f;
+    ja[k] = ok ? jarp[r] : 0.f;
+    jj[k] = ok ? jv[r] : 0.f;
+  }
   float lo = 0, hi = -1, alpha = 0, g0 = 0;
   for (int it = 0; it < 40; it++) {
     stage_count(c, CNT_LS_IT);
     float g = 0, h = 0;
-    for (int r = LANE; r < nefc; r += DX_WAVE) {
-      float j = jv[r];
-      if (j == 0) continue;
-      float f, hw;
-      bool fr = r < m.nfric;
-      row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r] + alpha * j, f, hw);
-      g -= f * j;
-      h += hw * j * j;
+#pragma unroll
+    for (int k = 0; k < DX_LS_SLOTS; k++) {
+      if (k < ns) {
+        float f, hw;
+        row_cost(ty[k], D[k], fl[k], Rf[k], ja[k] + alpha * jj[k], f, hw);
+        g -= f * jj[k];
+        h += hw * jj[k] * jj[k];
+      }
     }
     g = wave_sum(g) + qa * alpha + qb;
     h = wave_sum(h) + qa;
@@ -2062,11 +2111,9 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   }
   // rows whose cost zone differs between the current point and the new one
   int ch = 0;
-  for (int r = LANE; r < nefc; r += DX_WAVE) {
-    int type = meta[r] & 15;
-    float rf = r < m.nfric ? Rf[r] : 0.f;
-    ch += row_zone(type, rf, jar[r]) != row_zone(type, rf, jar[r] + alpha * jv[r]);
-  }
+#pragma unroll
+  for (int k = 0; k < DX_LS_SLOTS; k++)
+    if (k < ns) ch += jj[k] != 0.f && row_zone(ty[k], Rf[k], ja[k]) != row_zone(ty[k], Rf[k], ja[k] + alpha * jj[k]);
   *changed = wave_sum_i(ch);
   return alpha;
 }
