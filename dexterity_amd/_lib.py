@@ -27,11 +27,11 @@ EXPORTS = (
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
-    "dx_debug_poison_lds", "dx_hull_support",
+    "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout",
 )
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
-          "qfrc_constraint", "euler", "observe", "io", "np_setup", "np_mpr", "np_prim")
+          "qfrc_constraint", "euler", "observe", "io", "matvec", "np_mpr", "jacvec")
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
             26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc"}
 NSTAGE = 32
@@ -61,6 +61,7 @@ def load(path: str = LIB_PATH):
     L.dx_model_sizes.argtypes = [vp, ctypes.POINTER(i32)]
     L.dx_model_lds_bytes.argtypes = [vp]
     L.dx_field_width.argtypes = [vp, ctypes.c_int]
+    L.dx_model_layout.argtypes = [vp, ctypes.POINTER(i32), i32]
     L.dx_hull_support.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(i32)]
     L.dx_batch_create.restype = vp
     L.dx_batch_create.argtypes = [vp, i32, i32]

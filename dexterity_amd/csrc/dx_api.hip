@@ -559,6 +559,20 @@ extern "C" int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[
   return 0;
 }
 
+// Layout export for build.py's kernel specialization: the Lds struct (words, in
+// declaration order) followed by the 16 dimensions of dx_step.hip DX_DIMS.
+extern "C" int dx_model_layout(const dx_model* m, int32_t* out, int32_t n) {
+  if (!m || !out) return fail(DX_EINVAL, "null argument");
+  const int nl = (int)(sizeof(Lds) / sizeof(int));
+  const DevModel& d = m->dm;
+  int dims[16] = {d.nq, d.nv, d.nbody, d.njnt, d.nu, d.ntendon, d.nsite, d.nlevel, d.nroot,
+                  d.nfric, d.nlimj, d.nlimt, d.nbpair, d.any_damping, d.disable_contact, d.iterations};
+  if (n < nl + 16) return fail(DX_EINVAL, "output too small");
+  memcpy(out, &m->lds, sizeof(Lds));
+  memcpy(out + nl, dims, sizeof(dims));
+  return nl + 16;
+}
+
 extern "C" int dx_model_lds_bytes(const dx_model* m) {
   if (!m) return fail(DX_EINVAL, "null model");
   return m->lds.total * 4;
@@ -651,6 +665,7 @@ struct dx_batch {
   hipStream_t stream;
   DevModel dm;
   DevBatch db;
+  int spec;  // specialized step kernel (dx_specs.inc) or -1 for the generic one
   float* xfrc;
   std::vector<void*> allocs;
   bool debug;
@@ -684,6 +699,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
     return nullptr;
   }
   if (device_model(m, device, &b->dm) != 0) { delete b; return nullptr; }
+  b->spec = getenv("DX_GENERIC_KERNEL") ? -1 : dx_spec_find(b->dm, m->lds);
   const DevModel& d = b->dm;
   DevBatch& B = b->db;
   memset(&B, 0, sizeof(B));
@@ -821,10 +837,9 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   size_t lds = (size_t)b->model->lds.total * 4;
   hipEvent_t t0;
   timing_begin(b, &t0);
-  hipLaunchKernelGGL(dx_step_kernel, dim3(b->nenv), dim3(64), lds, b->stream, b->dm, b->db,
-                     b->model->lds, nsub, mode);
+  hipError_t e = dx_launch_step(b->spec, b->nenv, lds, b->stream, b->dm, b->db, b->model->lds, nsub, mode);
   timing_end(b, t0);
-  HIPCHK(hipGetLastError());
+  HIPCHK(e);
   return 0;
 }
 

@@ -126,3 +126,8 @@ struct TaskState {
   int *successes, *counter, *registered, *exceeded, *step_type, *episode, *skip, *failure;
 };
 
+
+// dx_step.hip: specialized-kernel lookup and launch (host side)
+int dx_spec_find(const DevModel& d, const Lds& L);
+hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+                          const Lds& L, int nsub, int mode);

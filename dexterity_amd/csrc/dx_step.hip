@@ -20,6 +20,7 @@
 #include "dx_internal.h"
 
 #include <math.h>
+#include <string.h>
 
 // The lane id is laundered through an empty volatile asm at every use: the compiler
 // can then neither hoist lane-dependent address arithmetic out of the substep loop
@@ -205,22 +206,55 @@ __device__ __forceinline__ float dot6(const float* a, const float* b) {
 // ------------------------------------------------------------------------ //
 // per-env context
 // ------------------------------------------------------------------------ //
-struct Ctx {
+// The model's dimensions and the LDS layout come either from the launch (generic
+// kernel) or from a compile-time model specialization (dx_specs.inc, generated by
+// build.py for the shipped scenes): then every LDS offset is an immediate, loop
+// bounds are constants, and far fewer scalar registers stay live (the generic
+// kernel spills its ~60 layout/dimension scalars into VGPR lanes).
+#define DX_DIMS(X) X(nq) X(nv) X(nbody) X(njnt) X(nu) X(ntendon) X(nsite) X(nlevel) X(nroot) \
+  X(nfric) X(nlimj) X(nlimt) X(nbpair) X(any_damping) X(disable_contact) X(iterations)
+struct SpecRT {};
+template <class SP>
+struct CtxT {
   const DevModel& m;
-  const Lds& L;
+  static constexpr Lds L = SP::L;
+#define DX_X(n) static constexpr int n = SP::n;
+  DX_DIMS(DX_X)
+#undef DX_X
   float* S;
   int* I;  // misc ints
   unsigned long long* stage_acc;
+  __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
+      : m(m_), S(S_), I(I_), stage_acc(acc) {}
+  __device__ float* f(int off) const { return S + off; }
+};
+template <>
+struct CtxT<SpecRT> {
+  const DevModel& m;
+  const Lds& L;
+#define DX_X(n) int n;
+  DX_DIMS(DX_X)
+#undef DX_X
+  float* S;
+  int* I;
+  unsigned long long* stage_acc;
+  __device__ CtxT(const DevModel& m_, const Lds& L_, float* S_, int* I_, unsigned long long* acc)
+      : m(m_), L(L_),
+#define DX_X(n) n(m_.n),
+        DX_DIMS(DX_X)
+#undef DX_X
+        S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
 };
 // Per-stage cycle accounting (runtime-gated by DevBatch::stage_acc, lane 0 only).
 enum {
   ST_KIN = 0, ST_CRB, ST_BROAD, ST_MID, ST_NARROW, ST_CON, ST_VEL, ST_SMOOTH, ST_NEWTON_EVAL,
   ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO,
-  ST_NP_SETUP, ST_NP_MPR, ST_NP_PRIM,
+  ST_MATVEC, ST_NP_MPR, ST_JACVEC,
   CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
   CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC  // event counters, not cycles
 };
+template <class Ctx>
 __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
   if (c.stage_acc && LANE == 0) {
     unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -229,6 +263,7 @@ __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
     *last = t;
   }
 }
+template <class Ctx>
 __device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
   if (c.stage_acc && LANE == 0) c.stage_acc[k] += n;
 }
@@ -238,6 +273,7 @@ enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NI
 // ------------------------------------------------------------------------ //
 // position stage
 // ------------------------------------------------------------------------ //
+template <class Ctx>
 __device__ __forceinline__ void kinematics(const Ctx& c) {
   const DevModel& m = c.m;
   float* qpos = c.f(c.L.qpos);
@@ -254,7 +290,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
     xipos[0] = xipos[1] = xipos[2] = 0;
   }
   SYNC();
-  for (int lv = 0; lv < m.nlevel; lv++) {
+  for (int lv = 0; lv < c.nlevel; lv++) {
     int a0 = m.lvl_adr[lv], a1 = m.lvl_adr[lv + 1];
     for (int k = a0 + LANE; k < a1; k += DX_WAVE) {
       int b = m.lvl_body[k];
@@ -307,15 +343,16 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
   }
 }
 
+template <class Ctx>
 __device__ __forceinline__ void com_pos(const Ctx& c) {
   const DevModel& m = c.m;
   float* xipos = c.f(c.L.xipos);
   float* xmat = c.f(c.L.xmat);
   float* rcom = c.f(c.L.rcom);
   // subtree com of every root (only roots are needed as com-frame origins)
-  for (int r = 0; r < m.nroot; r++) {
+  for (int r = 0; r < c.nroot; r++) {
     float s0 = 0, s1 = 0, s2 = 0, sm = 0;
-    for (int b = 1 + LANE; b < m.nbody; b += DX_WAVE) {
+    for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
       if (m.body_rootidx[b] != r) continue;
       float ms = m.body_mass[b];
       s0 += ms * xipos[3 * b]; s1 += ms * xipos[3 * b + 1]; s2 += ms * xipos[3 * b + 2]; sm += ms;
@@ -329,7 +366,7 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   }
   SYNC();
   float* cinert = c.f(c.L.cinert);
-  for (int b = 1 + LANE; b < m.nbody; b += DX_WAVE) {
+  for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
     float Rb[9];
     matmul3(Rb, xmat + 9 * b, m.body_imat + 9 * b);
     const float* I = m.body_inertia + 3 * b;
@@ -355,7 +392,7 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   float* cdof = c.f(c.L.cdof);
   float* xanchor = c.f(c.L.xanchor);
   float* xaxis = c.f(c.L.xaxis);
-  for (int d = LANE; d < m.nv; d += DX_WAVE) {
+  for (int d = LANE; d < c.nv; d += DX_WAVE) {
     int j = m.dof_jntid[d], b = m.dof_bodyid[d];
     const float* rc = rcom + 3 * m.body_rootidx[b];
     float off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
@@ -380,11 +417,12 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   SYNC();
 }
 
+template <class Ctx>
 __device__ __forceinline__ void tendon_lengths(const Ctx& c) {
   const DevModel& m = c.m;
   float* qpos = c.f(c.L.qpos);
   float* tl = c.f(c.L.ten_len);
-  for (int t = LANE; t < m.ntendon; t += DX_WAVE) {
+  for (int t = LANE; t < c.ntendon; t += DX_WAVE) {
     float len = 0;
     for (int w = m.tendon_adr[t]; w < m.tendon_adr[t] + m.tendon_num[t]; w++)
       len += m.wrap_coef[w] * qpos[m.wrap_qadr[w]];
@@ -392,7 +430,7 @@ __device__ __forceinline__ void tendon_lengths(const Ctx& c) {
   }
   SYNC();
   float* al = c.f(c.L.act_len);
-  for (int i = LANE; i < m.nu; i += DX_WAVE) {
+  for (int i = LANE; i < c.nu; i += DX_WAVE) {
     float g = m.actuator_gear[i];
     al[i] = m.actuator_trntype[i] == 0 ? g * qpos[m.jnt_qposadr[m.actuator_trnid[i]]]
                                        : g * tl[m.actuator_trnid[i]];
@@ -403,17 +441,18 @@ __device__ __forceinline__ void tendon_lengths(const Ctx& c) {
 // as packed lower triangles, row-major: (i, j <= i) -> ti(i) + j.
 __device__ __forceinline__ int ti(int i) { return (i * (i + 1)) >> 1; }
 
+template <class Ctx>
 __device__ __forceinline__ void crb_mass(const Ctx& c) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   float* crb = c.f(c.L.scr);
   float* cinert = c.f(c.L.cinert);
   float* M = c.f(c.L.M);
   float* cdof = c.f(c.L.cdof);
-  for (int k = LANE; k < 10 * m.nbody; k += DX_WAVE) crb[k] = cinert[k];
+  for (int k = LANE; k < 10 * c.nbody; k += DX_WAVE) crb[k] = cinert[k];
   for (int k = LANE; k < ti(nv); k += DX_WAVE) M[k] = 0;
   SYNC();
-  for (int lv = m.nlevel - 1; lv > 0; lv--) {
+  for (int lv = c.nlevel - 1; lv > 0; lv--) {
     for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
       int b = m.lvl_body[k], p = m.body_parent[b];
       if (p > 0)
@@ -511,8 +550,7 @@ __device__ __forceinline__ void reg_chol_solve32(const float* A, int n, const DX
   float dinv = 0.f;
 #pragma unroll
   for (int k = 0; k < NB; k++) {
-    float d = sqrtf(fmaxf(rl(r[k], k) + rl(add, k), 1e-30f));
-    float inv = 1.0f / d;
+    float inv = __builtin_amdgcn_rsqf(fmaxf(rl(r[k], k) + rl(add, k), 1e-30f));
     dinv = wl(dinv, inv, k);
     float lik = r[k] * inv;
     r[k] = lik;
@@ -565,6 +603,7 @@ struct Shape {
   const DXG float4* bin4;   // this hull's cells
 };
 
+template <class Ctx>
 __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
   const DevModel& m = c.m;
   int b = m.geom_bodyid[g];
@@ -576,6 +615,7 @@ __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float
   matmul3(mat, xm, m.geom_mat + 9 * g);
 }
 
+template <class Ctx>
 __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
   const DevModel& m = c.m;
   s.type = m.geom_type[g];
@@ -700,6 +740,7 @@ __device__ __forceinline__ void find_pos(const MPoint& P0, const MPoint& P1, con
 }
 
 // Shape of geom g from its record (two memory round trips: record, then body pose in LDS).
+template <class Ctx>
 __device__ __forceinline__ void make_shape_rec(const Ctx& c, int g, float half_margin, Shape& s) {
   const DevModel& m = c.m;
   const DXG float4* r = m.geom_rec + 8 * g;
@@ -1108,6 +1149,7 @@ __device__ __forceinline__ bool pair_is_prim(const DevModel& m, int gp) {
 }
 // Primitive narrowphase of one geom pair by one 16-lane group; returns the group's
 // contact count (group-uniform, at most 4).
+template <class Ctx>
 __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, NpStats& st) {
   const DevModel& m = c.m;
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
@@ -1209,6 +1251,7 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
 // spheres, lanes over every geom pair of the surviving body pairs) -> narrowphase
 // (whole wave per pair).  Writes contact records into LDS.
 // watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
+template <class Ctx>
 __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
   const DevModel& m = c.m;
   int* I = c.I;
@@ -1216,18 +1259,18 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int cmax = c.L.cand_max;
   if (LANE == 0) { I[I_NCON] = 0; I[I_NCAND] = 0; }
   SYNC();
-  if (m.disable_contact) return;
+  if (c.disable_contact) return;
   float* xpos = c.f(c.L.xpos);
   float* xmat = c.f(c.L.xmat);
   // 1. body-pair cull -> cand[0..nbc) body-pair ids, pref[0..nbc] prefix of geom-pair counts
   int half = cmax / 3;
   int* pref = cand + half;
   int nbc = 0, ngp = 0;
-  for (int base = 0; base < m.nbpair; base += DX_WAVE) {
+  for (int base = 0; base < c.nbpair; base += DX_WAVE) {
     int bp = base + LANE;
     bool keep = false;
     int cnt = 0;
-    if (bp < m.nbpair) {
+    if (bp < c.nbpair) {
       int b1 = m.bpair_body[2 * bp], b2 = m.bpair_body[2 * bp + 1];
       keep = true;
       if (watch_only) keep = (b2 == wb || b1 == wb) && (m.geom_bodyid[wg] == b1 || m.geom_bodyid[wg] == b2);
@@ -1447,6 +1490,7 @@ __device__ __forceinline__ float impedance(const float* solimp, float violation)
 }
 
 // row parameters -> D, aref, Rf.  vel = J*qvel.
+template <class Ctx>
 __device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float margin, float floss, float diag,
                            const float* solref, const float* solimp, float vel, float rscale, bool fric) {
   const DevModel& m = c.m;
@@ -1467,14 +1511,15 @@ __device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float
 }
 
 // sparse contact jacobian (frame rows) -> cj_idx / cj_val; then all rows
+template <class Ctx>
 __device__ __forceinline__ void make_constraint(const Ctx& c) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   int* I = c.I;
   float* qpos = c.f(c.L.qpos);
   float* qvel = c.f(c.L.qvel);
   int* meta = (int*)c.f(c.L.efc_meta);
-  int nfric = m.nfric;
+  int nfric = c.nfric;
   // 1. dof friction rows: fixed positions [0, nfric)
   for (int k = LANE; k < nfric; k += DX_WAVE) {
     int d = m.fric_dof[k];
@@ -1484,12 +1529,12 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   }
   // 2. joint limits (one side at most unless range < 2 margin): lane per limited joint
   int nrow = nfric;
-  for (int base = 0; base < m.nlimj; base += DX_WAVE) {
+  for (int base = 0; base < c.nlimj; base += DX_WAVE) {
     int k = base + LANE;
     int cnt = 0;
     float dist[2];
     int j = -1;
-    if (k < m.nlimj) {
+    if (k < c.nlimj) {
       j = m.limj_jnt[k];
       float q = qpos[m.jnt_qposadr[j]];
       dist[0] = q - m.jnt_range[2 * j];
@@ -1517,12 +1562,12 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   }
   // 3. tendon limits
   float* tl = c.f(c.L.ten_len);
-  for (int base = 0; base < m.nlimt; base += DX_WAVE) {
+  for (int base = 0; base < c.nlimt; base += DX_WAVE) {
     int k = base + LANE;
     int cnt = 0;
     float dist[2];
     int t = -1;
-    if (k < m.nlimt) {
+    if (k < c.nlimt) {
       t = m.limt_ten[k];
       dist[0] = tl[t] - m.tendon_range[2 * t];
       dist[1] = m.tendon_range[2 * t + 1] - tl[t];
@@ -1649,19 +1694,20 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
 // ------------------------------------------------------------------------ //
 // velocity stage: comVel, RNE (+ applied wrench), passive, actuation
 // ------------------------------------------------------------------------ //
+template <class Ctx>
 __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   float* qvel = c.f(c.L.qvel);
   float* cdof = c.f(c.L.cdof);
   float* cvel = c.f(c.L.cvel);
   float* cdd = c.f(c.L.cdof_dot);
   float* cinert = c.f(c.L.cinert);
   float* cacc = c.f(c.L.scr);
-  float* cfrc = cacc + 6 * m.nbody;
+  float* cfrc = cacc + 6 * c.nbody;
   if (LANE < 6) { cvel[LANE] = 0; cacc[LANE] = LANE < 3 ? 0.f : -m.gravity[LANE - 3]; }
   SYNC();
-  for (int lv = 0; lv < m.nlevel; lv++) {
+  for (int lv = 0; lv < c.nlevel; lv++) {
     for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
       int b = m.lvl_body[k], p = m.body_parent[b];
       float cv[6], ca[6];
@@ -1710,7 +1756,7 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
     }
     SYNC();
   }
-  for (int lv = m.nlevel - 1; lv > 0; lv--) {
+  for (int lv = c.nlevel - 1; lv > 0; lv--) {
     for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
       int b = m.lvl_body[k], p = m.body_parent[b];
       if (p > 0)
@@ -1727,7 +1773,7 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
   float* ctrl = c.f(c.L.ctrl);
   float* tl = c.f(c.L.ten_len);
   (void)tl;
-  for (int i = LANE; i < m.nu; i += DX_WAVE) {
+  for (int i = LANE; i < c.nu; i += DX_WAVE) {
     float cc = ctrl[i];
     if (m.actuator_ctrllimited[i])
       cc = fminf(m.actuator_ctrlrange[2 * i + 1], fmaxf(m.actuator_ctrlrange[2 * i], cc));
@@ -1799,6 +1845,7 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
 
 // J x for every row -> out[r]; uses cq as contact-frame scratch.  The contact
 // frame rows are gathered with DX_DOFMAX independent reads per lane.
+template <class Ctx>
 __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out) {
   const DevModel& m = c.m;
   int nefc = c.I[I_NEFC];
@@ -1843,9 +1890,10 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
 }
 
 // cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
+template <class Ctx>
 __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   const float* qs = c.f(c.L.qfrc_smooth);
   const float* a0 = c.f(c.L.qacc_smooth);
   float g = 0;
@@ -1858,18 +1906,21 @@ __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, con
   const float* jar = c.f(c.L.efc_jar);
   for (int r = LANE; r < nefc; r += DX_WAVE) {
     float f, hw;
-    bool fr = r < m.nfric;
+    bool fr = r < c.nfric;
     g += row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r], f, hw);
   }
   return wave_sum(g);
 }
 
 // jar = J qacc - aref, Ma = M qacc; returns cost
+template <class Ctx>
 __device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
-  int nv = c.m.nv;
+  int nv = c.nv;
   mat_vec(c.f(c.L.M), qacc, Ma, nv);
+  stage_mark(c, ST_MATVEC);
   float* jar = c.f(c.L.efc_jar);
   jac_vec(c, qacc, jar);
+  stage_mark(c, ST_JACVEC);
   const float* aref = c.f(c.L.efc_aref);
   int nefc = c.I[I_NEFC];
   for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] -= aref[r];
@@ -1879,9 +1930,10 @@ __device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, floa
 
 // out[d] = sum_r J[r][d] * w[r] computed as J^T applied to the per-row force of the
 // current jar (force mode) -- lane per dof, deterministic.
+template <class Ctx>
 __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
   const int* meta = (const int*)c.f(c.L.efc_meta);
@@ -1921,7 +1973,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     // friction row of this dof
     int fr = m.dof_fricrow[d];
     if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += f; }
-    for (int r = m.nfric; r < nefc; r++) {
+    for (int r = c.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
       if (type == DXR_LIMJ) {
         if (id != d) continue;
@@ -1954,9 +2006,10 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
 }
 
 // H = M + J^T D_active J  (at the current jar)
+template <class Ctx>
 __device__ __forceinline__ void build_hessian(const Ctx& c) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
   float* H = c.f(c.L.H);
@@ -1973,7 +2026,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
     float s = 0;
     int fr = m.dof_fricrow[d];
     if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
-    for (int r = m.nfric; r < nefc; r++) {
+    for (int r = c.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, id = mt >> 8;
       if (type != DXR_LIMJ) { if (type == DXR_LIMT) continue; break; }
       if (id != d) continue;
@@ -1985,7 +2038,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   }
   SYNC();
   // tendon limit rows: dense outer products, lanes over entries
-  for (int r = m.nfric; r < nefc; r++) {
+  for (int r = c.nfric; r < nefc; r++) {
     int mt = meta[r], type = mt & 15, id = mt >> 8;
     if (type == DXR_CON || type == DXR_CONFL) break;
     if (type != DXR_LIMT) continue;
@@ -2052,13 +2105,16 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // cost).  Every row's (type, D, friction, jar, J dir) is loaded into registers once
 // -- lane-owned rows r = LANE + 64 k -- so the iterations touch no LDS.
 #define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
+template <class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
   mat_vec(c.f(c.L.M), dir, Mdir, nv);
+  stage_mark(c, ST_MATVEC);
   float* jv = c.f(c.L.efc_jv);
   jac_vec(c, dir, jv);  // includes SYNC
+  stage_mark(c, ST_JACVEC);
   const float* qs = c.f(c.L.qfrc_smooth);
   float qa = 0, qb = 0;
   for (int i = LANE; i < nv; i += DX_WAVE) { qa += dir[i] * Mdir[i]; qb += dir[i] * (Ma[i] - qs[i]); }
@@ -2077,7 +2133,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   for (int k = 0; k < DX_LS_SLOTS; k++) {
     int r = LANE + DX_WAVE * k;
     bool ok = k < ns && r < nefc;
-    bool fr = ok && r < m.nfric;
+    bool fr = ok && r < c.nfric;
     ty[k] = ok ? (meta[r] & 15) : DXR_CON;
     D[k] = ok ? Dp[r] : 0.f;
     fl[k] = fr ? flp[r] : 0.f;
@@ -2118,9 +2174,10 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   return alpha;
 }
 
+template <class Ctx>
 __device__ __forceinline__ void solve(const Ctx& c) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   float* qacc = c.f(c.L.qacc);
   float* a0 = c.f(c.L.qacc_smooth);
   float* ws = c.f(c.L.v5);  // warmstart copy held in v5 by the caller
@@ -2154,7 +2211,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   stage_mark(c, ST_NEWTON_EVAL);
   stage_count(c, CNT_SOLVE);
   stage_count(c, CNT_NEFC, nefc);
-  for (; it < m.iterations; it++) {
+  for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
     jac_t_force(c, grad);  // grad <- J^T f
     float gn = 0;
@@ -2203,9 +2260,10 @@ __device__ __forceinline__ void solve(const Ctx& c) {
 // forward + Euler
 // ------------------------------------------------------------------------ //
 
+template <class Ctx>
 __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   // Stage order (LDS phases, see dx_api.hip layout): kinematics/com/crb and the
   // velocity stage use the com temporaries; the smooth solve reuses them for its
   // transpose; collision reuses them for candidates + hull staging; the constraint
@@ -2251,15 +2309,16 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   stage_mark(c, ST_QFRC);
 }
 
+template <class Ctx>
 __device__ __forceinline__ void euler(const Ctx& c, float* time) {
   const DevModel& m = c.m;
-  int nv = m.nv;
+  int nv = c.nv;
   float h = m.timestep;
   float* qacc = c.f(c.L.qacc);
   float* qvel = c.f(c.L.qvel);
   float* qpos = c.f(c.L.qpos);
   float* acc = c.f(c.L.v1);
-  if (m.any_damping) {
+  if (c.any_damping) {
     float* H = c.f(c.L.H);
     const float* M = c.f(c.L.M);
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
@@ -2280,7 +2339,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
   }
   for (int i = LANE; i < nv; i += DX_WAVE) qvel[i] += h * acc[i];
   SYNC();
-  for (int j = LANE; j < m.njnt; j += DX_WAVE) {
+  for (int j = LANE; j < c.njnt; j += DX_WAVE) {
     int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     if (m.jnt_type[j] == DXJ_FREE) {
       for (int k = 0; k < 3; k++) qpos[qa + k] += h * qvel[da + k];
@@ -2304,6 +2363,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
 }
 
 // observation pass at the new state: kinematics, com, velocities, sites, watch contact
+template <class Ctx>
 __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env) {
   const DevModel& m = c.m;
   kinematics(c);
@@ -2314,7 +2374,7 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
   float* cvel = c.f(c.L.cvel);
   if (LANE < 6) cvel[LANE] = 0;
   SYNC();
-  for (int lv = 0; lv < m.nlevel; lv++) {
+  for (int lv = 0; lv < c.nlevel; lv++) {
     for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
       int b = m.lvl_body[k], p = m.body_parent[b];
       float cv[6];
@@ -2328,26 +2388,26 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
   float* xpos = c.f(c.L.xpos);
   float* xmat = c.f(c.L.xmat);
   float* rcom = c.f(c.L.rcom);
-  for (int s = LANE; s < m.nsite; s += DX_WAVE) {
+  for (int s = LANE; s < c.nsite; s += DX_WAVE) {
     int b = m.site_bodyid[s];
     float t[3];
     matvec3(t, xmat + 9 * b, m.site_pos + 3 * s);
     float p[3] = {xpos[3 * b] + t[0], xpos[3 * b + 1] + t[1], xpos[3 * b + 2] + t[2]};
-    float* out = B.site_xpos + ((size_t)env * m.nsite + s) * 3;
+    float* out = B.site_xpos + ((size_t)env * c.nsite + s) * 3;
     out[0] = p[0]; out[1] = p[1]; out[2] = p[2];
     const float* cv = cvel + 6 * b;
     const float* rc = rcom + 3 * m.body_rootidx[b];
     float off[3] = {p[0] - rc[0], p[1] - rc[1], p[2] - rc[2]};
     float wx[3];
     cross3(wx, cv, off);
-    float* vo = B.site_vel + ((size_t)env * m.nsite + s) * 6;
+    float* vo = B.site_vel + ((size_t)env * c.nsite + s) * 6;
     vo[0] = cv[3] + wx[0]; vo[1] = cv[4] + wx[1]; vo[2] = cv[5] + wx[2];
     vo[3] = cv[0]; vo[4] = cv[1]; vo[5] = cv[2];
   }
   // body poses out before the watch pass reuses the com-temporary LDS block
   const float* xq = c.f(c.L.xquat);
-  for (int k = LANE; k < 3 * m.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * m.nbody + k] = xpos[k];
-  for (int k = LANE; k < 4 * m.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * m.nbody + k] = xq[k];
+  for (int k = LANE; k < 3 * c.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * c.nbody + k] = xpos[k];
+  for (int k = LANE; k < 4 * c.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * c.nbody + k] = xq[k];
   SYNC();
   if (B.watch_geom >= 0 && B.watch) {
     collision(c, 1, B.watch_geom, B.watch_body);
@@ -2364,12 +2424,15 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
 // kernels
 // ------------------------------------------------------------------------ //
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+template <class SP>
+__device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode) {
   extern __shared__ float smem[];
   int env = blockIdx.x;
   if (env >= B.nenv) return;
+  CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
+  const Lds& L = c.L;
   int* I = (int*)(smem + L.ints);
-  Ctx c{m, L, smem, I, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr};
+  c.I = I;
   // Zero the whole per-env LDS block once: reg_chol_solve32 reads a few words past
   // its packed triangles (padding lanes/columns, multiplied by exact zeros), and
   // those must be finite rather than whatever an earlier workgroup left behind.
@@ -2382,17 +2445,17 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
   float* qvel = c.f(L.qvel);
   float* ctrl = c.f(L.ctrl);
   float* ws = c.f(L.v5);
-  for (int i = LANE; i < m.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * m.nq + i];
-  for (int i = LANE; i < m.nv; i += DX_WAVE) {
-    qvel[i] = B.qvel[(size_t)env * m.nv + i];
-    ws[i] = B.qacc_ws[(size_t)env * m.nv + i];
+  for (int i = LANE; i < c.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * c.nq + i];
+  for (int i = LANE; i < c.nv; i += DX_WAVE) {
+    qvel[i] = B.qvel[(size_t)env * c.nv + i];
+    ws[i] = B.qacc_ws[(size_t)env * c.nv + i];
   }
-  for (int i = LANE; i < m.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * m.nu + i];
+  for (int i = LANE; i < c.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * c.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
-  if (m.nv > 32) {
+  if (c.nv > 32) {
     // lower-triangle index table for wave_cholesky: t -> (i << 8 | j), row-major
     unsigned short* tri = (unsigned short*)c.f(L.tri);
-    int T = m.nv * (m.nv + 1) / 2;
+    int T = c.nv * (c.nv + 1) / 2;
     for (int t = LANE; t < T; t += DX_WAVE) {
       int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
       while ((i + 1) * (i + 2) / 2 <= t) i++;
@@ -2408,20 +2471,20 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     forward(c, B.xfrc);
     if (mode == 0) {
       // warmstart <- solved qacc
-      for (int i = LANE; i < m.nv; i += DX_WAVE) ws[i] = c.f(L.qacc)[i];
+      for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(L.qacc)[i];
       SYNC();
       euler(c, &time);
     }
   }
   // debug record of the last forward
   if (B.dbg_qacc_smooth) {
-    for (int i = LANE; i < m.nv; i += DX_WAVE) {
-      B.dbg_qacc_smooth[(size_t)env * m.nv + i] = c.f(L.qacc_smooth)[i];
-      B.dbg_qfrc_smooth[(size_t)env * m.nv + i] = c.f(L.qfrc_smooth)[i];
+    for (int i = LANE; i < c.nv; i += DX_WAVE) {
+      B.dbg_qacc_smooth[(size_t)env * c.nv + i] = c.f(L.qacc_smooth)[i];
+      B.dbg_qfrc_smooth[(size_t)env * c.nv + i] = c.f(L.qfrc_smooth)[i];
     }
-    for (int k = LANE; k < m.nv * m.nv; k += DX_WAVE) {
-      int i = k / m.nv, j = k % m.nv;
-      B.dbg_M[(size_t)env * m.nv * m.nv + k] = c.f(L.M)[i >= j ? ti(i) + j : ti(j) + i];
+    for (int k = LANE; k < c.nv * c.nv; k += DX_WAVE) {
+      int i = k / c.nv, j = k % c.nv;
+      B.dbg_M[(size_t)env * c.nv * c.nv + k] = c.f(L.M)[i >= j ? ti(i) + j : ti(j) + i];
     }
     int n = I[I_NCON];
     for (int k = LANE; k < DX_NCON_MAX * 16; k += DX_WAVE) {
@@ -2444,17 +2507,73 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     B.niter[env] = I[I_NITER];
     B.ncand[env] = I[I_NCAND];
   }
-  for (int i = LANE; i < m.nv; i += DX_WAVE) B.qacc[(size_t)env * m.nv + i] = c.f(L.qacc)[i];
+  for (int i = LANE; i < c.nv; i += DX_WAVE) B.qacc[(size_t)env * c.nv + i] = c.f(L.qacc)[i];
   SYNC();
   stage_mark(c, ST_IO);
   observe(c, B, env);
   stage_mark(c, ST_OBSERVE);
-  for (int i = LANE; i < m.nq; i += DX_WAVE) B.qpos[(size_t)env * m.nq + i] = qpos[i];
-  for (int i = LANE; i < m.nv; i += DX_WAVE) {
-    B.qvel[(size_t)env * m.nv + i] = qvel[i];
-    B.qacc_ws[(size_t)env * m.nv + i] = ws[i];
+  for (int i = LANE; i < c.nq; i += DX_WAVE) B.qpos[(size_t)env * c.nq + i] = qpos[i];
+  for (int i = LANE; i < c.nv; i += DX_WAVE) {
+    B.qvel[(size_t)env * c.nv + i] = qvel[i];
+    B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
   }
   if (LANE == 0) B.time[env] = time;
+}
+
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+  step_body<SpecRT>(m, B, L, nsub, mode);
+}
+
+// ------------------------------------------------------------------------ //
+// model specializations (build.py writes dx_specs.inc from the shipped scenes)
+// ------------------------------------------------------------------------ //
+#if __has_include("dx_specs.inc")
+#include "dx_specs.inc"
+#endif
+#ifndef DX_SPECS
+#define DX_SPECS(X)
+#endif
+
+template <class SP>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_step_kernel_spec(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+  step_body<SP>(m, B, L, nsub, mode);
+}
+
+template <class SP>
+static bool spec_matches(const DevModel& d, const Lds& L) {
+  if (memcmp(&SP::L, &L, sizeof(Lds)) != 0) return false;
+#define DX_X(n) if (SP::n != d.n) return false;
+  DX_DIMS(DX_X)
+#undef DX_X
+  return true;
+}
+
+// Index of the specialization whose layout and dimensions equal the model's, or -1.
+int dx_spec_find(const DevModel& d, const Lds& L) {
+  int k = 0;
+#define DX_TRY(SP) if (spec_matches<SP>(d, L)) return k; k++;
+  DX_SPECS(DX_TRY)
+#undef DX_TRY
+  (void)k;
+  return -1;
+}
+
+hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+                          const Lds& L, int nsub, int mode) {
+  int k = 0;
+#define DX_LAUNCH(SP)                                                                                   \
+  if (spec == k) {                                                                                      \
+    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(nenv), dim3(64), lds, stream, m, B, L, nsub, mode); \
+    return hipGetLastError();                                                                           \
+  }                                                                                                     \
+  k++;
+  DX_SPECS(DX_LAUNCH)
+#undef DX_LAUNCH
+  (void)k;
+  hipLaunchKernelGGL(dx_step_kernel, dim3(nenv), dim3(64), lds, stream, m, B, L, nsub, mode);
+  return hipGetLastError();
 }
 
 // reset envs [env0, env0+n) to qpos0

@@ -85,6 +85,9 @@ int dx_model_lds_bytes(const dx_model* m);
    along local direction dir (direction-binned hulls); info =
    [vertex, cube-map cells per face edge (0: not binned), cell capacity]. */
 int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[3], int32_t info[3]);
+/* Build hook: the per-env LDS layout (dx_internal.h Lds, in words) followed by 16
+   model dimensions, for compile-time kernel specialization; returns the count. */
+int dx_model_layout(const dx_model* m, int32_t* out, int32_t n);
 /* Width (in 4-byte words per environment) of a dx_field. */
 int dx_field_width(const dx_model* m, int field);
 
