@@ -467,7 +467,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, B0 + r4(ntri));
   L.cand_max = 768;
   L.cand = B0;
-  end = std::max(end, L.cand + L.cand_max);
+  end = std::max(end, L.cand + L.cand_max + 4 * 36);  // + MPR portal points of the 4 groups
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_jar = take(L.nefc_max); L.efc_jv = take(L.nefc_max);

@@ -938,21 +938,43 @@ struct NpStats { int support, mpr, hit, plane_box, plane_convex, capsule, maxit;
 // MPR penetration on A - B (libccd ccdMPRPenetration structure, see the oracle's
 // mpr_penetration) as a resumable state machine: one support evaluation per
 // mpr_step, so the four 16-lane groups of a wave -- each on its own pair and in its
-// own MPR phase -- share every support pass.
+// own MPR phase -- share every support pass.  The portal points live in LDS (36
+// words per group: P0..P3 = v, a, b): kept in registers, every divergent phase
+// branch re-materialised all 36 of them at its join.
 //   phase 0: P1          phase 1: P2          phase 2: portal discovery (P3)
 //   phase 3: portal refinement towards the origin
 //   phase 4: refinement of the penetration (contact) portal
+#define MP_WORDS 36
+__device__ __forceinline__ void mp_st(float* d, const MPoint& p) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { d[k] = p.v[k]; d[3 + k] = p.a[k]; d[6 + k] = p.b[k]; }
+}
+__device__ __forceinline__ void mp_ld(const float* d, MPoint& p) {
+#pragma unroll
+  for (int k = 0; k < 3; k++) { p.v[k] = d[k]; p.a[k] = d[3 + k]; p.b[k] = d[6 + k]; }
+}
+__device__ __forceinline__ void v3sel(float* d, const float* s, bool c) {
+  d[0] = c ? s[0] : d[0]; d[1] = c ? s[1] : d[1]; d[2] = c ? s[2] : d[2];
+}
+__device__ __forceinline__ void portal_dir_v(const float* v1, const float* v2, const float* v3, float* dir) {
+  float a[3], b[3];
+  sub3(a, v2, v1);
+  sub3(b, v3, v1);
+  cross3(dir, a, b);
+  normalize3(dir);
+}
 struct MprState {
-  MPoint P0, P1, P2, P3;
+  float* P;  // this group's 36 LDS words
   float dir[3];
   int phase, it;
 };
 __device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprState& S) {
-  sub3(S.P0.v, A.center, B.center);
-  for (int k = 0; k < 3; k++) { S.P0.a[k] = A.center[k]; S.P0.b[k] = B.center[k]; }
-  if (fzero(S.P0.v[0]) && fzero(S.P0.v[1]) && fzero(S.P0.v[2])) S.P0.v[0] += 1e-9f;
-  S.P1 = S.P0; S.P2 = S.P0; S.P3 = S.P0;
-  S.dir[0] = -S.P0.v[0]; S.dir[1] = -S.P0.v[1]; S.dir[2] = -S.P0.v[2];
+  MPoint P0;
+  sub3(P0.v, A.center, B.center);
+  for (int k = 0; k < 3; k++) { P0.a[k] = A.center[k]; P0.b[k] = B.center[k]; }
+  if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-9f;
+  mp_st(S.P, P0);
+  S.dir[0] = -P0.v[0]; S.dir[1] = -P0.v[1]; S.dir[2] = -P0.v[2];
   normalize3(S.dir);
   S.phase = 0;
   S.it = 0;
@@ -962,90 +984,93 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
                                         float* pos, NpStats& st) {
   const float tol = 1e-6f;
   const int maxit = 50;
+  float* P = S.P;
+  float v0[3], v1[3], v2[3], v3[3];  // portal vertices (read before the support's memory round trip)
+  for (int k = 0; k < 3; k++) { v0[k] = P[k]; v1[k] = P[9 + k]; v2[k] = P[18 + k]; v3[k] = P[27 + k]; }
   MPoint p;
   float* dir = S.dir;
   support_pair(A, B, dir, p.a, p.b);
   sub3(p.v, p.a, p.b);
   st.support++;
   if (S.phase == 0) {
-    S.P1 = p;
-    float dt = dot3(S.P1.v, dir);
+    mp_st(P + 9, p);  // P1
+    float dt = dot3(p.v, dir);
     if (fzero(dt) || dt < 0) return 1;
-    cross3(dir, S.P0.v, S.P1.v);
+    cross3(dir, v0, p.v);
     if (fzero(dot3(dir, dir))) {
-      if (fzero(S.P1.v[0]) && fzero(S.P1.v[1]) && fzero(S.P1.v[2])) {
+      if (fzero(p.v[0]) && fzero(p.v[1]) && fzero(p.v[2])) {
         depth = 0;
         normal[0] = 0; normal[1] = 0; normal[2] = 1;
       } else {
-        depth = norm3(S.P1.v);
-        for (int k = 0; k < 3; k++) normal[k] = S.P1.v[k];
+        depth = norm3(p.v);
+        for (int k = 0; k < 3; k++) normal[k] = p.v[k];
         normalize3(normal);
       }
-      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (S.P1.a[k] + S.P1.b[k]);
+      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p.a[k] + p.b[k]);
       return 2;
     }
     normalize3(dir);
     S.phase = 1;
     return 0;
   }
-  if (S.phase == 1) {
-    S.P2 = p;
-    float dt = dot3(S.P2.v, dir);
+  if (S.phase == 1) {  // p = P2
+    float dt = dot3(p.v, dir);
     if (fzero(dt) || dt < 0) return 1;
     float va[3], vb[3];
-    sub3(va, S.P1.v, S.P0.v);
-    sub3(vb, S.P2.v, S.P0.v);
+    sub3(va, v1, v0);
+    sub3(vb, p.v, v0);
     cross3(dir, va, vb);
     normalize3(dir);
-    if (dot3(dir, S.P0.v) > 0) {
-      MPoint t = S.P1;
-      msel(S.P1, S.P2, true);
-      msel(S.P2, t, true);
+    if (dot3(dir, v0) > 0) {  // swap P1 and P2
+      MPoint q;
+      mp_ld(P + 9, q);
+      mp_st(P + 18, q);
+      mp_st(P + 9, p);
       dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
+    } else {
+      mp_st(P + 18, p);
     }
     S.phase = 2;
     S.it = 0;
     return 0;
   }
-  if (S.phase == 2) {
+  if (S.phase == 2) {  // p = P3
     if (S.it > 1000) return 1;
-    S.P3 = p;
-    float dt = dot3(S.P3.v, dir);
+    float dt = dot3(p.v, dir);
     if (fzero(dt) || dt < 0) return 1;
     float va[3], vb[3];
-    cross3(va, S.P1.v, S.P3.v);
-    dt = dot3(va, S.P0.v);
+    cross3(va, v1, p.v);
+    dt = dot3(va, v0);
     bool r2 = dt < 0 && !fzero(dt);
-    cross3(va, S.P3.v, S.P2.v);
-    dt = dot3(va, S.P0.v);
+    cross3(va, p.v, v2);
+    dt = dot3(va, v0);
     bool r1 = !r2 && dt < 0 && !fzero(dt);
-    msel(S.P2, S.P3, r2);
-    msel(S.P1, S.P3, r1);
+    mp_st(P + 27, p);
+    if (r2) mp_st(P + 18, p);
+    if (r1) mp_st(P + 9, p);
+    v3sel(v2, p.v, r2);
+    v3sel(v1, p.v, r1);
     S.it++;
     if (r1 || r2) {
-      sub3(va, S.P1.v, S.P0.v);
-      sub3(vb, S.P2.v, S.P0.v);
+      sub3(va, v1, v0);
+      sub3(vb, v2, v0);
       cross3(dir, va, vb);
       normalize3(dir);
     } else {
-      portal_dir(S.P1, S.P2, S.P3, dir);
-      S.phase = dot3(dir, S.P1.v) >= 0 ? 4 : 3;
+      portal_dir_v(v1, v2, p.v, dir);
+      S.phase = dot3(dir, v1) >= 0 ? 4 : 3;
       S.it = 0;
     }
     return 0;
   }
+  // phases 3 and 4 share one path: 3 stops on separation, 4 on convergence
   if (S.it > maxit) st.maxit++;
-  if (S.phase == 3) {
-    if (dot3(p.v, dir) < 0 || portal_reach_tol(S.P1, S.P2, S.P3, p, dir, tol) || S.it > maxit) return 1;
-    expand_portal(S.P0, S.P1, S.P2, S.P3, p);
-    S.it++;
-    portal_dir(S.P1, S.P2, S.P3, dir);
-    if (dot3(dir, S.P1.v) >= 0) { S.phase = 4; S.it = 0; }
-    return 0;
-  }
-  if (portal_reach_tol(S.P1, S.P2, S.P3, p, dir, tol) || S.it > maxit) {
+  float dv4 = dot3(p.v, dir);
+  bool stop = fminf(dv4 - dot3(v1, dir), fminf(dv4 - dot3(v2, dir), dv4 - dot3(v3, dir))) <= tol || S.it > maxit;
+  if (S.phase == 3 && (stop || dv4 < 0)) return 1;
+  if (S.phase == 4 && stop) {
     float cl[3];
-    float d2 = tri_origin_dist2(S.P1.v, S.P2.v, S.P3.v, cl);
+    float d2 = tri_origin_dist2(v1, v2, v3, cl);
     depth = sqrtf(d2);
     if (depth > 1e-20f) {
       float sc = 1.0f / depth;
@@ -1053,12 +1078,25 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
     } else {
       normal[0] = dir[0]; normal[1] = dir[1]; normal[2] = dir[2];
     }
-    find_pos(S.P0, S.P1, S.P2, S.P3, pos);
+    MPoint Q0, Q1, Q2, Q3;
+    mp_ld(P, Q0); mp_ld(P + 9, Q1); mp_ld(P + 18, Q2); mp_ld(P + 27, Q3);
+    find_pos(Q0, Q1, Q2, Q3, pos);
     return 2;
   }
-  expand_portal(S.P0, S.P1, S.P2, S.P3, p);
+  // expand the portal towards v4 = p (expand_portal)
+  float v4v0[3];
+  cross3(v4v0, p.v, v0);
+  bool c1 = dot3(v1, v4v0) > 0, c2 = dot3(v2, v4v0) > 0, c3 = dot3(v3, v4v0) > 0;
+  bool to1 = c1 ? c2 : !c3, to2 = !c1 && c3, to3 = c1 && !c2;
+  if (to1) mp_st(P + 9, p);
+  if (to2) mp_st(P + 18, p);
+  if (to3) mp_st(P + 27, p);
+  v3sel(v1, p.v, to1);
+  v3sel(v2, p.v, to2);
+  v3sel(v3, p.v, to3);
   S.it++;
-  portal_dir(S.P1, S.P2, S.P3, dir);
+  portal_dir_v(v1, v2, v3, dir);
+  if (S.phase == 3 && dot3(dir, v1) >= 0) { S.phase = 4; S.it = 0; }
   return 0;
 }
 
@@ -1383,6 +1421,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     float margin = 0;
     Shape A, B;
     MprState M;
+    M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
     for (;;) {
       bool act = q < ng;
       if (__ballot(act) == 0) break;
