@@ -27,7 +27,7 @@ EXPORTS = (
     "dx_env_create", "dx_env_destroy", "dx_env_batch", "dx_env_obs_dim", "dx_env_reset",
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
-    "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout",
+    "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout", "dx_env_goal_dim",
 )
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
@@ -35,8 +35,9 @@ STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constra
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
             26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc"}
 NSTAGE = 32
-OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES = range(6)
-TASK_REORIENT = 0
+OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES = range(7)
+TASK_REORIENT, TASK_REACH = 0, 1
+REACH_NPARAMS_HEAD = 26
 
 _lib = None
 
@@ -89,6 +90,7 @@ def load(path: str = LIB_PATH):
     L.dx_env_batch.restype = vp
     L.dx_env_batch.argtypes = [vp]
     L.dx_env_obs_dim.argtypes = [vp]
+    L.dx_env_goal_dim.argtypes = [vp]
     L.dx_env_reset.argtypes = [vp]
     L.dx_env_step.argtypes = [vp, vp]
     L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]

@@ -925,8 +925,14 @@ struct dx_env {
 
 extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task,
                                  uint64_t seed, const float* params, int32_t nparams) {
-  if (task != DX_TASK_REORIENT) { fail(DX_EINVAL, "unknown task kind"); return nullptr; }
-  if (!params || nparams < DX_REORIENT_NPARAMS) { fail(DX_EINVAL, "reorient needs 26 params"); return nullptr; }
+  if (task != DX_TASK_REORIENT && task != DX_TASK_REACH) { fail(DX_EINVAL, "unknown task kind"); return nullptr; }
+  if (!m) { fail(DX_EINVAL, "null model"); return nullptr; }
+  const int nq = m->dm.nq, nu = m->dm.nu;
+  if (!params || (task == DX_TASK_REORIENT && nparams < DX_REORIENT_NPARAMS) ||
+      (task == DX_TASK_REACH && nparams < DX_REACH_NPARAMS_HEAD + 3 * nq + nu * nq)) {
+    fail(DX_EINVAL, "too few task params");
+    return nullptr;
+  }
   dx_batch* b = dx_batch_create(m, nenv, device);
   if (!b) return nullptr;
   dx_env* e = new dx_env();
@@ -934,22 +940,46 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   const DevModel& d = b->dm;
   TaskParams& P = e->P;
   memset(&P, 0, sizeof(P));
-  P.kind = task;
+  P.kind = task == DX_TASK_REACH ? DX_KIND_REACH : DX_KIND_REORIENT;
   P.nenv = nenv; P.nq = d.nq; P.nv = d.nv; P.nu = d.nu; P.nsite = d.nsite;
+  P.seed = seed;
   e->nsub = (int)params[0];
   P.hand_nq = (int)params[1]; P.hand_nv = (int)params[2];
-  P.prop_qadr = (int)params[3]; P.prop_dadr = (int)params[4];
-  P.tip_site0 = (int)params[5]; P.ntips = (int)params[6];
-  P.successes_needed = (int)params[7]; P.steps_before_change = (int)params[8];
-  P.fall_termination = (int)params[9];
-  P.threshold = params[10]; P.eps = params[11]; P.w_orient = params[12]; P.w_success = params[13];
-  P.w_action = params[14]; P.max_time = params[15];
-  for (int k = 0; k < 3; k++) { P.bbox_lo[k] = params[16 + k]; P.bbox_hi[k] = params[19 + k]; }
-  int watch_geom = (int)params[22], watch_body = (int)params[23];
-  P.seed = seed;
-  P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + (P.prop_qadr >= 0 ? 17 : 0) + 4;
-  if (P.hand_nq > d.nq || P.hand_nv > d.nv || P.tip_site0 + P.ntips > d.nsite || e->nsub < 1 ||
-      (P.prop_qadr >= 0 && (P.prop_qadr + 7 > d.nq || P.prop_dadr + 6 > d.nv))) {
+  int watch_geom = -1, watch_body = -1;
+  bool bad = false;
+  if (task == DX_TASK_REORIENT) {
+    P.prop_qadr = (int)params[3]; P.prop_dadr = (int)params[4];
+    int tip0 = (int)params[5];
+    P.ntips = (int)params[6];
+    for (int t = 0; t < P.ntips && t < 8; t++) P.tip_sites[t] = tip0 + t;
+    P.successes_needed = (int)params[7]; P.steps_before_change = (int)params[8];
+    P.fall_termination = (int)params[9];
+    P.threshold = params[10]; P.eps = params[11]; P.w_orient = params[12]; P.w_success = params[13];
+    P.w_action = params[14]; P.max_time = params[15];
+    for (int k = 0; k < 3; k++) { P.bbox_lo[k] = params[16 + k]; P.bbox_hi[k] = params[19 + k]; }
+    watch_geom = (int)params[22]; watch_body = (int)params[23];
+    P.goal_dim = 4;
+    P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + (P.prop_qadr >= 0 ? 17 : 0) + 4;
+    bad = P.prop_qadr >= 0 && (P.prop_qadr + 7 > d.nq || P.prop_dadr + 6 > d.nv);
+  } else {
+    P.prop_qadr = -1; P.prop_dadr = -1;
+    P.ntips = (int)params[3];
+    for (int t = 0; t < P.ntips && t < 8; t++) P.tip_sites[t] = (int)params[4 + t];
+    P.successes_needed = (int)params[9]; P.steps_before_change = (int)params[10];
+    P.threshold = params[11]; P.max_time = params[12]; P.dense = (int)params[13];
+    P.range_frac = params[14]; P.goal_scale = params[15]; P.max_reject = (int)params[16];
+    P.ncoupled = (int)params[17];
+    for (int k = 0; k < P.ncoupled && k < 4; k++) {
+      P.coupled[k][0] = (int)params[18 + 2 * k];
+      P.coupled[k][1] = (int)params[19 + 2 * k];
+      bad = bad || P.coupled[k][0] < 0 || P.coupled[k][0] >= nq || P.coupled[k][1] < 0 || P.coupled[k][1] >= nq;
+    }
+    P.goal_dim = 3 * P.ntips;
+    P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + P.goal_dim;
+    bad = bad || P.hand_nq != d.nq || P.ncoupled > 4 || P.max_reject < 1;
+  }
+  for (int t = 0; t < P.ntips && t < 8; t++) bad = bad || P.tip_sites[t] < 0 || P.tip_sites[t] >= d.nsite;
+  if (bad || P.ntips > 8 || P.hand_nq > d.nq || P.hand_nv > d.nv || e->nsub < 1) {
     fail(DX_EINVAL, "task parameters inconsistent with the model");
     dx_batch_destroy(b);
     delete e;
@@ -960,24 +990,39 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   size_t E = nenv;
   auto al = [&](void** p, size_t bytes) { return balloc(b, p, bytes); };
   int rc = 0;
-  rc |= al((void**)&S.goal, E * 16); rc |= al((void**)&S.solve_start, E * 4);
+  rc |= al((void**)&S.goal, E * P.goal_dim * 4); rc |= al((void**)&S.solve_start, E * 4);
   rc |= al((void**)&S.reward, E * 4); rc |= al((void**)&S.discount, E * 4);
   rc |= al((void**)&S.obs, E * P.obs_dim * 4);
   rc |= al((void**)&S.successes, E * 4); rc |= al((void**)&S.counter, E * 4);
   rc |= al((void**)&S.registered, E * 4); rc |= al((void**)&S.exceeded, E * 4);
   rc |= al((void**)&S.step_type, E * 4); rc |= al((void**)&S.episode, E * 4);
   rc |= al((void**)&S.skip, E * 4); rc |= al((void**)&S.failure, E * 4);
-  if (rc) { dx_batch_destroy(b); delete e; return nullptr; }
-  std::vector<int> neg(E, -1);
-  if (hipMemcpy(S.episode, neg.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess) {
-    fail(DX_EHIP, "hipMemcpy failed");
-    dx_batch_destroy(b);
-    delete e;
-    return nullptr;
+  rc |= al((void**)&S.need, E * 4); rc |= al((void**)&S.goalnum, E * 4); rc |= al((void**)&S.goalfail, E * 4);
+  float* tdata = nullptr;
+  TaskParams* dP = nullptr;
+  TaskState* dS = nullptr;
+  if (!rc && task == DX_TASK_REACH) {
+    size_t nt = 3 * (size_t)nq + (size_t)nu * nq;
+    rc |= al((void**)&tdata, nt * 4);
+    if (!rc && hipMemcpy(tdata, params + DX_REACH_NPARAMS_HEAD, nt * 4, hipMemcpyHostToDevice) != hipSuccess)
+      rc = fail(DX_EHIP, "hipMemcpy failed");
+    P.tdata = tdata;
   }
+  if (!rc) rc |= al((void**)&dP, sizeof(TaskParams));
+  if (!rc) rc |= al((void**)&dS, sizeof(TaskState));
+  std::vector<int> neg(E, -1);
+  if (!rc && (hipMemcpy(S.episode, neg.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(dP, &P, sizeof(P), hipMemcpyHostToDevice) != hipSuccess ||
+              hipMemcpy(dS, &S, sizeof(S), hipMemcpyHostToDevice) != hipSuccess))
+    rc = fail(DX_EHIP, "hipMemcpy failed");
+  if (rc) { dx_batch_destroy(b); delete e; return nullptr; }
   b->db.skip = S.skip;
+  b->db.tp = dP;
+  b->db.ts = dS;
   return e;
 }
+
+extern "C" int dx_env_goal_dim(const dx_env* e) { return e ? e->P.goal_dim : fail(DX_EINVAL, "null env"); }
 
 extern "C" void dx_env_destroy(dx_env* e) {
   if (!e) return;
@@ -995,6 +1040,10 @@ static int env_run(dx_env* e, const float* action) {
   hipLaunchKernelGGL(dx_task_pre_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db,
                      b->dm.qpos0, action);
   HIPCHK(hipGetLastError());
+  // reach: goal rollouts / joint sampling for the envs that need them (the rest of
+  // the grid exits at once)
+  if (e->P.kind == DX_KIND_REACH)
+    if (int rc = launch_step(b, 1, 2)) return rc;
   if (int rc = launch_step(b, e->nsub, 0)) return rc;
   hipLaunchKernelGGL(dx_task_post_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db);
   HIPCHK(hipGetLastError());
@@ -1028,6 +1077,7 @@ extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
     case DX_OUT_STEP_TYPE: *devptr = e->S.step_type; return 0;
     case DX_OUT_GOAL: *devptr = e->S.goal; return 0;
     case DX_OUT_SUCCESSES: *devptr = e->S.successes; return 0;
+    case DX_OUT_GOAL_FAILURES: *devptr = e->S.goalfail; return 0;
   }
   return fail(DX_EINVAL, "unknown output");
 }

@@ -76,6 +76,8 @@ struct DevModel {
   const DXG float *gpair_friction, *gpair_solref, *gpair_solimp, *gpair_margin;
 };
 
+struct TaskParams;
+struct TaskState;
 struct DevBatch {
   int nenv;
   float *qpos, *qvel, *ctrl, *qacc_ws, *qacc, *time;
@@ -88,6 +90,8 @@ struct DevBatch {
   float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
   int* dbg_nefc;
   unsigned long long* stage_acc;  // [DX_NSTAGE] s_memtime cycles per stage (null: off)
+  const TaskParams* tp;           // device copies, reach sampling pass only (mode 2)
+  const TaskState* ts;
 };
 #define DX_NSTAGE 32
 
@@ -107,25 +111,45 @@ struct Lds {
   int total;
 };
 
-// Task (reorient) parameters and per-env task state, see dx_task.hip.
+// Task parameters and per-env task state, see dx_task.hip.
+enum { DX_KIND_REORIENT = 0, DX_KIND_REACH = 1 };
 struct TaskParams {
-  int kind;                 // 0 = reorient
+  int kind;                 // DX_KIND_*
   int nenv, nq, nv, nu, nsite;
   int hand_nq, hand_nv;     // hand joints are qpos[0:hand_nq], qvel[0:hand_nv]
-  int prop_qadr, prop_dadr; // free joint of the prop
-  int tip_site0, ntips;     // fingertip sites
-  int obs_dim;
+  int prop_qadr, prop_dadr; // free joint of the prop (reorient), -1 otherwise
+  int ntips;                // fingertip sites
+  int tip_sites[8];
+  int obs_dim, goal_dim;
   int successes_needed, steps_before_change, fall_termination;
   float threshold, eps, w_orient, w_success, w_action, max_time, timestep_ctrl;
   float bbox_lo[3], bbox_hi[3];
+  // reach (fingertip_position.py / dexterous_hand.py samplers)
+  int dense, max_reject, ncoupled;
+  int coupled[8][2];        // qpos[c[0]] = qpos[c[1]] after uniform joint sampling
+  float range_frac, goal_scale;
+  const float* tdata;       // device: ref[nq] | lo[nq] | hi[nq] | position->control [nu][nq]
   uint64_t seed;
 };
 
 struct TaskState {
   float *goal, *solve_start, *reward, *discount, *obs;
   int *successes, *counter, *registered, *exceeded, *step_type, *episode, *skip, *failure;
+  int *need, *goalnum, *goalfail;  // reach: bit0 next_goal, bit1 joint init; goals drawn; rejected-out goals
 };
 
+// Counter-based RNG: splitmix64 over (seed, env, episode, draw).
+__device__ __forceinline__ uint64_t dx_mix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, int draw) {
+  uint64_t h = dx_mix64(seed ^ dx_mix64(((uint64_t)env << 32) ^ (uint64_t)(uint32_t)episode) ^
+                        dx_mix64(0x51ed27ull + (uint64_t)(uint32_t)draw));
+  return (float)((h >> 40) * (1.0 / 16777216.0));
+}
 
 // dx_step.hip: specialized-kernel lookup and launch (host side)
 int dx_spec_find(const DevModel& d, const Lds& L);

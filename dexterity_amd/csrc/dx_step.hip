@@ -2460,6 +2460,126 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
 }
 
 // ------------------------------------------------------------------------ //
+// reach: fingertip goals and collision-free joint angles (mode 2 pass)
+// ------------------------------------------------------------------------ //
+// Fingertip sites of the current kinematics: lane t < 3 * ntips holds coordinate
+// t % 3 of tip t / 3 (site_xpos of dexterous_hand.py:286-291).
+template <class Ctx>
+__device__ __forceinline__ float tip_coord(const Ctx& c, const TaskParams& P) {
+  const DevModel& m = c.m;
+  float gc = 0;
+  if (LANE < 3 * P.ntips) {
+    int t = LANE / 3, e = LANE - 3 * t;
+    int sid = P.tip_sites[t];
+    int b = m.site_bodyid[sid];
+    const float* xp = c.f(c.L.xpos) + 3 * b;
+    const float* xm = c.f(c.L.xmat) + 9 * b;
+    const DXG float* sp = m.site_pos + 3 * sid;
+    gc = xp[e] + xm[3 * e] * sp[0] + xm[3 * e + 1] * sp[1] + xm[3 * e + 2] * sp[2];
+  }
+  return gc;
+}
+// Any contact with dist <= 1e-8 at the current kinematics (has_self_collision,
+// utils/mujoco_collisions.py:95-127; in the reach scenes every contact pair is
+// hand-hand because the ground is disabled, reach.py:131-132).
+template <class Ctx>
+__device__ __forceinline__ bool contact_now(const Ctx& c) {
+  collision(c, 0, -1, -1);
+  int n = c.I[I_NCON];
+  const float* con = c.f(c.L.con);
+  int hit = 0;
+  for (int k = LANE; k < n; k += DX_WAVE) hit |= con[DX_CON_STRIDE * k + 12] <= 1e-8f;
+  return __any(hit) != 0;
+}
+
+// FingertipCartesianPosition.next_goal (fingertip_position.py:72-125) and
+// DexterousHand.sample_collision_free_joint_angles (dexterous_hand.py:144-168) for
+// one environment, with the reference's side effects on the physics state: after a
+// goal draw qpos and ctrl are restored, qvel / warm start keep the last rollout's
+// values, time advances by the accepted rollout (a rejected one restores it).
+template <class Ctx>
+__device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int env, float& time) {
+  const TaskParams& P = *B.tp;
+  const TaskState& T = *B.ts;
+  float* qpos = c.f(c.L.qpos);
+  float* ctrl = c.f(c.L.ctrl);
+  float* ws = c.f(c.L.v5);
+  const int nq = c.nq, nu = c.nu;
+  const int need = T.need[env];
+  const int ep = T.episode[env];
+  const float* ref = P.tdata;
+  const float* lo = ref + nq;
+  const float* hi = lo + nq;
+  const float* p2c = hi + nq;
+  const float q_init = LANE < nq ? qpos[LANE] : 0.f;
+  const float c_init = LANE < nu ? ctrl[LANE] : 0.f;
+  if (need & 1) {
+    const int g = T.goalnum[env];
+    float gc = 0;
+    bool ok = false;
+    for (int a = 0; a < P.max_reject; a++) {
+      // qpos_desired ~ N(midrange, scale * range), clipped to the joint range
+      if (LANE < nq) {
+        int draw = 0x100000 + (((g & 4095) * 128 + (a & 127)) * 64 + LANE) * 2;
+        float u1 = dx_urand(P.seed, env, ep, draw), u2 = dx_urand(P.seed, env, ep, draw + 1);
+        float z = sqrtf(-2.0f * logf(fmaxf(u1, 1e-12f))) * cosf(6.283185307179586f * u2);
+        float l = lo[LANE], h = hi[LANE];
+        qpos[LANE] = fminf(h, fmaxf(l, ref[LANE] + P.goal_scale * (h - l) * z));
+      }
+      SYNC();
+      // joint_positions_to_control (shadow_hand_e.py:109-119; identity for Adroit)
+      if (LANE < nu) {
+        float sacc = 0;
+        for (int j = 0; j < nq; j++) sacc += p2c[LANE * nq + j] * qpos[j];
+        ctrl[LANE] = sacc;
+      }
+      SYNC();
+      const float t0 = time;
+      for (int s = 0; s < 2; s++) {  // JointStaticIsolator: two physics steps
+        forward(c, B.xfrc);
+        for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
+        SYNC();
+        euler(c, &time);
+      }
+      kinematics(c);
+      gc = tip_coord(c, P);
+      if (!contact_now(c)) { ok = true; break; }
+      time = t0;
+    }
+    if (LANE < 3 * P.ntips) T.goal[(size_t)env * P.goal_dim + LANE] = gc;
+    if (LANE == 0) {
+      T.goalnum[env] = g + 1;
+      if (!ok) T.goalfail[env] += 1;  // the reference raises GoalInitializationError here
+      // GoalTask.initialize_episode / before_step bookkeeping (task.py:137-165)
+      T.counter[env] = 0;
+      T.exceeded[env] = 0;
+      T.registered[env] = 0;
+      T.solve_start[env] = time;
+    }
+    if (LANE < nq) qpos[LANE] = q_init;
+    if (LANE < nu) ctrl[LANE] = c_init;
+    SYNC();
+  }
+  if (need & 2) {
+    // uniform within range_fraction * range, coupled joints equalised, until no contact
+    for (int a = 0; a < 1000; a++) {
+      if (LANE < nq) {
+        float u = dx_urand(P.seed, env, ep, 0x200000 + a * 64 + LANE);
+        float l = P.range_frac * lo[LANE], h = P.range_frac * hi[LANE];
+        qpos[LANE] = l + (h - l) * u;
+      }
+      SYNC();
+      if (LANE < P.ncoupled) qpos[P.coupled[LANE][0]] = qpos[P.coupled[LANE][1]];
+      SYNC();
+      kinematics(c);
+      if (!contact_now(c)) break;
+    }
+  }
+  if (LANE == 0) T.need[env] = 0;
+  SYNC();
+}
+
+// ------------------------------------------------------------------------ //
 // kernels
 // ------------------------------------------------------------------------ //
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
@@ -2468,6 +2588,7 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   extern __shared__ float smem[];
   int env = blockIdx.x;
   if (env >= B.nenv) return;
+  if (mode == 2 && !B.ts->need[env]) return;
   CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
   const Lds& L = c.L;
   int* I = (int*)(smem + L.ints);
@@ -2504,6 +2625,16 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   }
   float time = B.time[env];
   SYNC();
+  if (mode == 2) {  // reach sampling pass: new state only, no outputs
+    reach_prep(c, B, env, time);
+    for (int i = LANE; i < c.nq; i += DX_WAVE) B.qpos[(size_t)env * c.nq + i] = qpos[i];
+    for (int i = LANE; i < c.nv; i += DX_WAVE) {
+      B.qvel[(size_t)env * c.nv + i] = qvel[i];
+      B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
+    }
+    if (LANE == 0) B.time[env] = time;
+    return;
+  }
   int steps = mode == 0 ? nsub : 1;
   if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
   for (int s = 0; s < steps; s++) {

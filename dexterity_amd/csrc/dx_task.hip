@@ -25,16 +25,8 @@
 
 enum { ST_FIRST = 0, ST_MID = 1, ST_LAST = 2 };
 
-// counter-based RNG: splitmix64 over (seed, env, episode, draw)
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z += 0x9e3779b97f4a7c15ull;
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-  return z ^ (z >> 31);
-}
 __device__ __forceinline__ float urand(uint64_t seed, int env, int episode, int draw) {
-  uint64_t h = mix64(seed ^ mix64(((uint64_t)env << 32) ^ (uint64_t)episode) ^ mix64(0x51ed27ull + draw));
-  return (float)((h >> 40) * (1.0 / 16777216.0));
+  return dx_urand(seed, env, episode, draw);
 }
 // uniform unit quaternion (Shoemake), as dm_control rotations.UniformQuaternion
 __device__ void uniform_quat(uint64_t seed, int env, int episode, int draw0, float* q) {
@@ -64,8 +56,7 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
     for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = action[(size_t)env * P.nu + i];
   int st = S.step_type[env];
   if (st == ST_LAST || S.episode[env] < 0) {
-    // initialize_episode: qpos0, prop placed uniformly in the bbox with a uniform
-    // orientation, new goal; reorient.py:182-188
+    // initialize_episode from a reset physics state (mj_resetData)
     int ep = S.episode[env] + 1;
     S.episode[env] = ep;
     float* q = B.qpos + (size_t)env * P.nq;
@@ -77,12 +68,21 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
     if (action)
       for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = 0;
     B.time[env] = 0;
-    float* g = S.goal + 4 * env;
-    uniform_quat(P.seed, env, ep, 0, g);  // goal first (GoalTask.initialize_episode)
-    if (P.prop_qadr >= 0) {
-      for (int k = 0; k < 3; k++)
-        q[P.prop_qadr + k] = P.bbox_lo[k] + (P.bbox_hi[k] - P.bbox_lo[k]) * urand(P.seed, env, ep, 3 + k);
-      uniform_quat(P.seed, env, ep, 6, q + P.prop_qadr + 3);
+    if (P.kind == DX_KIND_REORIENT) {
+      // reorient.py:182-188: goal first (GoalTask.initialize_episode), then the prop
+      // placed uniformly in the bbox with a uniform orientation
+      float* g = S.goal + P.goal_dim * env;
+      uniform_quat(P.seed, env, ep, 0, g);
+      if (P.prop_qadr >= 0) {
+        for (int k = 0; k < 3; k++)
+          q[P.prop_qadr + k] = P.bbox_lo[k] + (P.bbox_hi[k] - P.bbox_lo[k]) * urand(P.seed, env, ep, 3 + k);
+        uniform_quat(P.seed, env, ep, 6, q + P.prop_qadr + 3);
+      }
+    } else {
+      // reach.py:155-168: fingertip goal (physics rollouts) and collision-free joint
+      // angles, both drawn by the sampling pass of the step kernel (mode 2)
+      S.need[env] = 3;
+      S.goalnum[env] = 0;
     }
     S.successes[env] = 0;
     S.counter[env] = 0;
@@ -96,13 +96,24 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
   S.skip[env] = 0;
   // GoalTask.before_step (task.py:154-165)
   if (S.counter[env] > P.steps_before_change) {
-    int draw = 16 + 3 * S.successes[env];
-    uniform_quat(P.seed, env, S.episode[env], draw, S.goal + 4 * env);
-    S.counter[env] = 0;
-    S.exceeded[env] = 0;
-    S.solve_start[env] = B.time[env];
-    S.registered[env] = 0;
+    if (P.kind == DX_KIND_REORIENT) {
+      int draw = 16 + 3 * S.successes[env];
+      uniform_quat(P.seed, env, S.episode[env], draw, S.goal + P.goal_dim * env);
+      S.counter[env] = 0;
+      S.exceeded[env] = 0;
+      S.solve_start[env] = B.time[env];
+      S.registered[env] = 0;
+    } else {
+      S.need[env] = 1;  // next_goal and the bookkeeping run in the sampling pass
+    }
   }
+}
+
+// tanh_squared(x, margin, 0.95) of manipulation/shared/rewards.py:18-28
+__device__ __forceinline__ float tanh_squared(float x, float margin) {
+  const float w = 2.178272210300875f / margin;  // arctanh(sqrt(0.95))
+  float t = tanhf(w * x);
+  return t * t;
 }
 
 extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B) {
@@ -110,11 +121,30 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
   if (env >= P.nenv) return;
   const float* q = B.qpos + (size_t)env * P.nq;
   const float* v = B.qvel + (size_t)env * P.nv;
-  const float* g = S.goal + 4 * env;
+  const float* g = S.goal + P.goal_dim * env;
+  const bool reach = P.kind == DX_KIND_REACH;
   float cur[4] = {1, 0, 0, 0};
   if (P.prop_qadr >= 0)
     for (int k = 0; k < 4; k++) cur[k] = q[P.prop_qadr + 3 + k];
-  float dist = quat_distance(g, cur);
+  // goal distance: orientation (prop_orientation.py:40-50) or per-fingertip
+  // Cartesian distances (fingertip_position.py:127-137)
+  float dist = 0, dtip[8];
+  bool all_close = true;
+  float rsum = 0;
+  if (reach) {
+    for (int t = 0; t < P.ntips; t++) {
+      const float* x = B.site_xpos + ((size_t)env * P.nsite + P.tip_sites[t]) * 3;
+      float d0 = g[3 * t] - x[0], d1 = g[3 * t + 1] - x[1], d2 = g[3 * t + 2] - x[2];
+      dtip[t] = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+      bool close = dtip[t] <= P.threshold;
+      all_close = all_close && close;
+      // reach.py:196-210: dense -tanh^2(d, 0.1), sparse -1, 0 within the threshold
+      rsum += close ? 0.f : (P.dense ? -tanh_squared(dtip[t], 0.1f) : -1.f);
+    }
+  } else {
+    dist = quat_distance(g, cur);
+    all_close = dist <= P.threshold;
+  }
   bool reset = S.skip[env] != 0;
   if (reset) {
     S.step_type[env] = ST_FIRST;
@@ -123,25 +153,29 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
   } else {
     // GoalTask.after_step (task.py:167-185)
     float time = B.time[env];
-    if (dist <= P.threshold) {
+    if (all_close) {
       S.counter[env] += 1;
       if (!S.registered[env]) { S.successes[env] += 1; S.registered[env] = 1; }
     } else if (P.max_time > 0 && time - S.solve_start[env] > P.max_time) {
       S.exceeded[env] = 1;
     }
     // ReOrient.after_step: fall detection (prop-ground contact at the new state)
-    int failure = P.fall_termination && B.watch && B.watch[env];
+    int failure = !reach && P.fall_termination && B.watch && B.watch[env];
     S.failure[env] = failure;
     bool success_done = S.successes[env] >= P.successes_needed;
     bool terminate = success_done || S.exceeded[env] || failure;
-    // reward (reorient.py:238-284): 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
-    float cn = 0;
-    for (int i = 0; i < P.nu; i++) {
-      float c = B.ctrl[(size_t)env * P.nu + i];
-      cn += c * c;
+    float r;
+    if (reach) {
+      r = rsum / (float)P.ntips;
+    } else {
+      // reorient.py:238-284: 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
+      float cn = 0;
+      for (int i = 0; i < P.nu; i++) {
+        float c = B.ctrl[(size_t)env * P.nu + i];
+        cn += c * c;
+      }
+      r = P.w_orient * (1.0f / (dist + P.eps)) + P.w_success * (dist <= P.threshold ? 1.0f : 0.0f) + P.w_action * cn;
     }
-    float r = P.w_orient * (1.0f / (dist + P.eps)) + P.w_success * (dist <= P.threshold ? 1.0f : 0.0f) +
-              P.w_action * cn;
     S.reward[env] = r;
     // discount (reorient.py:222-225, task.py:195-204)
     S.discount[env] = failure ? 1.0f : (success_done ? 0.0f : 1.0f);
@@ -149,7 +183,8 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
   }
   // observation (STATE_ONLY), flat layout:
   // [sin/cos(qpos_hand) 2*hand_nq | qvel_hand | tip pos 3*ntips | tip linvel 3*ntips |
-  //  prop pos 3 | prop quat 4 | prop linvel 3 | prop angvel 3 | target quat 4 | goal 4]
+  //  reorient: prop pos 3 | prop quat 4 | prop linvel 3 | prop angvel 3 | target quat 4 |
+  //  goal (4 quaternion, or 3*ntips fingertip positions for reach)]
   float* o = S.obs + (size_t)env * P.obs_dim;
   int k = 0;
   for (int i = 0; i < P.hand_nq; i++) {
@@ -160,9 +195,9 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
   }
   for (int i = 0; i < P.hand_nv; i++) o[k++] = v[i];
   for (int t = 0; t < P.ntips; t++)
-    for (int e = 0; e < 3; e++) o[k++] = B.site_xpos[((size_t)env * P.nsite + P.tip_site0 + t) * 3 + e];
+    for (int e = 0; e < 3; e++) o[k++] = B.site_xpos[((size_t)env * P.nsite + P.tip_sites[t]) * 3 + e];
   for (int t = 0; t < P.ntips; t++)
-    for (int e = 0; e < 3; e++) o[k++] = B.site_vel[((size_t)env * P.nsite + P.tip_site0 + t) * 6 + e];
+    for (int e = 0; e < 3; e++) o[k++] = B.site_vel[((size_t)env * P.nsite + P.tip_sites[t]) * 6 + e];
   if (P.prop_qadr >= 0) {
     for (int e = 0; e < 3; e++) o[k++] = q[P.prop_qadr + e];
     float n = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2] + cur[3] * cur[3]);
@@ -177,7 +212,7 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
     for (int e = 0; e < 3; e++) o[k++] = R[3 * e] * wl[0] + R[3 * e + 1] * wl[1] + R[3 * e + 2] * wl[2];
     for (int e = 0; e < 4; e++) o[k++] = g[e];  // target_prop/orientation (hint cube = goal)
   }
-  for (int e = 0; e < 4; e++) o[k++] = g[e];  // goal_state
+  for (int e = 0; e < P.goal_dim; e++) o[k++] = g[e];  // goal_state
 }
 
 // Uniform random actions within the actuator ctrlrange: the synthetic agent of

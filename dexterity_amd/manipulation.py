@@ -9,6 +9,10 @@ reference's constants and the host-side API.
 
 Suite (names as in the reference):
   reorient.state_dense   manipulation/tasks/reorient.py:367-371  (Shadow hand + cube)
+  reach.state_dense      manipulation/tasks/reach.py:252-259     (Adroit hand, fingertip goals)
+  reach.state_sparse     manipulation/tasks/reach.py:262-269
+  reach_shadow.state_dense  BASELINE.json config 2: reach with the Shadow hand,
+                         contact-free smooth dynamics (not a reference suite entry)
 """
 
 from __future__ import annotations
@@ -23,6 +27,7 @@ import numpy as np
 
 from dexterity_amd import _lib
 from dexterity_amd import effectors as effectors_lib
+from dexterity_amd import hands as hands_lib
 from dexterity_amd import physics as physics_lib
 from dexterity_amd.mjcf.compiler import CompiledModel
 from dexterity_amd.specs import Array, BoundedArray, StepType, TimeStep
@@ -57,7 +62,8 @@ class ReOrientConfig:
         return self.max_steps_single_solve * self.control_timestep
 
 
-def observation_layout(hand_nq: int, hand_nv: int, ntips: int, with_prop: bool, hand: str) -> "collections.OrderedDict[str, slice]":
+def observation_layout(hand_nq: int, hand_nv: int, ntips: int, with_prop: bool, hand: str,
+                       goal_dim: int = 4) -> "collections.OrderedDict[str, slice]":
     """Named slices of the flat observation vector written by dx_task_post_kernel."""
     out = collections.OrderedDict()
     k = 0
@@ -77,7 +83,7 @@ def observation_layout(hand_nq: int, hand_nv: int, ntips: int, with_prop: bool, 
         add("prop/linear_velocity", 3)
         add("prop/angular_velocity", 3)
         add("target_prop/orientation", 4)
-    add("goal_state", 4)
+    add("goal_state", goal_dim)
     return out
 
 
@@ -85,6 +91,7 @@ class ReOrient:
     """Batched counterpart of `ReOrient` (reorient.py:90-235)."""
 
     domain = "reorient"
+    kind = _lib.TASK_REORIENT
 
     def __init__(self, config: ReOrientConfig = ReOrientConfig(), asset: str = "shadow_reorient.npz"):
         self.config = config
@@ -130,6 +137,96 @@ class ReOrient:
         return observation_layout(self.hand_nq, self.hand_nv, self.ntips, True, self.hand_name)
 
 
+@dataclasses.dataclass(frozen=True)
+class ReachConfig:
+    """Constants of manipulation/tasks/reach.py:30-70 and fingertip_position.py:21-35."""
+
+    physics_timestep: float = 0.02  # reach.py:54
+    control_timestep: float = 0.02  # reach.py:59
+    success_threshold: float = 0.01  # reach.py:47 (_DISTANCE_TO_TARGET_THRESHOLD)
+    successes_needed: int = 50  # reach.py:62
+    steps_before_moving_target: int = 5  # reach.py:37
+    max_steps_single_solve: int = 150  # reach.py:65
+    init_joint_range_fraction: float = 0.5  # reach.py:34
+    goal_scale: float = 0.1  # fingertip_position.py:26
+    max_rejection_samples: int = 100  # fingertip_position.py:25
+    dense_reward: bool = True  # reach.py:252-269 (state_dense / state_sparse)
+
+    @property
+    def n_sub_steps(self) -> int:
+        return int(round(self.control_timestep / self.physics_timestep))
+
+    @property
+    def max_time_per_goal(self) -> float:
+        return self.max_steps_single_solve * self.control_timestep
+
+
+class Reach:
+    """Batched counterpart of `Reach` (reach.py:73-210) over `GoalTask`.
+
+    Goals come from the batched `FingertipCartesianPosition.next_goal`
+    (fingertip_position.py:72-125: joint targets ~ N(midrange, 0.1 * range), two
+    physics steps, rejected while the hand self-collides) and episodes start from
+    `sample_collision_free_joint_angles(range_fraction=0.5)` (dexterous_hand.py:
+    120-168); both run on the device inside the step kernel (dx_step.hip reach_prep).
+    """
+
+    domain = "reach"
+    kind = _lib.TASK_REACH
+
+    def __init__(self, config: ReachConfig = ReachConfig(), hand: str = "adroit"):
+        self.config = config
+        asset = {"adroit": "adroit_reach.npz", "shadow": "shadow_reach.npz"}[hand]
+        self.compiled = CompiledModel.load(os.path.join(ASSETS, asset))
+        cm = self.compiled
+        if abs(cm.timestep - config.physics_timestep) > 1e-12:
+            raise ValueError("asset timestep does not match the task's physics timestep")
+        names = cm.names
+        if hand == "adroit":
+            self.hand_name = "adroit_hand"
+            tips = [f"{self.hand_name}/{s}" for s in hands_lib.ADROIT_FINGERTIP_SITES]
+            self.position_to_control = np.eye(cm.nu, cm.nq)  # adroit_hand.py:106-112
+            coupled = []
+        else:
+            self.hand_name = "shadow_hand_e"
+            tips = [f"{self.hand_name}/{t}_site" for t in hands_lib.SHADOW_FINGERTIPS]
+            self.position_to_control = hands_lib.POSITION_TO_CONTROL  # shadow_hand_e.py:109-119
+            coupled = [(ids[0], ids[-1]) for ids in hands_lib.COUPLED_JOINT_IDS]  # shadow_hand_e.py:124-129
+        self.tip_sites = [names["site"].index(t) for t in tips]
+        self.coupled = coupled
+        self.hand_nq = cm.nq
+        self.hand_nv = cm.nv
+        self.ntips = len(self.tip_sites)
+        self.actuator_ids = list(range(cm.nu))
+        self.hand_effector = effectors_lib.HandEffector(self.actuator_ids, self.hand_name)
+        # FingertipCartesianPosition.initialize_episode (fingertip_position.py:55-62)
+        self.gravity_compensation = physics_lib.gravity_compensation(cm, self.hand_name + "/")
+        rng = np.asarray(cm.arrays["jnt_range"], dtype=np.float64).reshape(-1, 2)[: cm.nq]
+        self.joint_range = rng
+
+    def params(self) -> np.ndarray:
+        c, cm = self.config, self.compiled
+        head = np.zeros(_lib.REACH_NPARAMS_HEAD, dtype=np.float32)
+        head[0] = c.n_sub_steps
+        head[1], head[2], head[3] = self.hand_nq, self.hand_nv, self.ntips
+        head[4:4 + self.ntips] = self.tip_sites
+        head[9], head[10] = c.successes_needed, c.steps_before_moving_target
+        head[11], head[12] = c.success_threshold, c.max_time_per_goal
+        head[13] = 1.0 if c.dense_reward else 0.0
+        head[14], head[15], head[16] = c.init_joint_range_fraction, c.goal_scale, c.max_rejection_samples
+        head[17] = len(self.coupled)
+        for k, (j, src) in enumerate(self.coupled):
+            head[18 + 2 * k], head[19 + 2 * k] = j, src
+        lo, hi = self.joint_range[:, 0], self.joint_range[:, 1]
+        mid = self.joint_range.mean(axis=1)  # fingertip_position.py:80-82
+        tail = np.concatenate([mid, lo, hi, np.asarray(self.position_to_control, dtype=np.float64).ravel()])
+        assert tail.size == 3 * cm.nq + cm.nu * cm.nq
+        return np.concatenate([head, tail.astype(np.float32)])
+
+    def observation_layout(self):
+        return observation_layout(self.hand_nq, self.hand_nv, self.ntips, False, self.hand_name, 3 * self.ntips)
+
+
 class GoalEnvironment:
     """Batched `GoalEnvironment` (environment.py:9-34) over `num_envs` environments.
 
@@ -145,7 +242,7 @@ class GoalEnvironment:
         L = _lib.load()
         p = task.params()
         self._seed = 0 if seed is None else int(seed)
-        self.ptr = L.dx_env_create(self.model.ptr, self.num_envs, device, _lib.TASK_REORIENT,
+        self.ptr = L.dx_env_create(self.model.ptr, self.num_envs, device, task.kind,
                                    self._seed, p.ctypes.data, len(p))
         if not self.ptr:
             raise _lib.DxError(f"dx_env_create failed: {L.dx_last_error().decode()}")
@@ -154,6 +251,7 @@ class GoalEnvironment:
         # gravity compensation (shadow_hand_e.py:35-41 in initialize_episode)
         self.physics.set_xfrc(task.gravity_compensation)
         self.obs_dim = _lib.check(L.dx_env_obs_dim(self.ptr))
+        self.goal_dim = _lib.check(L.dx_env_goal_dim(self.ptr))
         self._layout = task.observation_layout()
         self._action_spec = task.hand_effector.action_spec(self.physics)
         self._host_action = np.zeros((self.num_envs, self.model.nu), dtype=np.float32)
@@ -231,7 +329,10 @@ class GoalEnvironment:
         return TimeStep(st.astype(np.int32), rew, disc, observation)
 
     def goals(self) -> np.ndarray:
-        return self._read(_lib.OUT_GOAL, np.float32, 4)
+        return self._read(_lib.OUT_GOAL, np.float32, self.goal_dim)
+
+    def goal_failures(self) -> np.ndarray:
+        return self._read(_lib.OUT_GOAL_FAILURES, np.int32, 1)[:, 0]
 
     def successes(self) -> np.ndarray:
         return self._read(_lib.OUT_SUCCESSES, np.int32, 1)[:, 0]
@@ -253,7 +354,12 @@ def _copy_d2h(out: np.ndarray, devptr: int) -> None:
 
 _hip = None
 
-SUITE = {("reorient", "state_dense"): ReOrient}
+SUITE = {
+    ("reorient", "state_dense"): ReOrient,
+    ("reach", "state_dense"): lambda: Reach(ReachConfig(dense_reward=True), hand="adroit"),
+    ("reach", "state_sparse"): lambda: Reach(ReachConfig(dense_reward=False), hand="adroit"),
+    ("reach_shadow", "state_dense"): lambda: Reach(ReachConfig(dense_reward=True), hand="shadow"),
+}
 ALL_TASKS = tuple(sorted(SUITE))
 ALL_NAMES = [".".join(t) for t in ALL_TASKS]
 
@@ -269,4 +375,5 @@ def load(domain_name: str, task_name: str, seed: Optional[int] = None, num_envs:
     return GoalEnvironment(SUITE[key](), num_envs=num_envs, seed=seed, device=device)
 
 
-__all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "ALL_TASKS", "ALL_NAMES", "StepType"]
+__all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "Reach", "ReachConfig", "ALL_TASKS",
+           "ALL_NAMES", "StepType"]

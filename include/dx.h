@@ -139,7 +139,7 @@ int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
  * observation vector, for every env, with dm_env auto-reset (an env that returned
  * LAST is re-initialised by its next step and returns FIRST). */
 typedef struct dx_env dx_env;
-enum dx_task_kind { DX_TASK_REORIENT = 0 };
+enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
 /* Reorient params (float[26]), reorient.py:40-78 / task.py:120-135:
  *  0 n_sub_steps  1 hand_nq  2 hand_nv  3 prop_qposadr  4 prop_dofadr
  *  5 first fingertip site  6 n fingertips  7 successes_needed
@@ -148,19 +148,32 @@ enum dx_task_kind { DX_TASK_REORIENT = 0 };
  *  15 max_time_per_goal  16-18 prop bbox lower  19-21 prop bbox upper
  *  22 ground geom  23 prop body  24-25 reserved */
 #define DX_REORIENT_NPARAMS 26
+/* Reach params (float[26 + 3*nq + nu*nq]), reach.py:43-70, task.py:120-135,
+ * fingertip_position.py:21-35, dexterous_hand.py:120-168:
+ *  0 n_sub_steps  1 hand_nq (= nq)  2 hand_nv  3 n fingertips  4-8 fingertip sites
+ *  9 successes_needed  10 steps_before_changing_goal  11 success_threshold
+ *  12 max_time_per_goal  13 dense reward (1) / sparse (0)  14 init joint range fraction
+ *  15 goal sampling scale  16 max rejection samples  17 n coupled joint pairs
+ *  18-25 coupled pairs (joint, source joint): qpos[joint] = qpos[source]
+ *  26..  joint midrange [nq], lower [nq], upper [nq], position->control [nu][nq] */
+#define DX_REACH_NPARAMS_HEAD 26
 enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT_STEP_TYPE = 3,
-                  DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5 };
+                  DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5, DX_OUT_GOAL_FAILURES = 6 };
 dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task, uint64_t seed,
                       const float* params, int32_t nparams);
 void dx_env_destroy(dx_env* e);
 dx_batch* dx_env_batch(dx_env* e);
 int dx_env_obs_dim(const dx_env* e);
+/* Goal width: 4 (reorient quaternion) or 3 * n fingertips (reach positions). */
+int dx_env_goal_dim(const dx_env* e);
 /* Re-initialises every env (initialize_episode) and computes FIRST observations. */
 int dx_env_reset(dx_env* e);
 /* One control step for every env; action is [nenv][nu] float32, device memory. */
 int dx_env_step(dx_env* e, const float* action);
 /* Device pointers of the outputs: obs [nenv][obs_dim] f32, reward/discount [nenv] f32,
- * step_type [nenv] i32 (0 FIRST, 1 MID, 2 LAST), goal [nenv][4] f32, successes i32. */
+ * step_type [nenv] i32 (0 FIRST, 1 MID, 2 LAST), goal [nenv][goal_dim] f32, successes i32,
+ * goal failures i32 (reach goals that exhausted the rejection samples: the reference
+ * raises GoalInitializationError there, fingertip_position.py:118-122). */
 int dx_env_output(dx_env* e, int which, void** devptr);
 /* Library-owned [nenv][nu] device action buffer, and a fill of it with actions
  * drawn uniformly within each actuator's ctrlrange (the random agent of

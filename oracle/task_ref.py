@@ -86,3 +86,16 @@ def shaped_reorientation_reward(distance: float, ctrl) -> dict:
 def reorient_reward(distance: float, ctrl) -> float:
     """reorient.py:215-220."""
     return weighted_average(shaped_reorientation_reward(distance, ctrl).values())
+
+
+def fingertip_distances(goal, tips):
+    """FingertipCartesianPosition.goal_distance (fingertip_position.py:127-137)."""
+    return np.linalg.norm(np.asarray(goal, float).reshape(-1, 3) - np.asarray(tips, float).reshape(-1, 3), axis=1)
+
+
+def reach_reward(goal, tips, dense: bool = True, threshold: float = 0.01) -> float:
+    """Reach.get_reward (reach.py:196-210)."""
+    d = fingertip_distances(goal, tips)
+    if dense:
+        return float(np.mean(np.where(d <= threshold, 0.0, [-tanh_squared(x, margin=0.1) for x in d])))
+    return float(np.mean(np.where(d <= threshold, 0.0, -1.0)))

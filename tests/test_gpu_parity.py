@@ -320,3 +320,75 @@ def test_full_batch_properties(gpu):
     ncon = env.physics.get(_lib.NCON)[:, 0]
     assert (ncon > 0).mean() > 0.5
     env.close()
+
+
+def _check_reach_rewards(env, ts, dense):
+    from oracle import task_ref
+
+    obs = ts.observation
+    hand = env.task.hand_name
+    for e in range(env.num_envs):
+        if ts.step_type[e] == 0:
+            assert ts.reward[e] == 0 and ts.discount[e] == 1
+            continue
+        r = task_ref.reach_reward(obs["goal_state"][e], obs[f"{hand}/fingertip_positions"][e], dense=dense)
+        assert ts.reward[e] == pytest.approx(r, rel=1e-4, abs=1e-5)
+        assert ts.discount[e] in (0.0, 1.0)
+
+
+@pytest.mark.parametrize("task", ["state_dense", "state_sparse"])
+def test_reach_adroit_env(gpu, task):
+    """Reach (reference task, Adroit hand): rewards equal the fp64 restatement of
+    reach.py:196-210 on the step's own observation; episodes start inside half the
+    joint range (reach.py:34, dexterous_hand.py:120-142) after the goal rollouts
+    advanced time by two physics steps (fingertip_position.py:93-111)."""
+    from dexterity_amd import manipulation
+
+    n = 64
+    env = manipulation.load("reach", task, seed=3, num_envs=n)
+    ts = env.reset()
+    assert np.all(ts.first())
+    lo, hi = env.task.joint_range.T
+    q = env.physics.qpos
+    assert np.all(q >= 0.5 * lo - 1e-6) and np.all(q <= 0.5 * hi + 1e-6)
+    t = env.physics.get(_lib.TIME)[:, 0]
+    np.testing.assert_allclose(t, 0.04, atol=1e-6)
+    goals = env.goals()
+    assert goals.shape == (n, 15) and np.all(np.isfinite(goals))
+    tips0 = ts.observation[f"{env.task.hand_name}/fingertip_positions"]
+    d0 = np.linalg.norm((goals - tips0).reshape(n, 5, 3), axis=2)
+    assert np.all(d0 < 0.25) and d0.mean() > 1e-3  # reachable, not the start pose
+    assert len({tuple(np.round(g, 5)) for g in goals}) == n  # per-env draws
+    spec = env.action_spec()
+    rng = np.random.RandomState(12345)
+    for step in range(12):
+        action = rng.uniform(spec.minimum, spec.maximum, size=(n, spec.shape[0])).astype(np.float32)
+        ts = env.step(action)
+        _check_reach_rewards(env, ts, dense=task == "state_dense")
+        for k, v in ts.observation.items():
+            assert np.all(np.isfinite(v)), k
+    assert env.goal_failures().sum() == 0
+    for name, spec_ in env.observation_spec().items():
+        assert ts.observation[name].shape[1:] == spec_.shape
+    assert env.obs_dim == 117
+    env.close()
+
+
+def test_reach_shadow_config2(gpu):
+    """BASELINE config 2: reach with the Shadow hand, contact-free, 1024 envs.
+    Coupled joints equal after the initial sampling (shadow_hand_e.py:124-129);
+    rewards match the restatement; 30 control steps stay finite."""
+    from dexterity_amd import hands, manipulation
+
+    n = 1024
+    env = manipulation.load("reach_shadow", "state_dense", seed=11, num_envs=n)
+    env.reset()
+    q = env.physics.qpos
+    for ids in hands.COUPLED_JOINT_IDS:
+        np.testing.assert_array_equal(q[:, ids[0]], q[:, ids[-1]])
+    for step in range(30):
+        env.step(env.sample_actions(step), device_action=True)
+    ts = env.timestep()
+    _check_reach_rewards(env, ts, dense=True)
+    assert np.all(np.isfinite(env.physics.qpos))
+    env.close()
