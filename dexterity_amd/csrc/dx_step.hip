@@ -2232,7 +2232,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     return;
   }
   float scale = 1.0f / (m.meaninertia * (float)max(1, nv));
-  float tol = fmaxf(m.tolerance, 1e-6f);
+  float tol = fmaxf(m.tolerance, 1e-9f);
   // warm start vs smooth
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
@@ -2286,7 +2286,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     // Converged when (a) the full Newton step kept every row in its cost zone: the
     // cost is quadratic on that zone set, so the step landed on its exact minimiser;
     // or (b) the improvement is below the tolerance or at fp32 noise level of the cost.
-    if ((changed == 0 && fabsf(alpha - 1.0f) < 1e-3f) || impr < tol || (prev - nc) <= 2e-6f * fabsf(prev)) {
+    if ((changed == 0 && fabsf(alpha - 1.0f) < 1e-3f) || impr < tol || (prev - nc) <= 1e-9f * fabsf(prev)) {
       it++;
       break;
     }

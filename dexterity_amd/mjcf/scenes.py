@@ -14,6 +14,10 @@ compiled blobs under `assets/` are what the runtime (and the GPU box) loads.
   collisions disabled (`reach.py:131-132`), dt 0.02.
 * `shadow_reach`     -- BASELINE.json config 2 naming (reach with the Shadow hand,
   contact-free smooth dynamics), dt 0.02.
+* `bimanual_handover` -- BASELINE.json config 5 (synthetic; the reference has no
+  bimanual task): two Shadow hands welded to the world palm-up side by side at the
+  Juggle task's x offsets (`juggle.py:22-26`, +-0.1 m, here +-0.12 m so the palms do not
+  overlap), the reorient cube on the left palm, dt 0.005 as reorient.  nq 55 / nv 54.
 """
 
 from __future__ import annotations
@@ -76,8 +80,27 @@ def adroit_reach():
     return scene.compile()
 
 
+BIMANUAL_OFFSET = 0.12
+
+
+def bimanual_handover():
+    scene = Scene(timestep=0.005)
+    _ground(scene, collide=True)
+    for side, dx in (("left", BIMANUAL_OFFSET), ("right", -BIMANUAL_OFFSET)):
+        prefix = f"shadow_hand_{side}/"
+        pos = (PALM_UPRIGHT_POS[0] + dx, PALM_UPRIGHT_POS[1], PALM_UPRIGHT_POS[2])
+        scene.attach_mjcf(SHADOW_XML, prefix, pos, PALM_UPRIGHT_QUAT)
+        for tip in SHADOW_FINGERTIPS:
+            scene.add_site(prefix + tip, prefix + tip + "_site")
+    centre = [(a + b) / 2 for a, b in zip(PROP_BBOX_LOWER, PROP_BBOX_UPPER)]
+    centre[0] += BIMANUAL_OFFSET
+    scene.add_free_box("prop", 0.02, centre)
+    return scene.compile()
+
+
 SCENES = {
     "shadow_reorient": shadow_reorient,
     "shadow_reach": shadow_reach,
     "adroit_reach": adroit_reach,
+    "bimanual_handover": bimanual_handover,
 }

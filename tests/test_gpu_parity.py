@@ -392,3 +392,95 @@ def test_reach_shadow_config2(gpu):
     _check_reach_rewards(env, ts, dense=True)
     assert np.all(np.isfinite(env.physics.qpos))
     env.close()
+
+
+@pytest.fixture(scope="module")
+def bimanual_setup(gpu, oracle_mod):
+    """BASELINE config 5 scene: two Shadow hands (nv 54, the n > 32 Cholesky path)."""
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "bimanual_handover.npz"))
+    xfrc = gpu.gravity_compensation(cm, "shadow_hand_")
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    rng = np.random.RandomState(5)
+    lo, hi = cm.actuator_ctrlrange.T
+    states = []
+    for t in range(3):
+        d = oracle_mod.OracleData(om)
+        d.xfrc_applied[:] = xfrc.ravel()
+        d.qpos[48:51] += rng.uniform(-0.02, 0.02, size=3) * [1, 1, 0]
+        ctrl = rng.uniform(lo, hi) * 0.3
+        for s in range(100):
+            d.ctrl[:] = ctrl
+            d.step()
+            if s in (40, 99):
+                states.append((d.qpos.copy(), d.qvel.copy(), d.qacc_warmstart.copy(), ctrl.copy()))
+    model = gpu.Model(cm)
+    return cm, xfrc, om, states, model
+
+
+def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
+    """Mass matrix, smooth and constrained accelerations and the contact set of the
+    two-hand scene match the fp64 oracle.  Tolerances as the reorient test, except the
+    cube's own dofs: its contact points may differ by up to 2e-4 m (where fp32 and
+    fp64 MPR stop refining the portal), which on a 2 cm cube is a ~1 % lever-arm
+    change of its angular acceleration, so those six dofs get 3e-3 of the scale."""
+    cm, xfrc, om, states, model = bimanual_setup
+    phys = _load_states(gpu, model, xfrc, states)
+    phys.debug(True)
+    phys.forward()
+    phys.sync()
+    M = phys.debug_get("M")
+    a0 = phys.debug_get("qacc_smooth")
+    con = phys.debug_get("contact")
+    cnt = phys.debug_get("efc_count")
+    qacc = phys.qacc
+    with_contacts = 0
+    for e, st in enumerate(states):
+        d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        Mo = d.M.reshape(cm.nv, cm.nv)
+        assert np.abs(M[e] - Mo).max() <= 1e-5 * np.abs(Mo).max()
+        scale = np.abs(d.qacc_smooth).max()
+        assert np.abs(a0[e] - d.qacc_smooth).max() <= 1e-5 * scale
+        oc = d.contacts()
+        gc = con[e, : (con[e, :, 13] != 0).sum()]
+        assert cnt[e, 1] == 0, "overflow flag set"
+        assert {(int(r[13]), int(r[14])) for r in gc} == {(int(r[13]), int(r[14])) for r in oc}
+        with_contacts += len(oc) > 0
+        tie = False
+        ok = {(int(r[13]), int(r[14])): r for r in oc}
+        for r in gc:
+            o = ok[(int(r[13]), int(r[14]))]
+            assert abs(r[12] - o[12]) < 2e-5
+            tie = tie or np.abs(r[0:3] - o[0:3]).max() >= 2e-4
+        if not tie:
+            err = np.abs(qacc[e] - d.qacc)
+            assert err[:48].max() <= 5e-4 * max(1.0, scale), f"env {e}"
+            assert err[48:].max() <= 3e-3 * max(1.0, scale), f"env {e}"
+    assert with_contacts >= 3
+
+
+def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
+    """One substep vs the oracle (qpos 1e-6), then BASELINE config 5 at full size:
+    4096 envs x 20 control steps of random actions stay finite and in contact."""
+    cm, xfrc, om, states, model = bimanual_setup
+    phys = _load_states(gpu, model, xfrc, states)
+    phys.step(1)
+    qpos = phys.qpos
+    for e, st in enumerate(states):
+        d = oracle_mod.OracleData(om)
+        d.xfrc_applied[:] = xfrc.ravel()
+        d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = st
+        d.step()
+        assert np.abs(qpos[e] - d.qpos).max() < 1e-5
+    n = 4096
+    big = gpu.BatchedPhysics(model, n)
+    big.set_xfrc(xfrc)
+    q0 = np.tile(cm.qpos0, (n, 1))
+    q0[:, 48:51] += np.random.RandomState(0).uniform(-0.02, 0.02, size=(n, 3)) * [1, 1, 0]
+    big.set(_lib.QPOS, q0)
+    lo, hi = cm.actuator_ctrlrange.T
+    rng = np.random.RandomState(1)
+    for step in range(20):
+        big.set(_lib.CTRL, rng.uniform(lo, hi, size=(n, cm.nu)).astype(np.float32))
+        big.step(5)
+    assert np.all(np.isfinite(big.qpos)) and np.all(np.isfinite(big.qvel))
+    assert (big.get(_lib.NCON)[:, 0] > 0).mean() > 0.5
