@@ -514,15 +514,18 @@ __device__ __forceinline__ void wave_chol_solve(const float* A, float* x, int n)
   SYNC();
 }
 
-// Register Cholesky solve for n <= 32: lane i holds row i of A in r[0..31].
-// Right-looking like wave_cholesky (same per-element update order); the column
-// broadcast is a v_readlane instead of an LDS round trip + barrier.  No per-lane
-// predicates in the hot loops (they made the compiler keep 32 exec masks live):
-// rows are loaded unconditionally (entries above the diagonal, and the rows of
-// lanes >= n, hold garbage that never reaches rows < n because every broadcast
-// reads a lane < n), the diagonal lives in dinv (set with v_writelane), and the
-// substitutions deposit results with v_writelane.  The back substitution needs
-// columns of L: one LDS transpose through T (packed, may alias A).
+// Cholesky solve for n <= 32 on the matrix cores.  The matrix, padded to 32 x 32 with
+// an identity block, lives in the 16 accumulator VGPRs of v_mfma_f32_32x32x2_f32
+// (lane l, VGPR v holds C[8 (v/4) + 4 (l/32) + v%4][l%32]; probe:
+// tools/probes/mfma_layout.hip).  Right-looking, two columns per step: rows k, k+1
+// are one VGPR pair in one half-wave, broadcast to both halves by v_permlane32_swap
+// (symmetry makes them the columns); the 2 x 2 diagonal block is factored from
+// three readlanes; the panel (L[:,k], L[:,k+1]) is the 32 x 2 A operand and its
+// transpose the B operand of ONE MFMA that applies the rank-2 update to the whole
+// trailing matrix.  16 steps instead of 32 columns of ~31 readlanes each.  The
+// substitutions then run on lane rows of L (lane i holds L[i][k] in Lr[k]) with
+// readlane/writelane; the backward one reads L's columns after an LDS transpose
+// through T (packed, may alias A).
 // A (+ hs*dadd on the diagonal, if dadd) -> x = A^-1 x.
 __device__ __forceinline__ float rl(float v, int k) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
@@ -532,61 +535,75 @@ extern "C" __device__ int dx_writelane_i32(int val, int lane, int old) __asm("ll
 __device__ __forceinline__ float wl(float v, float s, int k) {  // v with lane k := s
   return __int_as_float(dx_writelane_i32(__float_as_int(s), k, __float_as_int(v)));
 }
-__device__ __forceinline__ void reg_chol_solve32(const float* A, int n, const DXG float* dadd, float hs,
-                                                 float* x, float* T) {
-  // All 32 steps run regardless of n (no n-dependent branches: the compiler would
-  // hoist 32 loop-invariant masks out of the Newton loop and spill them).  Lanes
-  // and columns >= n only ever see finite LDS words (the kernel zeroes its LDS
-  // block at entry) and multiply into zeros.
-  constexpr int NB = 32;
-  const int i = LANE;
-  const float* Ai = A + ti(min(i, n - 1));
-  float r[NB];
+typedef float dx_f16v __attribute__((ext_vector_type(16)));
+// v with its lower (up = false) or upper (up = true) half-wave copied into both halves
+__device__ __forceinline__ float half_dup(float v, bool up) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(up ? r[1] : r[0]);
+}
+__device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const DXG float* dadd, float hs,
+                                                  float* x, float* T) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  dx_f16v C;
 #pragma unroll
-  for (int k = 0; k < NB; k++) r[k] = Ai[k];
-  float add = (dadd && i < n) ? hs * dadd[i] : 0.f;
-  float b = i < n ? x[i] : 0.f;
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    const int ra = max(i, j), rb = min(i, j);
+    const bool in = i < n && j < n;
+    float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
+    if (dadd && i == j && in) e += hs * dadd[i];
+    C[v] = e;
+  }
+  float b = l < n ? x[l] : 0.f;
   SYNC();  // A may alias T
+  float Lr[32];  // lane j: L[j][k], strictly below the diagonal
   float dinv = 0.f;
 #pragma unroll
-  for (int k = 0; k < NB; k++) {
-    float inv = __builtin_amdgcn_rsqf(fmaxf(rl(r[k], k) + rl(add, k), 1e-30f));
-    dinv = wl(dinv, inv, k);
-    float lik = r[k] * inv;
-    r[k] = lik;
-#pragma unroll
-    for (int j = k + 1; j < NB; j++) r[j] = fmaf(-lik, rl(lik, j), r[j]);
+  for (int k = 0; k < 32; k += 2) {
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // C[k][j], C[k+1][j]
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
+    const float l21 = rl(rk1, k) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    dinv = wl(dinv, i11, k);
+    dinv = wl(dinv, i22, k + 1);
+    const float lk = rk * i11;                  // L[j][k]   (j > k)
+    const float lk1 = (rk1 - lk * l21) * i22;   // L[j][k+1] (j > k + 1)
+    Lr[k] = j > k ? lk : 0.f;
+    Lr[k + 1] = j > k + 1 ? lk1 : 0.f;
+    const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;  // panel: A[j][hi], B[hi][j]
+    C = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C, 0, 0, 0);
   }
-  // strictly-lower row -> T (packed), and zero the rest of r
+  // strictly-lower row -> T (packed)
+  const int i = l;
 #pragma unroll
-  for (int k = 0; k < NB; k++) {
-    bool low = k < i && i < n;
-    r[k] = low ? r[k] : 0.f;
-    if (low) T[ti(i) + k] = r[k];
-  }
+  for (int k = 0; k < 32; k++)
+    if (k < i && i < n) T[ti(i) + k] = Lr[k];
   // forward: L y = b
   float y = 0.f;
 #pragma unroll
-  for (int k = 0; k < NB; k++) {
+  for (int k = 0; k < 32; k++) {
     float yk = rl(b, k) * rl(dinv, k);
     y = wl(y, yk, k);
-    b = fmaf(-r[k], yk, b);
+    b = fmaf(-Lr[k], yk, b);
   }
   SYNC();
-  // column i of L (below the diagonal) -> r; rows >= n of T are never written
+  // column i of L (below the diagonal) -> Lr; rows >= n of T are never written
   const int ic = min(i, n - 1);
 #pragma unroll
-  for (int k = 0; k < NB; k++) {
+  for (int k = 0; k < 32; k++) {
     float v = T[ti(k) + ic];
-    r[k] = ic < k ? v : 0.f;
+    Lr[k] = ic < k && k < n ? v : 0.f;
   }
-  // backward: L^T x = y  (y is 0 on lanes >= n, so steps k >= n add 0 * finite)
+  // backward: L^T x = y
   float xo = 0.f;
 #pragma unroll
-  for (int k = NB - 1; k >= 0; k--) {
+  for (int k = 31; k >= 0; k--) {
     float xk = rl(y, k) * rl(dinv, k);
     xo = wl(xo, xk, k);
-    y = fmaf(-r[k], xk, y);
+    y = fmaf(-Lr[k], xk, y);
   }
   if (i < n) x[i] = xo;
   SYNC();
@@ -2267,7 +2284,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
     SYNC();
     if (nv <= 32) {
-      reg_chol_solve32(H, nv, nullptr, 0.f, dir, H);
+      mfma_chol_solve32(H, nv, nullptr, 0.f, dir, H);
     } else {
       wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
       wave_chol_solve(H, dir, nv);
@@ -2325,7 +2342,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
   if (nv <= 32) {
     SYNC();
-    reg_chol_solve32(M, nv, nullptr, 0.f, a0, H);
+    mfma_chol_solve32(M, nv, nullptr, 0.f, a0, H);
   } else {
     for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
     SYNC();
@@ -2363,7 +2380,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
     if (nv <= 32) {
       SYNC();
-      reg_chol_solve32(M, nv, m.dof_damping, h, acc, H);
+      mfma_chol_solve32(M, nv, m.dof_damping, h, acc, H);
     } else {
       for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
       SYNC();
@@ -2593,7 +2610,7 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   const Lds& L = c.L;
   int* I = (int*)(smem + L.ints);
   c.I = I;
-  // Zero the whole per-env LDS block once: reg_chol_solve32 reads a few words past
+  // Zero the whole per-env LDS block once: the Cholesky solve reads a few words past
   // its packed triangles (padding lanes/columns, multiplied by exact zeros), and
   // those must be finite rather than whatever an earlier workgroup left behind.
 #ifndef DX_SKIP_LDS_ZERO  // (defined only by the test that shows why this is needed)
