@@ -364,6 +364,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     }
     m->hf["gpair_rec"] = prec;
   }
+
   // geom bounding spheres with centres in the body frame (mid-phase cull)
   {
     std::vector<float> gb(4 * std::max(d.ngeom, 1), 0.f);
@@ -390,6 +391,48 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
       for (int k = 0; k < 3; k++) ob[15 * g + 12 + k] = a[3 + k];
     }
     m->hf["geom_obb_b"] = ob;
+  }
+  // collision culling records: per geom {type, body}{bsphere (body frame)}{obb centre,
+  // R (body <- box), half extents; planes: point, normal} and per body pair {b1, b2,
+  // first geom pair, count}{sphere 1}{sphere 2}{margin, plane geom, plane body}{plane
+  // point}{plane normal} (body frames) -- one memory round trip per culling item
+  {
+    auto& gt = m->hi["geom_type"]; auto& gb = m->hi["geom_bodyid"];
+    auto& gbs = m->hf["geom_bsphere_b"]; auto& gob = m->hf["geom_obb_b"];
+    auto& gp = m->hf["geom_pos"]; auto& gm = m->hf["geom_mat"];
+    int ng = (int)gt.size();
+    std::vector<float> cr(24 * std::max(ng, 1), 0.f);
+    for (int g = 0; g < ng; g++) {
+      float* r = cr.data() + 24 * g;
+      int iv[2] = {gt[g], gb[g]};
+      memcpy(r, iv, 8);
+      for (int k = 0; k < 4; k++) r[4 + k] = gbs[4 * g + k];
+      if (gt[g] == DXG_PLANE) {
+        for (int k = 0; k < 3; k++) { r[8 + k] = gp[3 * g + k]; r[20 + k] = gm[9 * g + 3 * k + 2]; }
+      } else {
+        for (int k = 0; k < 3; k++) r[8 + k] = gob[15 * g + k];
+        for (int k = 0; k < 9; k++) r[11 + k] = gob[15 * g + 3 + k];
+        for (int k = 0; k < 3; k++) r[20 + k] = gob[15 * g + 12 + k];
+      }
+    }
+    m->hf["geom_crec"] = cr;
+    auto& bb = m->hi["bpair_body"]; auto& ba = m->hi["bpair_adr"]; auto& bnum = m->hi["bpair_num"];
+    auto& bpl = m->hi["bpair_plane"]; auto& bs = m->hf["bpair_sphere"]; auto& pm = m->hf["gpair_margin"];
+    int nbp = (int)bnum.size();
+    std::vector<float> br(24 * std::max(nbp, 1), 0.f);
+    for (int k = 0; k < nbp; k++) {
+      float* r = br.data() + 24 * k;
+      int iv[4] = {bb[2 * k], bb[2 * k + 1], ba[k], bnum[k]};
+      memcpy(r, iv, 16);
+      for (int e = 0; e < 8; e++) r[4 + e] = bs[8 * k + e];
+      r[12] = pm[ba[k]];
+      int pg = bpl[k], pb = pg >= 0 ? gb[pg] : 0;
+      memcpy(r + 13, &pg, 4);
+      memcpy(r + 14, &pb, 4);
+      if (pg >= 0)
+        for (int e = 0; e < 3; e++) { r[16 + e] = gp[3 * pg + e]; r[20 + e] = gm[9 * pg + 3 * e + 2]; }
+    }
+    m->hf["bpair_rec"] = br;
   }
   // friction rows / limited joints / limited tendons
   std::vector<int> fric_dof, dof_fricrow(nv, -1), limj, limt;
@@ -634,7 +677,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere); UF(geom_bsphere_b); UF(geom_obb_b);
   UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert4);
   UI(mesh_binn); UI(mesh_bincap); UI(mesh_binadr); UF(mesh_bin4);
-  UF(geom_rec); UF(gpair_rec);
+  UF(geom_rec); UF(gpair_rec); UF(geom_crec); UF(bpair_rec);
   UI(site_bodyid); UF(site_pos); UF(site_mat);
   UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
   UF(tendon_range); UF(tendon_margin); UF(tendon_solref); UF(tendon_solimp); UF(tendon_invweight0);

@@ -59,6 +59,8 @@ struct DevModel {
   // bin_cap, vert4 offset, bin4 offset, -}{size, -}{pos, -}{mat 9, center 3, -};
   // gpair_rec [ngpair] = {g1, g2, margin, primitive-pair flag}
   const DXG float4 *geom_rec, *gpair_rec;
+  // culling records (dx_api.hip): geom_crec [ngeom][6], bpair_rec [nbpair][6] float4
+  const DXG float4 *geom_crec, *bpair_rec;
   // sites
   const DXG int* site_bodyid;
   const DXG float *site_pos, *site_mat;

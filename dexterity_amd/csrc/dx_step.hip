@@ -1324,39 +1324,45 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   for (int base = 0; base < c.nbpair; base += DX_WAVE) {
     int bp = base + LANE;
     bool keep = false;
-    int cnt = 0;
+    int cnt = 0, adr = 0;
     if (bp < c.nbpair) {
-      int b1 = m.bpair_body[2 * bp], b2 = m.bpair_body[2 * bp + 1];
+      const DXG float4* R = m.bpair_rec + 6 * bp;
+      float4 r0 = R[0], s1 = R[1], s2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5];
+      int b1 = __float_as_int(r0.x), b2 = __float_as_int(r0.y);
+      adr = __float_as_int(r0.z);
       keep = true;
       if (watch_only) keep = (b2 == wb || b1 == wb) && (m.geom_bodyid[wg] == b1 || m.geom_bodyid[wg] == b2);
-      const float* s1 = m.bpair_sphere + 8 * bp;
-      const float* s2 = s1 + 4;
-      float mg = m.gpair_margin[m.bpair_adr[bp]];
-      if (keep && s2[3] >= 0) {
+      float mg = r3.x;
+      int pg = __float_as_int(r3.y);
+      if (keep && s2.w >= 0) {
         float c2[3];
-        matvec3(c2, xmat + 9 * b2, s2);
+        const float s2v[3] = {s2.x, s2.y, s2.z};
+        matvec3(c2, xmat + 9 * b2, s2v);
         for (int k = 0; k < 3; k++) c2[k] += xpos[3 * b2 + k];
-        int pg = m.bpair_plane[bp];
         if (pg >= 0) {
-          float pp[3], pm[9];
-          geom_pose(c, pg, pp, pm);
-          float r[3] = {c2[0] - pp[0], c2[1] - pp[1], c2[2] - pp[2]};
-          keep = r[0] * pm[2] + r[1] * pm[5] + r[2] * pm[8] <= s2[3] + mg;
-        } else if (s1[3] >= 0) {
+          int pb = __float_as_int(r3.z);
+          const float pl[3] = {r4.x, r4.y, r4.z}, nl[3] = {r5.x, r5.y, r5.z};
+          float pp[3], n[3];
+          matvec3(pp, xmat + 9 * pb, pl);
+          matvec3(n, xmat + 9 * pb, nl);
+          float rr[3] = {c2[0] - pp[0] - xpos[3 * pb], c2[1] - pp[1] - xpos[3 * pb + 1], c2[2] - pp[2] - xpos[3 * pb + 2]};
+          keep = dot3(rr, n) <= s2.w + mg;
+        } else if (s1.w >= 0) {
           float c1[3];
-          matvec3(c1, xmat + 9 * b1, s1);
+          const float s1v[3] = {s1.x, s1.y, s1.z};
+          matvec3(c1, xmat + 9 * b1, s1v);
           for (int k = 0; k < 3; k++) c1[k] += xpos[3 * b1 + k];
-          keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
+          keep = sphere_overlap(c1, s1.w, c2, s2.w, mg);
         }
       }
-      cnt = keep ? m.bpair_num[bp] : 0;
+      cnt = keep ? __float_as_int(r0.w) : 0;
     }
     uint64_t mask = __ballot(keep);
     int pos = __popcll(mask & ((1ull << LANE) - 1ull));
     int inc = wave_incl_scan(cnt);
     int off = inc - cnt;
     if (keep && nbc + pos < half) {
-      cand[nbc + pos] = bp;
+      cand[nbc + pos] = adr;  // first geom pair of the body pair
       pref[nbc + pos] = ngp + off;
     }
     nbc += __popcll(mask);
@@ -1381,32 +1387,39 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
         int mid = (lo + hi) >> 1;
         if (pref[mid] <= t) lo = mid; else hi = mid;
       }
-      gp = m.bpair_adr[cand[lo]] + (t - pref[lo]);
-      int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+      gp = cand[lo] + (t - pref[lo]);
+      float4 pr = m.gpair_rec[gp];
+      int g1 = __float_as_int(pr.x), g2 = __float_as_int(pr.y);
       keep = !watch_only || g1 == wg || g2 == wg;
       if (keep) {
-        float mg = m.gpair_margin[gp];
-        int b2 = m.geom_bodyid[g2];
-        const float* s2 = m.geom_bsphere_b + 4 * g2;
+        float mg = pr.z;
+        const DXG float4* G1 = m.geom_crec + 6 * g1;
+        const DXG float4* G2 = m.geom_crec + 6 * g2;
+        float4 a0 = G1[0], a1 = G1[1], a2 = G1[2], a3 = G1[3], a4 = G1[4], a5 = G1[5];
+        float4 e0 = G2[0], e1 = G2[1], e2 = G2[2], e3 = G2[3], e4 = G2[4], e5 = G2[5];
+        int b1 = __float_as_int(a0.y), b2 = __float_as_int(e0.y);
         float c2[3];
+        const float s2[3] = {e1.x, e1.y, e1.z};
         matvec3(c2, xmat + 9 * b2, s2);
         for (int k = 0; k < 3; k++) c2[k] += xpos[3 * b2 + k];
-        int b1 = m.geom_bodyid[g1];
-        if (m.geom_type[g1] == DXG_PLANE) {
-          float p1[3], m1[9];
-          geom_pose(c, g1, p1, m1);
-          float n[3] = {m1[2], m1[5], m1[8]}, r[3];
-          sub3(r, c2, p1);
-          keep = dot3(r, n) <= s2[3] + mg;
+        if (__float_as_int(a0.x) == DXG_PLANE) {
+          const float pl[3] = {a2.x, a2.y, a2.z}, nl[3] = {a5.x, a5.y, a5.z};
+          float p1[3], n[3], r[3];
+          matvec3(p1, xmat + 9 * b1, pl);
+          matvec3(n, xmat + 9 * b1, nl);
+          for (int k = 0; k < 3; k++) r[k] = c2[k] - p1[k] - xpos[3 * b1 + k];
+          keep = dot3(r, n) <= e1.w + mg;
         } else {
-          const float* s1 = m.geom_bsphere_b + 4 * g1;
+          const float s1[3] = {a1.x, a1.y, a1.z};
           float c1[3];
           matvec3(c1, xmat + 9 * b1, s1);
           for (int k = 0; k < 3; k++) c1[k] += xpos[3 * b1 + k];
-          keep = sphere_overlap(c1, s1[3], c2, s2[3], mg);
-          if (keep)
-            keep = obb_overlap(m.geom_obb_b + 15 * g1, xpos + 3 * b1, xmat + 9 * b1, m.geom_obb_b + 15 * g2,
-                               xpos + 3 * b2, xmat + 9 * b2, mg);
+          keep = sphere_overlap(c1, a1.w, c2, e1.w, mg);
+          if (keep) {
+            const float o1[15] = {a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w, a4.x, a4.y, a4.z, a4.w, a5.x, a5.y, a5.z};
+            const float o2[15] = {e2.x, e2.y, e2.z, e2.w, e3.x, e3.y, e3.z, e3.w, e4.x, e4.y, e4.z, e4.w, e5.x, e5.y, e5.z};
+            keep = obb_overlap(o1, xpos + 3 * b1, xmat + 9 * b1, o2, xpos + 3 * b2, xmat + 9 * b2, mg);
+          }
         }
       }
     }
@@ -1945,6 +1958,25 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
   SYNC();
 }
 
+// sum of the constraint rows' costs at residuals jr (+ g0, the Gauss term)
+template <class Ctx>
+__device__ __forceinline__ float rows_cost(const Ctx& c, const float* jr, float g0) {
+  const DevModel& m = c.m;
+  int nefc = c.I[I_NEFC];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  float g = g0;
+  for (int r = LANE; r < nefc; r += DX_WAVE) {
+    float f, hw;
+    bool fr = r < c.nfric;
+    g += row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jr[r], f, hw);
+  }
+  (void)m;
+  return wave_sum(g);
+}
+
 // cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
 template <class Ctx>
 __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
@@ -2134,9 +2166,15 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
       }
     }
     if (W[0] == 0 && W[4] == 0 && W[8] == 0) continue;
-    for (int t = LANE; t < nnz * nnz; t += DX_WAVE) {
-      int a = t / nnz, b = t % nnz;
-      if (b > a) continue;  // cj_idx ascending: lower triangle only
+    // lower triangle of the contact's nnz x nnz block, item t -> (a >= b); cj_idx is
+    // ascending, so (idx_a, idx_b) is in H's lower triangle.  The entries of one
+    // contact are distinct; SYNC (a compiler barrier) orders consecutive contacts.
+    const int items = nnz * (nnz + 1) / 2;
+    for (int t = LANE; t < items; t += DX_WAVE) {
+      int a = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+      a += (a + 1) * (a + 2) / 2 <= t;
+      a -= a * (a + 1) / 2 > t;
+      int b = t - a * (a + 1) / 2;
       float ja[3], jb[3];
       for (int k = 0; k < 3; k++) {
         ja[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + a];
@@ -2250,18 +2288,24 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   }
   float scale = 1.0f / (m.meaninertia * (float)max(1, nv));
   float tol = fmaxf(m.tolerance, 1e-9f);
-  // warm start vs smooth
+  // warm start vs smooth.  M qacc_smooth = qfrc_smooth, so the smooth candidate needs
+  // no M product and has a zero Gauss term: only J qacc_smooth (into efc_jv).
+  float* jar = c.f(c.L.efc_jar);
+  float* jvs = c.f(c.L.efc_jv);
+  const float* aref = c.f(c.L.efc_aref);
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
   float cw = eval_cost(c, qacc, Ma);
-  for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i];
+  jac_vec(c, a0, jvs);
+  for (int r = LANE; r < nefc; r += DX_WAVE) jvs[r] -= aref[r];
   SYNC();
-  float cs = eval_cost(c, qacc, Ma);
-  float cost = cs;
-  if (cw < cs) {
-    for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
+  float cs = rows_cost(c, jvs, 0.f);
+  float cost = cw;
+  if (!(cw < cs)) {
+    for (int i = LANE; i < nv; i += DX_WAVE) { qacc[i] = a0[i]; Ma[i] = qs[i]; }
+    for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] = jvs[r];
     SYNC();
-    cost = eval_cost(c, qacc, Ma);
+    cost = cs;
   }
   int it = 0;
   stage_mark(c, ST_NEWTON_EVAL);
@@ -2293,9 +2337,17 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     int changed = 0;
     float alpha = line_search(c, qacc, Ma, dir, &changed);
     stage_mark(c, ST_NEWTON_LS);
-    for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] += alpha * dir[i];
+    // qacc += alpha dir; M qacc and J qacc - aref follow by linearity from the line
+    // search's M dir (v4) and J dir (efc_jv): no products recomputed
+    const float* Mdir = c.f(c.L.v4);
+    const float* jvd = c.f(c.L.efc_jv);
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      qacc[i] += alpha * dir[i];
+      Ma[i] += alpha * Mdir[i];
+    }
+    for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] += alpha * jvd[r];
     SYNC();
-    float nc = eval_cost(c, qacc, Ma);
+    float nc = total_cost(c, qacc, Ma);
     stage_mark(c, ST_NEWTON_EVAL);
     float impr = scale * (cost - nc);
     float prev = cost;
