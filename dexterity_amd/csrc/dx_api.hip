@@ -434,6 +434,59 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     }
     m->hf["bpair_rec"] = br;
   }
+  // tree records: per body (lane = body in the level loops) and per dof, so a stage
+  // loads its model data in one memory round trip instead of a chain per tree level
+  if (nb > 64) {
+    fail(DX_ELIMIT, "nbody must be <= 64 (one lane per body)");
+    delete m;
+    return nullptr;
+  }
+  {
+    auto& bja = m->hi["body_jntadr"]; auto& bjn = m->hi["body_jntnum"];
+    auto& jt = m->hi["jnt_type"]; auto& jqa = m->hi["jnt_qposadr"]; auto& jda = m->hi["jnt_dofadr"];
+    auto& bpos = m->hf["body_pos"]; auto& bquat = m->hf["body_quat"]; auto& bipos = m->hf["body_ipos"];
+    auto& jpos = m->hf["jnt_pos"]; auto& jax = m->hf["jnt_axis"]; auto& q0 = m->hf["qpos0"];
+    auto& bmass = m->hf["body_mass"]; auto& binert = m->hf["body_inertia"];
+    std::vector<float> br(32 * nb, 0.f);
+    for (int b = 0; b < nb; b++) {
+      float* r = br.data() + 32 * b;
+      int ja = bja[b], jn = bjn[b];
+      int iv0[4] = {parent[b], depth[b], ja, jn};
+      memcpy(r, iv0, 16);
+      int jtp = jn > 0 ? jt[ja] : -1, qa = jn > 0 ? jqa[ja] : 0, jd = jn > 0 ? jda[ja] : 0;
+      for (int k = 0; k < 3; k++) { r[4 + k] = bpos[3 * b + k]; r[12 + k] = bipos[3 * b + k]; }
+      memcpy(r + 7, &jtp, 4);
+      for (int k = 0; k < 4; k++) r[8 + k] = bquat[4 * b + k];
+      memcpy(r + 15, &rootidx[b], 4);
+      if (jn > 0)
+        for (int k = 0; k < 3; k++) { r[16 + k] = jpos[3 * ja + k]; r[20 + k] = jax[3 * ja + k]; }
+      memcpy(r + 19, &qa, 4);
+      r[23] = jn > 0 ? q0[qa] : 0.f;
+      int iv6[2] = {dofadr[b], dofnum[b]};
+      memcpy(r + 24, iv6, 8);
+      r[26] = bmass[b];
+      memcpy(r + 27, &jd, 4);
+      for (int k = 0; k < 3; k++) r[28 + k] = binert[3 * b + k];
+    }
+    m->hf["body_rec"] = br;
+    auto& dbody = m->hi["dof_bodyid"]; auto& djnt = m->hi["dof_jntid"];
+    auto& arm = m->hf["dof_armature"]; auto& dmp = m->hf["dof_damping"];
+    std::vector<float> dr(8 * nv, 0.f);
+    for (int d2 = 0; d2 < nv; d2++) {
+      float* r = dr.data() + 8 * d2;
+      int b = dbody[d2], j = djnt[d2];
+      int tk = jt[j] | ((d2 - jda[j]) << 8);
+      int iv[4] = {b, j, rootidx[b], tk};
+      memcpy(r, iv, 16);
+      r[4] = arm[d2];
+      r[5] = dmp[d2];
+      uint64_t anc = m->body_chain[b] & ((d2 >= 63) ? ~0ull : ((2ull << d2) - 1ull));
+      uint32_t lo = (uint32_t)anc, hi = (uint32_t)(anc >> 32);
+      memcpy(r + 6, &lo, 4);
+      memcpy(r + 7, &hi, 4);
+    }
+    m->hf["dof_rec"] = dr;
+  }
   // friction rows / limited joints / limited tendons
   std::vector<int> fric_dof, dof_fricrow(nv, -1), limj, limt;
   auto& floss = m->hf["dof_frictionloss"];
@@ -677,7 +730,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere); UF(geom_bsphere_b); UF(geom_obb_b);
   UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert4);
   UI(mesh_binn); UI(mesh_bincap); UI(mesh_binadr); UF(mesh_bin4);
-  UF(geom_rec); UF(gpair_rec); UF(geom_crec); UF(bpair_rec);
+  UF(geom_rec); UF(gpair_rec); UF(geom_crec); UF(bpair_rec); UF(body_rec); UF(dof_rec);
   UI(site_bodyid); UF(site_pos); UF(site_mat);
   UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
   UF(tendon_range); UF(tendon_margin); UF(tendon_solref); UF(tendon_solimp); UF(tendon_invweight0);

@@ -61,6 +61,8 @@ struct DevModel {
   const DXG float4 *geom_rec, *gpair_rec;
   // culling records (dx_api.hip): geom_crec [ngeom][6], bpair_rec [nbpair][6] float4
   const DXG float4 *geom_crec, *bpair_rec;
+  // tree records (dx_api.hip): body_rec [nbody][8] float4, dof_rec [nv][2] float4
+  const DXG float4 *body_rec, *dof_rec;
   // sites
   const DXG int* site_bodyid;
   const DXG float *site_pos, *site_mat;

@@ -273,6 +273,39 @@ enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NI
 // ------------------------------------------------------------------------ //
 // position stage
 // ------------------------------------------------------------------------ //
+// Per-body model data of lane b = body (nbody <= 64), loaded in one memory round trip
+// at the start of a tree pass (dx_api.hip body_rec); the level loops then touch only
+// LDS.  Joint fields are the body's first joint (Shadow / Adroit bodies have <= 1).
+struct BodyRec {
+  int parent, depth, ja, jn, jtype, qadr, dofadr, dofnum, jdof, rootidx;
+  float pos[3], quat[4], ipos[3], jpos[3], jaxis[3], q0, mass;
+};
+template <class Ctx>
+__device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
+  const int b = LANE;
+  const bool act = b >= 1 && b < c.nbody;
+  const DXG float4* R = c.m.body_rec + 8 * (act ? b : 0);
+  const float4 a = R[0], p = R[1], q = R[2], i = R[3], jp = R[4], jx = R[5], d = R[6];
+  r.parent = __float_as_int(a.x);
+  r.depth = act ? __float_as_int(a.y) : -1;
+  r.ja = __float_as_int(a.z);
+  r.jn = __float_as_int(a.w);
+  r.pos[0] = p.x; r.pos[1] = p.y; r.pos[2] = p.z;
+  r.jtype = __float_as_int(p.w);
+  r.quat[0] = q.x; r.quat[1] = q.y; r.quat[2] = q.z; r.quat[3] = q.w;
+  r.ipos[0] = i.x; r.ipos[1] = i.y; r.ipos[2] = i.z;
+  r.rootidx = __float_as_int(i.w);
+  r.jpos[0] = jp.x; r.jpos[1] = jp.y; r.jpos[2] = jp.z;
+  r.qadr = __float_as_int(jp.w);
+  r.jaxis[0] = jx.x; r.jaxis[1] = jx.y; r.jaxis[2] = jx.z;
+  r.q0 = jx.w;
+  r.dofadr = __float_as_int(d.x);
+  r.dofnum = __float_as_int(d.y);
+  r.mass = d.z;
+  r.jdof = __float_as_int(d.w);
+  return act;
+}
+
 template <class Ctx>
 __device__ __forceinline__ void kinematics(const Ctx& c) {
   const DevModel& m = c.m;
@@ -283,6 +316,8 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
   float* xipos = c.f(c.L.xipos);
   float* xanchor = c.f(c.L.xanchor);
   float* xaxis = c.f(c.L.xaxis);
+  BodyRec br;
+  const bool act = load_body(c, br);
   if (LANE == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0;
     xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
@@ -290,14 +325,12 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
     xipos[0] = xipos[1] = xipos[2] = 0;
   }
   SYNC();
-  for (int lv = 0; lv < c.nlevel; lv++) {
-    int a0 = m.lvl_adr[lv], a1 = m.lvl_adr[lv + 1];
-    for (int k = a0 + LANE; k < a1; k += DX_WAVE) {
-      int b = m.lvl_body[k];
-      int p = m.body_parent[b], ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+  for (int lv = 1; lv <= c.nlevel; lv++) {
+    if (act && br.depth == lv) {
+      const int b = LANE, p = br.parent, ja = br.ja, jn = br.jn;
       float xp[3], xq[4];
-      if (jn > 0 && m.jnt_type[ja] == DXJ_FREE) {
-        const float* q = qpos + m.jnt_qposadr[ja];
+      if (jn > 0 && br.jtype == DXJ_FREE) {
+        const float* q = qpos + br.qadr;
         xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
         xq[0] = q[3]; xq[1] = q[4]; xq[2] = q[5]; xq[3] = q[6];
         quatnorm(xq);
@@ -305,24 +338,34 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
         xaxis[3 * ja] = 0; xaxis[3 * ja + 1] = 0; xaxis[3 * ja + 2] = 1;
       } else {
         float t[3];
-        matvec3(t, xmat + 9 * p, m.body_pos + 3 * b);
+        matvec3(t, xmat + 9 * p, br.pos);
         xp[0] = xpos[3 * p] + t[0]; xp[1] = xpos[3 * p + 1] + t[1]; xp[2] = xpos[3 * p + 2] + t[2];
-        quatmul(xq, xquat + 4 * p, m.body_quat + 4 * b);
-        for (int j = ja; j < ja + jn; j++) {
+        quatmul(xq, xquat + 4 * p, br.quat);
+        for (int jj = 0; jj < jn; jj++) {
+          const int j = ja + jj;
+          float jp[3], ja3[3], q0;
+          int qa;
+          if (jj == 0) {
+            for (int k = 0; k < 3; k++) { jp[k] = br.jpos[k]; ja3[k] = br.jaxis[k]; }
+            qa = br.qadr;
+            q0 = br.q0;
+          } else {
+            for (int k = 0; k < 3; k++) { jp[k] = m.jnt_pos[3 * j + k]; ja3[k] = m.jnt_axis[3 * j + k]; }
+            qa = m.jnt_qposadr[j];
+            q0 = m.qpos0[qa];
+          }
           float R[9];
           quat2mat(R, xq);
-          const float* jp = m.jnt_pos + 3 * j;
-          const float* ja3 = m.jnt_axis + 3 * j;
           matvec3(t, R, jp);
           float anc[3] = {t[0] + xp[0], t[1] + xp[1], t[2] + xp[2]};
           float ax[3];
           matvec3(ax, R, ja3);
           xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
           xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
-          float ang = qpos[m.jnt_qposadr[j]] - m.qpos0[m.jnt_qposadr[j]];
-          float s, co;
-          sincosf(0.5f * ang, &s, &co);
-          float ql[4] = {co, ja3[0] * s, ja3[1] * s, ja3[2] * s};
+          float ang = qpos[qa] - q0;
+          float sn, co;
+          sincosf(0.5f * ang, &sn, &co);
+          float ql[4] = {co, ja3[0] * sn, ja3[1] * sn, ja3[2] * sn};
           quatmul(xq, xq, ql);
           quatnorm(xq);
           quat2mat(R, xq);
@@ -336,7 +379,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
       for (int e = 0; e < 4; e++) xquat[4 * b + e] = xq[e];
       for (int e = 0; e < 9; e++) xmat[9 * b + e] = R[e];
       float t[3];
-      matvec3(t, R, m.body_ipos + 3 * b);
+      matvec3(t, R, br.ipos);
       for (int e = 0; e < 3; e++) xipos[3 * b + e] = xp[e] + t[e];
     }
     SYNC();
@@ -393,12 +436,13 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   float* xanchor = c.f(c.L.xanchor);
   float* xaxis = c.f(c.L.xaxis);
   for (int d = LANE; d < c.nv; d += DX_WAVE) {
-    int j = m.dof_jntid[d], b = m.dof_bodyid[d];
-    const float* rc = rcom + 3 * m.body_rootidx[b];
+    const float4 dr = m.dof_rec[2 * d];
+    const int b = __float_as_int(dr.x), j = __float_as_int(dr.y), tk = __float_as_int(dr.w);
+    const float* rc = rcom + 3 * __float_as_int(dr.z);
     float off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
     float* cd = cdof + 6 * d;
-    if (m.jnt_type[j] == DXJ_FREE) {
-      int k = d - m.jnt_dofadr[j];
+    if ((tk & 255) == DXJ_FREE) {
+      int k = tk >> 8;
       if (k < 3) {
         for (int e = 0; e < 6; e++) cd[e] = 0;
         cd[3 + k] = 1;
@@ -452,21 +496,25 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
   for (int k = LANE; k < 10 * c.nbody; k += DX_WAVE) crb[k] = cinert[k];
   for (int k = LANE; k < ti(nv); k += DX_WAVE) M[k] = 0;
   SYNC();
-  for (int lv = c.nlevel - 1; lv > 0; lv--) {
-    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
-      int b = m.lvl_body[k], p = m.body_parent[b];
-      if (p > 0)
-        for (int e = 0; e < 10; e++) atomicAdd(crb + 10 * p + e, crb[10 * b + e]);
-    }
+  BodyRec br;
+  const bool act = load_body(c, br);
+  for (int lv = c.nlevel; lv >= 2; lv--) {
+    if (act && br.depth == lv && br.parent > 0)
+      for (int e = 0; e < 10; e++) atomicAdd(crb + 10 * br.parent + e, crb[10 * LANE + e]);
     SYNC();
   }
+  // row i: j over the dof's ancestors (incl. itself), a bit mask from dof_rec
   for (int i = LANE; i < nv; i += DX_WAVE) {
+    const float4 d0 = m.dof_rec[2 * i], d1 = m.dof_rec[2 * i + 1];
     float f[6];
-    mul_inert(f, crb + 10 * m.dof_bodyid[i], cdof + 6 * i);
-    for (int j = i; j >= 0; j = m.dof_parentid[j]) {
-      M[ti(i) + j] = dot6(cdof + 6 * j, f);  // ancestors j < i
+    mul_inert(f, crb + 10 * __float_as_int(d0.x), cdof + 6 * i);
+    uint64_t anc = (uint64_t)(uint32_t)__float_as_int(d1.z) | ((uint64_t)(uint32_t)__float_as_int(d1.w) << 32);
+    while (anc) {
+      int j = __ffsll((long long)anc) - 1;
+      anc &= anc - 1;
+      M[ti(i) + j] = dot6(cdof + 6 * j, f);
     }
-    M[ti(i) + i] += m.dof_armature[i];
+    M[ti(i) + i] += d1.x;
   }
   SYNC();
 }
@@ -1776,15 +1824,21 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
   float* cfrc = cacc + 6 * c.nbody;
   if (LANE < 6) { cvel[LANE] = 0; cacc[LANE] = LANE < 3 ? 0.f : -m.gravity[LANE - 3]; }
   SYNC();
-  for (int lv = 0; lv < c.nlevel; lv++) {
-    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
-      int b = m.lvl_body[k], p = m.body_parent[b];
+  BodyRec br;
+  const bool act = load_body(c, br);
+  float f6[6] = {0, 0, 0, 0, 0, 0};  // applied wrench of this lane's body (read up front)
+  if (xfrc && act)
+    for (int e = 0; e < 6; e++) f6[e] = xfrc[6 * LANE + e];
+  for (int lv = 1; lv <= c.nlevel; lv++) {
+    if (act && br.depth == lv) {
+      const int b = LANE, p = br.parent;
       float cv[6], ca[6];
       for (int e = 0; e < 6; e++) { cv[e] = cvel[6 * p + e]; ca[e] = cacc[6 * p + e]; }
-      int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
-      for (int j = ja; j < ja + jn; j++) {
-        int da = m.jnt_dofadr[j];
-        if (m.jnt_type[j] == DXJ_FREE) {
+      for (int jj = 0; jj < br.jn; jj++) {
+        const int j = br.ja + jj;
+        const int da = jj == 0 ? br.jdof : m.jnt_dofadr[j];
+        const int jt = jj == 0 ? br.jtype : m.jnt_type[j];
+        if (jt == DXJ_FREE) {
           for (int q = 0; q < 3; q++)
             for (int e = 0; e < 6; e++) cdd[6 * (da + q) + e] = 0;
           for (int q = 0; q < 3; q++)
@@ -1797,7 +1851,7 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
           for (int e = 0; e < 6; e++) cv[e] += cdof[6 * da + e] * qvel[da];
         }
       }
-      for (int d = m.body_dofadr[b]; d >= 0 && d < m.body_dofadr[b] + m.body_dofnum[b]; d++)
+      for (int d = br.dofadr; d >= 0 && d < br.dofadr + br.dofnum; d++)
         for (int e = 0; e < 6; e++) ca[e] += cdd[6 * d + e] * qvel[d];
       for (int e = 0; e < 6; e++) { cvel[6 * b + e] = cv[e]; cacc[6 * b + e] = ca[e]; }
       // body force: I a + v x* I v - applied wrench (as com-frame spatial force)
@@ -1806,37 +1860,33 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
       mul_inert(t2, cinert + 10 * b, cv);
       cross_force(t3, cv, t2);
       for (int e = 0; e < 6; e++) cfrc[6 * b + e] = t1[e] + t3[e];
-      if (xfrc) {
-        const float* f = xfrc + 6 * b;
-        if (f[0] != 0 || f[1] != 0 || f[2] != 0 || f[3] != 0 || f[4] != 0 || f[5] != 0) {
-          const float* rc = c.f(c.L.rcom) + 3 * m.body_rootidx[b];
-          const float* xi = c.f(c.L.xipos) + 3 * b;
-          float off[3] = {xi[0] - rc[0], xi[1] - rc[1], xi[2] - rc[2]};
-          float tq[3];
-          cross3(tq, off, f);
-          cfrc[6 * b + 0] -= f[3] + tq[0];
-          cfrc[6 * b + 1] -= f[4] + tq[1];
-          cfrc[6 * b + 2] -= f[5] + tq[2];
-          cfrc[6 * b + 3] -= f[0];
-          cfrc[6 * b + 4] -= f[1];
-          cfrc[6 * b + 5] -= f[2];
-        }
+      if (f6[0] != 0 || f6[1] != 0 || f6[2] != 0 || f6[3] != 0 || f6[4] != 0 || f6[5] != 0) {
+        const float* rc = c.f(c.L.rcom) + 3 * br.rootidx;
+        const float* xi = c.f(c.L.xipos) + 3 * b;
+        float off[3] = {xi[0] - rc[0], xi[1] - rc[1], xi[2] - rc[2]};
+        float tq[3];
+        cross3(tq, off, f6);
+        cfrc[6 * b + 0] -= f6[3] + tq[0];
+        cfrc[6 * b + 1] -= f6[4] + tq[1];
+        cfrc[6 * b + 2] -= f6[5] + tq[2];
+        cfrc[6 * b + 3] -= f6[0];
+        cfrc[6 * b + 4] -= f6[1];
+        cfrc[6 * b + 5] -= f6[2];
       }
     }
     SYNC();
   }
-  for (int lv = c.nlevel - 1; lv > 0; lv--) {
-    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
-      int b = m.lvl_body[k], p = m.body_parent[b];
-      if (p > 0)
-        for (int e = 0; e < 6; e++) atomicAdd(cfrc + 6 * p + e, cfrc[6 * b + e]);
-    }
+  for (int lv = c.nlevel; lv >= 2; lv--) {
+    if (act && br.depth == lv && br.parent > 0)
+      for (int e = 0; e < 6; e++) atomicAdd(cfrc + 6 * br.parent + e, cfrc[6 * LANE + e]);
     SYNC();
   }
   // qfrc_smooth = passive - (bias - applied) + actuator
   float* qs = c.f(c.L.qfrc_smooth);
-  for (int d = LANE; d < nv; d += DX_WAVE)
-    qs[d] = -m.dof_damping[d] * qvel[d] - dot6(cdof + 6 * d, cfrc + 6 * m.dof_bodyid[d]);
+  for (int d = LANE; d < nv; d += DX_WAVE) {
+    const float4 d0 = m.dof_rec[2 * d], d1 = m.dof_rec[2 * d + 1];
+    qs[d] = -d1.y * qvel[d] - dot6(cdof + 6 * d, cfrc + 6 * __float_as_int(d0.x));
+  }
   SYNC();
   float* al = c.f(c.L.act_len);
   float* ctrl = c.f(c.L.ctrl);
@@ -2482,14 +2532,15 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
   float* cvel = c.f(c.L.cvel);
   if (LANE < 6) cvel[LANE] = 0;
   SYNC();
-  for (int lv = 0; lv < c.nlevel; lv++) {
-    for (int k = m.lvl_adr[lv] + LANE; k < m.lvl_adr[lv + 1]; k += DX_WAVE) {
-      int b = m.lvl_body[k], p = m.body_parent[b];
+  BodyRec br;
+  const bool act = load_body(c, br);
+  for (int lv = 1; lv <= c.nlevel; lv++) {
+    if (act && br.depth == lv) {
       float cv[6];
-      for (int e = 0; e < 6; e++) cv[e] = cvel[6 * p + e];
-      for (int d = m.body_dofadr[b]; d >= 0 && d < m.body_dofadr[b] + m.body_dofnum[b]; d++)
+      for (int e = 0; e < 6; e++) cv[e] = cvel[6 * br.parent + e];
+      for (int d = br.dofadr; d >= 0 && d < br.dofadr + br.dofnum; d++)
         for (int e = 0; e < 6; e++) cv[e] += cdof[6 * d + e] * qvel[d];
-      for (int e = 0; e < 6; e++) cvel[6 * b + e] = cv[e];
+      for (int e = 0; e < 6; e++) cvel[6 * LANE + e] = cv[e];
     }
     SYNC();
   }
