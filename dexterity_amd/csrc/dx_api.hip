@@ -816,6 +816,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.watch, E * 4);
   rc |= balloc(b, (void**)&B.niter, E * 4);
   rc |= balloc(b, (void**)&B.ncand, E * 4);
+  rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc

@@ -14,6 +14,7 @@
 // 0-2 pos, 3-11 frame (normal, tangents), 12 dist, 13 geom pair, 14 nnz | nrows << 8
 // (key while sorting), 15 first efc row, 16-17 friction (mu1, mu2), 18-19 dof support mask
 #define DX_MAX_NV 64      // dof bitmasks are uint64
+#define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
 
 enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };
 enum { DXJ_FREE = 0, DXJ_HINGE = 3 };
@@ -94,6 +95,7 @@ struct DevBatch {
   float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
   int* dbg_nefc;
   unsigned long long* stage_acc;  // [DX_NSTAGE] s_memtime cycles per stage (null: off)
+  float4* sepcache;               // [nenv][DX_SEP_SLOTS] (dir, pair + 1) of separated pairs
   const TaskParams* tp;           // device copies, reach sampling pass only (mode 2)
   const TaskState* ts;
 };

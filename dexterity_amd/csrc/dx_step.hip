@@ -224,6 +224,7 @@ struct CtxT {
   float* S;
   int* I;  // misc ints
   unsigned long long* stage_acc;
+  float4* sep = nullptr;  // this env's separating-direction cache (DX_SEP_SLOTS), or null
   __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
       : m(m_), S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
@@ -238,6 +239,7 @@ struct CtxT<SpecRT> {
   float* S;
   int* I;
   unsigned long long* stage_acc;
+  float4* sep = nullptr;
   __device__ CtxT(const DevModel& m_, const Lds& L_, float* S_, int* I_, unsigned long long* acc)
       : m(m_), L(L_),
 #define DX_X(n) n(m_.n),
@@ -1033,7 +1035,10 @@ struct MprState {
   float dir[3];
   int phase, it;
 };
-__device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprState& S) {
+// cached: a separating direction of this pair from an earlier collision pass (world
+// frame), tried first (phase -1): if the supports along it do not reach the origin the
+// pair is separated -- the verdict MPR's own tests give -- in one support pass.
+__device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprState& S, const float* cached) {
   MPoint P0;
   sub3(P0.v, A.center, B.center);
   for (int k = 0; k < 3; k++) { P0.a[k] = A.center[k]; P0.b[k] = B.center[k]; }
@@ -1043,6 +1048,10 @@ __device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprStat
   normalize3(S.dir);
   S.phase = 0;
   S.it = 0;
+  if (cached) {
+    S.dir[0] = cached[0]; S.dir[1] = cached[1]; S.dir[2] = cached[2];
+    S.phase = -1;
+  }
 }
 // Returns 0: running, 1: separated (no contact), 2: penetration (depth/normal/pos set).
 __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState& S, float& depth, float* normal,
@@ -1057,6 +1066,14 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
   support_pair(A, B, dir, p.a, p.b);
   sub3(p.v, p.a, p.b);
   st.support++;
+  if (S.phase == -1) {  // cached separating direction
+    float dt = dot3(p.v, dir);
+    if (fzero(dt) || dt < 0) return 1;
+    dir[0] = -v0[0]; dir[1] = -v0[1]; dir[2] = -v0[2];
+    normalize3(dir);
+    S.phase = 0;
+    return 0;
+  }
   if (S.phase == 0) {
     mp_st(P + 9, p);  // P1
     float dt = dot3(p.v, dir);
@@ -1499,6 +1516,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     float margin = 0;
     Shape A, B;
     MprState M;
+    bool cached = false;
     M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
     for (;;) {
       bool act = q < ng;
@@ -1521,7 +1539,10 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
             margin = pr.z;
             make_shape_rec(c, __float_as_int(pr.x), 0.5f * margin, A);
             make_shape_rec(c, __float_as_int(pr.y), 0.5f * margin, B);
-            mpr_init(A, B, M);
+            float4 ce = c.sep ? c.sep[gp & (DX_SEP_SLOTS - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            cached = __float_as_int(ce.w) == gp + 1;
+            const float cd[3] = {ce.x, ce.y, ce.z};
+            mpr_init(A, B, M, cached ? cd : nullptr);
             fresh = false;
             stepping = true;
           }
@@ -1529,6 +1550,11 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
         if (stepping) {
           float depth, nrm[3], pos[3];
           int r = mpr_step(A, B, M, depth, nrm, pos, st);
+          if (r && c.sep && SL == 0) {
+            // remember a separating direction; forget it once the pair touches
+            if (r == 1) c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1));
+            else if (cached) c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
           if (r) {
             done = true;
             if (r == 2) {
@@ -2713,6 +2739,7 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   const Lds& L = c.L;
   int* I = (int*)(smem + L.ints);
   c.I = I;
+  c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
   // Zero the whole per-env LDS block once: the Cholesky solve reads a few words past
   // its packed triangles (padding lanes/columns, multiplied by exact zeros), and
   // those must be finite rather than whatever an earlier workgroup left behind.
