@@ -1386,13 +1386,26 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int half = cmax / 3;
   int* pref = cand + half;
   int nbc = 0, ngp = 0;
+  // the next chunk's records are loaded while this chunk is tested (one memory
+  // round trip in flight across chunk boundaries)
+  float4 nx[6];
+  {
+    const int bp0 = min(LANE, c.nbpair - 1);
+    const DXG float4* R = m.bpair_rec + 6 * max(bp0, 0);
+#pragma unroll
+    for (int k = 0; k < 6; k++) nx[k] = R[k];
+  }
   for (int base = 0; base < c.nbpair; base += DX_WAVE) {
     int bp = base + LANE;
     bool keep = false;
     int cnt = 0, adr = 0;
+    const float4 r0 = nx[0], s1 = nx[1], s2 = nx[2], r3 = nx[3], r4 = nx[4], r5 = nx[5];
+    if (base + DX_WAVE < c.nbpair) {
+      const DXG float4* R = m.bpair_rec + 6 * min(base + DX_WAVE + LANE, c.nbpair - 1);
+#pragma unroll
+      for (int k = 0; k < 6; k++) nx[k] = R[k];
+    }
     if (bp < c.nbpair) {
-      const DXG float4* R = m.bpair_rec + 6 * bp;
-      float4 r0 = R[0], s1 = R[1], s2 = R[2], r3 = R[3], r4 = R[4], r5 = R[5];
       int b1 = __float_as_int(r0.x), b2 = __float_as_int(r0.y);
       adr = __float_as_int(r0.z);
       keep = true;
@@ -1627,6 +1640,7 @@ __device__ __forceinline__ float impedance(const float* solimp, float violation)
   if (x >= 1) return dmax;
   float y;
   if (power == 1) y = x;
+  else if (power == 2) y = x <= mid ? x * x / mid : 1 - (1 - x) * (1 - x) / (1 - mid);  // MuJoCo's default
   else if (x <= mid) y = powf(x, power) / powf(mid, power - 1);
   else y = 1 - powf(1 - x, power) / powf(1 - mid, power - 1);
   return d0 + y * (dmax - d0);
