@@ -817,9 +817,20 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.niter, E * 4);
   rc |= balloc(b, (void**)&B.ncand, E * 4);
   rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
+  if (!getenv("DX_NO_LPT_ORDER")) {
+    void* po = nullptr;
+    rc |= balloc(b, (void**)&B.cost, E * 4);
+    rc |= balloc(b, &po, E * 4);
+    B.order = (const int*)po;
+  }
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
+  if (B.order && dx_launch_order(nenv, b->stream, B.cost, (int*)B.order) != hipSuccess) {  // a permutation
+    fail(DX_EHIP, "order kernel launch failed");
+    dx_batch_destroy(b);
+    return nullptr;
+  }
   B.watch_geom = -1;
   B.watch_body = -1;
   if (dx_reset(b, 0, nenv) != 0) { dx_batch_destroy(b); return nullptr; }
@@ -937,6 +948,8 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   hipError_t e = dx_launch_step(b->spec, b->nenv, lds, b->stream, b->dm, b->db, b->model->lds, nsub, mode);
   timing_end(b, t0);
   HIPCHK(e);
+  // next launch: heaviest environments first (costs just measured)
+  if (mode == 0 && b->db.order) HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order));
   return 0;
 }
 

@@ -96,6 +96,8 @@ struct DevBatch {
   int* dbg_nefc;
   unsigned long long* stage_acc;  // [DX_NSTAGE] s_memtime cycles per stage (null: off)
   float4* sepcache;               // [nenv][DX_SEP_SLOTS] (dir, pair + 1) of separated pairs
+  const int* order;               // [nenv] workgroup -> env (heaviest first), or null
+  unsigned* cost;                 // [nenv] shader cycles / 1024 of the env's last step, or null
   const TaskParams* tp;           // device copies, reach sampling pass only (mode 2)
   const TaskState* ts;
 };
@@ -161,3 +163,4 @@ __device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, i
 int dx_spec_find(const DevModel& d, const Lds& L);
 hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
+hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);

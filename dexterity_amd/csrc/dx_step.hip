@@ -2746,8 +2746,10 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
 template <class SP>
 __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode) {
   extern __shared__ float smem[];
-  int env = blockIdx.x;
-  if (env >= B.nenv) return;
+  if ((int)blockIdx.x >= B.nenv) return;
+  // longest-first dispatch: the order kernel sorts envs by their last step's cost
+  int env = B.order ? B.order[blockIdx.x] : (int)blockIdx.x;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
   if (mode == 2 && !B.ts->need[env]) return;
   CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
   const Lds& L = c.L;
@@ -2849,6 +2851,8 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
     B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
   }
   if (LANE == 0) B.time[env] = time;
+  if (LANE == 0 && B.cost && mode == 0)
+    B.cost[env] = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
 }
 
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
@@ -2889,6 +2893,31 @@ int dx_spec_find(const DevModel& d, const Lds& L) {
 #undef DX_TRY
   (void)k;
   return -1;
+}
+
+// Longest-processing-time-first dispatch order: a counting sort of the envs by their
+// last step's cost (descending, 256 buckets of 16 K shader cycles), one workgroup.
+// The order within a bucket depends on atomic timing, which only changes which CU
+// runs an environment, never its results.
+__global__ void __launch_bounds__(1024) dx_order_kernel(int nenv, const unsigned* cost, int* order) {
+  __shared__ int hist[256];
+  __shared__ int base[256];
+  const int t = threadIdx.x;
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  for (int e = t; e < nenv; e += 1024) atomicAdd(&hist[255 - (int)min(cost[e] >> 4, 255u)], 1);
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int k = 0; k < 256; k++) { base[k] = acc; acc += hist[k]; }
+  }
+  __syncthreads();
+  for (int e = t; e < nenv; e += 1024) order[atomicAdd(&base[255 - (int)min(cost[e] >> 4, 255u)], 1)] = e;
+}
+
+hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order) {
+  hipLaunchKernelGGL(dx_order_kernel, dim3(1), dim3(1024), 0, stream, nenv, cost, order);
+  return hipGetLastError();
 }
 
 hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
