@@ -28,6 +28,7 @@ EXPORTS = (
     "dx_env_step", "dx_env_output", "dx_env_action_buffer", "dx_env_sample_actions",
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
     "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout", "dx_env_goal_dim",
+    "dx_jac_site", "dx_ik_solve",
 )
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
@@ -44,6 +45,22 @@ _lib = None
 
 class DxError(RuntimeError):
     pass
+
+
+class IkOptions(ctypes.Structure):
+    """struct dx_ik_options (include/dx.h)."""
+
+    _fields_ = [
+        ("linear_tol", ctypes.c_float),
+        ("regularization", ctypes.c_float),
+        ("gain", ctypes.c_float),
+        ("progress_threshold", ctypes.c_float),
+        ("max_steps", ctypes.c_int32),
+        ("early_stop", ctypes.c_int32),
+        ("num_attempts", ctypes.c_int32),
+        ("stop_on_first", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
 
 
 def load(path: str = LIB_PATH):
@@ -102,6 +119,8 @@ def load(path: str = LIB_PATH):
     L.dx_stage_timing.argtypes = [vp, ctypes.c_int]
     L.dx_stage_read.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), i32]
     L.dx_debug_poison_lds.argtypes = [i32]
+    L.dx_jac_site.argtypes = [vp, vp, i32, vp, vp]
+    L.dx_ik_solve.argtypes = [vp, ctypes.POINTER(IkOptions), vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
     _lib = L
     return L
 

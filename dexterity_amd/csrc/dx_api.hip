@@ -963,6 +963,129 @@ extern "C" int dx_forward(dx_batch* b) {
   return launch_step(b, 1, 1);
 }
 
+// ------------------------------------------------------------------------ //
+// site Jacobians and batched IK (dx_ik.hip)
+// ------------------------------------------------------------------------ //
+// Per-call device scratch, released (after the batch stream drains) on every exit path.
+struct CallScratch {
+  hipStream_t s;
+  std::vector<void*> p;
+  explicit CallScratch(hipStream_t s_) : s(s_) {}
+  ~CallScratch() {
+    (void)hipStreamSynchronize(s);
+    for (void* q : p) (void)hipFree(q);
+  }
+  void* get(size_t bytes) {
+    void* q = nullptr;
+    if (hipMalloc(&q, std::max<size_t>(bytes, 4)) != hipSuccess) return nullptr;
+    p.push_back(q);
+    return q;
+  }
+};
+
+static int ik_check_sites(dx_batch* b, const int32_t* sites, int32_t nsite) {
+  if (!sites || nsite < 1 || 3 * nsite > 32) return fail(DX_EINVAL, "need 1 <= nsite <= 10 site ids");
+  for (int s = 0; s < nsite; s++)
+    if (sites[s] < 0 || sites[s] >= b->dm.nsite) return fail(DX_EINVAL, "site id out of range");
+  return 0;
+}
+
+static int ik_lds_bytes(dx_batch* b, size_t* bytes) {
+  *bytes = ((size_t)b->model->lds.total + dx_ik_lds_words(b->dm, 0)) * 4;
+  if (*bytes > 160 * 1024) return fail(DX_ELIMIT, "IK LDS footprint exceeds 160 KiB");
+  return 0;
+}
+
+extern "C" int dx_jac_site(dx_batch* b, const int32_t* sites, int32_t nsite, float* jacp, float* jacr) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (int rc = ik_check_sites(b, sites, nsite)) return rc;
+  size_t lds;
+  if (int rc = ik_lds_bytes(b, &lds)) return rc;
+  HIPCHK(hipSetDevice(b->device));
+  CallScratch S(b->stream);
+  IkDev P;
+  memset(&P, 0, sizeof(P));
+  P.mode = 1;
+  P.nsite = nsite;
+  P.blk = b->model->lds.total;
+  const size_t n = (size_t)b->nenv * 3 * nsite * b->dm.nv;
+  int* ds = (int*)S.get(nsite * 4);
+  P.jacp = jacp ? (float*)S.get(n * 4) : nullptr;
+  P.jacr = jacr ? (float*)S.get(n * 4) : nullptr;
+  if (!ds || (jacp && !P.jacp) || (jacr && !P.jacr)) return fail(DX_ENOMEM, "device scratch allocation failed");
+  P.sites = ds;
+  HIPCHK(hipMemcpyAsync(ds, sites, nsite * 4, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(dx_launch_ik(b->nenv, lds, b->stream, b->dm, b->db, b->model->lds, P));
+  if (jacp) HIPCHK(hipMemcpyAsync(jacp, P.jacp, n * 4, hipMemcpyDefault, b->stream));
+  if (jacr) HIPCHK(hipMemcpyAsync(jacr, P.jacr, n * 4, hipMemcpyDefault, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
+extern "C" int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t* sites, int32_t nsite,
+                           const int32_t* joints, int32_t njoint, const float* targets, float* qpos_out,
+                           int32_t* success, float* linear_err, int32_t* attempt, int32_t* steps) {
+  if (!b || !opt || !targets) return fail(DX_EINVAL, "null batch, options or targets");
+  if (int rc = ik_check_sites(b, sites, nsite)) return rc;
+  if (!joints || njoint < 1 || njoint > DX_MAX_NV) return fail(DX_EINVAL, "need 1 <= njoint <= 64 joint ids");
+  const std::vector<int>& jtype = b->model->hi.at("jnt_type");
+  for (int k = 0; k < njoint; k++) {
+    if (joints[k] < 0 || joints[k] >= b->dm.njnt) return fail(DX_EINVAL, "joint id out of range");
+    if (jtype[joints[k]] == DXJ_FREE) return fail(DX_EINVAL, "IK joints must be hinge or slide joints");
+  }
+  if (opt->max_steps < 1 || opt->num_attempts < 1) return fail(DX_EINVAL, "max_steps and num_attempts must be >= 1");
+  if (!(opt->regularization > 0.f)) return fail(DX_EINVAL, "regularization must be positive");
+  size_t lds;
+  if (int rc = ik_lds_bytes(b, &lds)) return rc;
+  const size_t E = b->nenv, A = opt->num_attempts;
+  if (E * A > 0x7fffffffull) return fail(DX_EINVAL, "nenv * num_attempts too large");
+  HIPCHK(hipSetDevice(b->device));
+  CallScratch S(b->stream);
+  IkDev P;
+  memset(&P, 0, sizeof(P));
+  P.mode = 0;
+  P.nsite = nsite;
+  P.njoint = njoint;
+  P.max_steps = opt->max_steps;
+  P.early_stop = opt->early_stop != 0;
+  P.nattempt = (int)A;
+  P.stop_on_first = opt->stop_on_first != 0;
+  P.tol = opt->linear_tol;
+  P.reg = opt->regularization;
+  P.gain = opt->gain;
+  P.progress = opt->progress_threshold;
+  P.seed = opt->seed;
+  P.blk = b->model->lds.total;
+  int* ds = (int*)S.get(nsite * 4);
+  int* dj = (int*)S.get(njoint * 4);
+  float* dt = (float*)S.get(E * 3 * nsite * 4);
+  P.att_qpos = (float*)S.get(E * A * njoint * 4);
+  P.att_err = (float*)S.get(E * A * nsite * 4);
+  P.att_steps = (int*)S.get(E * A * 4);
+  float* oq = (float*)S.get(E * njoint * 4);
+  int* os = (int*)S.get(E * 4);
+  float* oe = (float*)S.get(E * nsite * 4);
+  int* oa = (int*)S.get(E * 4);
+  int* ot = (int*)S.get(E * 4);
+  if (!ds || !dj || !dt || !P.att_qpos || !P.att_err || !P.att_steps || !oq || !os || !oe || !oa || !ot)
+    return fail(DX_ENOMEM, "device scratch allocation failed");
+  HIPCHK(hipMemcpyAsync(ds, sites, nsite * 4, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(dj, joints, njoint * 4, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipMemcpyAsync(dt, targets, E * 3 * nsite * 4, hipMemcpyDefault, b->stream));
+  P.sites = ds;
+  P.joints = dj;
+  P.targets = dt;
+  HIPCHK(dx_launch_ik((int)(E * A), lds, b->stream, b->dm, b->db, b->model->lds, P));
+  HIPCHK(dx_launch_ik_select((int)E, b->stream, b->dm, P, oq, os, oe, oa, ot));
+  if (qpos_out) HIPCHK(hipMemcpyAsync(qpos_out, oq, E * njoint * 4, hipMemcpyDefault, b->stream));
+  if (success) HIPCHK(hipMemcpyAsync(success, os, E * 4, hipMemcpyDefault, b->stream));
+  if (linear_err) HIPCHK(hipMemcpyAsync(linear_err, oe, E * nsite * 4, hipMemcpyDefault, b->stream));
+  if (attempt) HIPCHK(hipMemcpyAsync(attempt, oa, E * 4, hipMemcpyDefault, b->stream));
+  if (steps) HIPCHK(hipMemcpyAsync(steps, ot, E * 4, hipMemcpyDefault, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
+}
+
 extern "C" void* dx_stream(dx_batch* b) { return b ? (void*)b->stream : nullptr; }
 
 extern "C" int dx_sync(dx_batch* b) {

@@ -1,0 +1,646 @@
+// dx_device.h -- device toolkit shared by the step kernel (dx_step.hip) and the
+// kinematic-query / inverse-kinematics kernels (dx_ik.hip): wave primitives, small
+// 3D / spatial algebra, the per-env context, the tree passes (kinematics, com
+// positions, tendons, CRB) and the wave / matrix-core Cholesky solvers.
+#pragma once
+#include "dx_internal.h"
+
+#include <math.h>
+#include <string.h>
+
+// The lane id is laundered through an empty volatile asm at every use: the compiler
+// can then neither hoist lane-dependent address arithmetic out of the substep loop
+// nor keep it alive across the stages (it did, and spilled those values to scratch).
+__device__ __forceinline__ int lane_id() {
+  int l = (int)threadIdx.x;
+  asm volatile("" : "+v"(l));
+  return l;
+}
+#define LANE (lane_id())
+// A workgroup is exactly one wavefront, and a wavefront's LDS instructions execute
+// in issue order, so cross-lane LDS hand-offs need only a compiler-level barrier
+// (no s_barrier, and no s_waitcnt on outstanding global stores).
+#define SYNC() __builtin_amdgcn_wave_barrier()
+
+// ------------------------------------------------------------------------ //
+// wave helpers
+// ------------------------------------------------------------------------ //
+// DPP row reductions (gfx9 family): quad_perm, row_half_mirror, row_mirror, then
+// row_bcast15 / row_bcast31 carry the partial results up to lane 63.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK, 0xF, false));
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xF, false);
+}
+// Sums: quad, half-row, row sums by DPP, then rows carried up to lane 63 (each lane
+// contributes exactly once), broadcast with readlane.
+__device__ __forceinline__ float wave_sum(float v) {
+  v += dpp_f<0xB1, 0xF>(v);
+  v += dpp_f<0x4E, 0xF>(v);
+  v += dpp_f<0x141, 0xF>(v);
+  v += dpp_f<0x140, 0xF>(v);
+  v += dpp_f<0x142, 0xA>(v);
+  v += dpp_f<0x143, 0xC>(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+  v += dpp_i<0xB1, 0xF>(v);
+  v += dpp_i<0x4E, 0xF>(v);
+  v += dpp_i<0x141, 0xF>(v);
+  v += dpp_i<0x140, 0xF>(v);
+  v += dpp_i<0x142, 0xA>(v);
+  v += dpp_i<0x143, 0xC>(v);
+  return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ float wave_max_f(float m) {
+  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x141, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x140, 0xF>(m));
+  m = fmaxf(m, dpp_f<0x142, 0xA>(m));
+  m = fmaxf(m, dpp_f<0x143, 0xC>(m));
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 63));
+}
+__device__ __forceinline__ int wave_min_i(int m) {
+  m = min(m, dpp_i<0xB1, 0xF>(m));
+  m = min(m, dpp_i<0x4E, 0xF>(m));
+  m = min(m, dpp_i<0x141, 0xF>(m));
+  m = min(m, dpp_i<0x140, 0xF>(m));
+  m = min(m, dpp_i<0x142, 0xA>(m));
+  m = min(m, dpp_i<0x143, 0xC>(m));
+  return __builtin_amdgcn_readlane(m, 63);
+}
+// index of the first (lowest-index) maximum over lanes' (best, index) pairs
+__device__ __forceinline__ int wave_argmax_first(float best, int bi) {
+  float vmax = wave_max_f(best);
+  return wave_min_i(best == vmax ? bi : 0x7fffffff);
+}
+
+// Inclusive prefix sum over the wave by DPP: Hillis-Steele within each 16-lane row
+// (row_shr 1, 2, 4, 8 with zero fill), then row_bcast:15 / row_bcast:31 carry the
+// row totals upwards.  No LDS round trip.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i0(int x) {  // lanes without a source read 0
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xF, false);
+}
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += dpp_i0<0x111, 0xF>(x);  // row_shr:1
+  x += dpp_i0<0x112, 0xF>(x);  // row_shr:2
+  x += dpp_i0<0x114, 0xF>(x);  // row_shr:4
+  x += dpp_i0<0x118, 0xF>(x);  // row_shr:8
+  x += dpp_i0<0x142, 0xA>(x);  // row_bcast:15 -> rows 1, 3
+  x += dpp_i0<0x143, 0xC>(x);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+// exclusive prefix sum over lanes
+__device__ __forceinline__ int wave_excl_scan(int v) { return wave_incl_scan(v) - v; }
+
+// ------------------------------------------------------------------------ //
+// small math
+// ------------------------------------------------------------------------ //
+__device__ __forceinline__ float dot3(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+}
+__device__ __forceinline__ void cross3(float* r, const float* a, const float* b) {
+  float t0 = a[1] * b[2] - a[2] * b[1], t1 = a[2] * b[0] - a[0] * b[2], t2 = a[0] * b[1] - a[1] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void sub3(float* r, const float* a, const float* b) {
+  r[0] = a[0] - b[0]; r[1] = a[1] - b[1]; r[2] = a[2] - b[2];
+}
+__device__ __forceinline__ float norm3(const float* a) { return sqrtf(dot3(a, a)); }
+__device__ __forceinline__ void normalize3(float* a) {
+  float n = norm3(a);
+  if (n > 1e-20f) { float s = 1.0f / n; a[0] *= s; a[1] *= s; a[2] *= s; }
+}
+__device__ __forceinline__ void matvec3(float* r, const float* R, const float* v) {
+  float t0 = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
+  float t1 = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
+  float t2 = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void mattvec3(float* r, const float* R, const float* v) {
+  float t0 = R[0] * v[0] + R[3] * v[1] + R[6] * v[2];
+  float t1 = R[1] * v[0] + R[4] * v[1] + R[7] * v[2];
+  float t2 = R[2] * v[0] + R[5] * v[1] + R[8] * v[2];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+__device__ __forceinline__ void matmul3(float* r, const float* A, const float* B) {
+  float t[9];
+#pragma unroll
+  for (int i = 0; i < 3; i++)
+#pragma unroll
+    for (int j = 0; j < 3; j++) t[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = t[i];
+}
+__device__ __forceinline__ void quat2mat(float* R, const float* q) {
+  float w = q[0], x = q[1], y = q[2], z = q[3];
+  R[0] = 1 - 2 * (y * y + z * z); R[1] = 2 * (x * y - w * z); R[2] = 2 * (x * z + w * y);
+  R[3] = 2 * (x * y + w * z); R[4] = 1 - 2 * (x * x + z * z); R[5] = 2 * (y * z - w * x);
+  R[6] = 2 * (x * z - w * y); R[7] = 2 * (y * z + w * x); R[8] = 1 - 2 * (x * x + y * y);
+}
+__device__ __forceinline__ void quatmul(float* r, const float* a, const float* b) {
+  float t0 = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+  float t1 = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+  float t2 = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+  float t3 = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2; r[3] = t3;
+}
+__device__ __forceinline__ void quatnorm(float* q) {
+  float n = sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  if (n < 1e-20f) { q[0] = 1; q[1] = q[2] = q[3] = 0; return; }
+  float s = 1.0f / n;
+  q[0] *= s; q[1] *= s; q[2] *= s; q[3] *= s;
+}
+// spatial algebra: [angular; linear] about the root-com frame origin
+__device__ __forceinline__ void mul_inert(float* r, const float* I, const float* v) {
+  const float* w = v;
+  const float* l = v + 3;
+  const float* mc = I + 6;
+  float m = I[9];
+  r[0] = I[0] * w[0] + I[3] * w[1] + I[4] * w[2] + (mc[1] * l[2] - mc[2] * l[1]);
+  r[1] = I[3] * w[0] + I[1] * w[1] + I[5] * w[2] + (mc[2] * l[0] - mc[0] * l[2]);
+  r[2] = I[4] * w[0] + I[5] * w[1] + I[2] * w[2] + (mc[0] * l[1] - mc[1] * l[0]);
+  r[3] = m * l[0] - (mc[1] * w[2] - mc[2] * w[1]);
+  r[4] = m * l[1] - (mc[2] * w[0] - mc[0] * w[2]);
+  r[5] = m * l[2] - (mc[0] * w[1] - mc[1] * w[0]);
+}
+__device__ __forceinline__ void cross_motion(float* r, const float* v, const float* m) {
+  float a[3], b[3], c[3];
+  cross3(a, v, m);
+  cross3(b, v, m + 3);
+  cross3(c, v + 3, m);
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2];
+  r[3] = b[0] + c[0]; r[4] = b[1] + c[1]; r[5] = b[2] + c[2];
+}
+__device__ __forceinline__ void cross_force(float* r, const float* v, const float* f) {
+  float a[3], b[3], c[3];
+  cross3(a, v, f);
+  cross3(b, v + 3, f + 3);
+  cross3(c, v, f + 3);
+  r[0] = a[0] + b[0]; r[1] = a[1] + b[1]; r[2] = a[2] + b[2];
+  r[3] = c[0]; r[4] = c[1]; r[5] = c[2];
+}
+__device__ __forceinline__ float dot6(const float* a, const float* b) {
+  return a[0] * b[0] + a[1] * b[1] + a[2] * b[2] + a[3] * b[3] + a[4] * b[4] + a[5] * b[5];
+}
+
+// ------------------------------------------------------------------------ //
+// per-env context
+// ------------------------------------------------------------------------ //
+// The model's dimensions and the LDS layout come either from the launch (generic
+// kernel) or from a compile-time model specialization (dx_specs.inc, generated by
+// build.py for the shipped scenes): then every LDS offset is an immediate, loop
+// bounds are constants, and far fewer scalar registers stay live (the generic
+// kernel spills its ~60 layout/dimension scalars into VGPR lanes).
+#define DX_DIMS(X) X(nq) X(nv) X(nbody) X(njnt) X(nu) X(ntendon) X(nsite) X(nlevel) X(nroot) \
+  X(nfric) X(nlimj) X(nlimt) X(nbpair) X(any_damping) X(disable_contact) X(iterations)
+struct SpecRT {};
+template <class SP>
+struct CtxT {
+  const DevModel& m;
+  static constexpr Lds L = SP::L;
+#define DX_X(n) static constexpr int n = SP::n;
+  DX_DIMS(DX_X)
+#undef DX_X
+  float* S;
+  int* I;  // misc ints
+  unsigned long long* stage_acc;
+  float4* sep = nullptr;  // this env's separating-direction cache (DX_SEP_SLOTS), or null
+  __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
+      : m(m_), S(S_), I(I_), stage_acc(acc) {}
+  __device__ float* f(int off) const { return S + off; }
+};
+template <>
+struct CtxT<SpecRT> {
+  const DevModel& m;
+  const Lds& L;
+#define DX_X(n) int n;
+  DX_DIMS(DX_X)
+#undef DX_X
+  float* S;
+  int* I;
+  unsigned long long* stage_acc;
+  float4* sep = nullptr;
+  __device__ CtxT(const DevModel& m_, const Lds& L_, float* S_, int* I_, unsigned long long* acc)
+      : m(m_), L(L_),
+#define DX_X(n) n(m_.n),
+        DX_DIMS(DX_X)
+#undef DX_X
+        S(S_), I(I_), stage_acc(acc) {}
+  __device__ float* f(int off) const { return S + off; }
+};
+// Per-stage cycle accounting (runtime-gated by DevBatch::stage_acc, lane 0 only).
+enum {
+  ST_KIN = 0, ST_CRB, ST_BROAD, ST_MID, ST_NARROW, ST_CON, ST_VEL, ST_SMOOTH, ST_NEWTON_EVAL,
+  ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO,
+  ST_MATVEC, ST_NP_MPR, ST_JACVEC,
+  CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
+  CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC  // event counters, not cycles
+};
+template <class Ctx>
+__device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
+  if (c.stage_acc && LANE == 0) {
+    unsigned long long t = __builtin_amdgcn_s_memtime();
+    unsigned long long* last = (unsigned long long*)(c.I + 10);
+    c.stage_acc[k] += t - *last;  // this env's own slots
+    *last = t;
+  }
+}
+template <class Ctx>
+__device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
+  if (c.stage_acc && LANE == 0) c.stage_acc[k] += n;
+}
+// misc int slots
+enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
+
+// ------------------------------------------------------------------------ //
+// position stage
+// ------------------------------------------------------------------------ //
+// Per-body model data of lane b = body (nbody <= 64), loaded in one memory round trip
+// at the start of a tree pass (dx_api.hip body_rec); the level loops then touch only
+// LDS.  Joint fields are the body's first joint (Shadow / Adroit bodies have <= 1).
+struct BodyRec {
+  int parent, depth, ja, jn, jtype, qadr, dofadr, dofnum, jdof, rootidx;
+  float pos[3], quat[4], ipos[3], jpos[3], jaxis[3], q0, mass;
+};
+template <class Ctx>
+__device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
+  const int b = LANE;
+  const bool act = b >= 1 && b < c.nbody;
+  const DXG float4* R = c.m.body_rec + 8 * (act ? b : 0);
+  const float4 a = R[0], p = R[1], q = R[2], i = R[3], jp = R[4], jx = R[5], d = R[6];
+  r.parent = __float_as_int(a.x);
+  r.depth = act ? __float_as_int(a.y) : -1;
+  r.ja = __float_as_int(a.z);
+  r.jn = __float_as_int(a.w);
+  r.pos[0] = p.x; r.pos[1] = p.y; r.pos[2] = p.z;
+  r.jtype = __float_as_int(p.w);
+  r.quat[0] = q.x; r.quat[1] = q.y; r.quat[2] = q.z; r.quat[3] = q.w;
+  r.ipos[0] = i.x; r.ipos[1] = i.y; r.ipos[2] = i.z;
+  r.rootidx = __float_as_int(i.w);
+  r.jpos[0] = jp.x; r.jpos[1] = jp.y; r.jpos[2] = jp.z;
+  r.qadr = __float_as_int(jp.w);
+  r.jaxis[0] = jx.x; r.jaxis[1] = jx.y; r.jaxis[2] = jx.z;
+  r.q0 = jx.w;
+  r.dofadr = __float_as_int(d.x);
+  r.dofnum = __float_as_int(d.y);
+  r.mass = d.z;
+  r.jdof = __float_as_int(d.w);
+  return act;
+}
+
+template <class Ctx>
+__device__ __forceinline__ void kinematics(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* qpos = c.f(c.L.qpos);
+  float* xpos = c.f(c.L.xpos);
+  float* xquat = c.f(c.L.xquat);
+  float* xmat = c.f(c.L.xmat);
+  float* xipos = c.f(c.L.xipos);
+  float* xanchor = c.f(c.L.xanchor);
+  float* xaxis = c.f(c.L.xaxis);
+  BodyRec br;
+  const bool act = load_body(c, br);
+  if (LANE == 0) {
+    xpos[0] = xpos[1] = xpos[2] = 0;
+    xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
+    for (int k = 0; k < 9; k++) xmat[k] = (k % 4 == 0) ? 1.f : 0.f;
+    xipos[0] = xipos[1] = xipos[2] = 0;
+  }
+  SYNC();
+  for (int lv = 1; lv <= c.nlevel; lv++) {
+    if (act && br.depth == lv) {
+      const int b = LANE, p = br.parent, ja = br.ja, jn = br.jn;
+      float xp[3], xq[4];
+      if (jn > 0 && br.jtype == DXJ_FREE) {
+        const float* q = qpos + br.qadr;
+        xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
+        xq[0] = q[3]; xq[1] = q[4]; xq[2] = q[5]; xq[3] = q[6];
+        quatnorm(xq);
+        xanchor[3 * ja] = xp[0]; xanchor[3 * ja + 1] = xp[1]; xanchor[3 * ja + 2] = xp[2];
+        xaxis[3 * ja] = 0; xaxis[3 * ja + 1] = 0; xaxis[3 * ja + 2] = 1;
+      } else {
+        float t[3];
+        matvec3(t, xmat + 9 * p, br.pos);
+        xp[0] = xpos[3 * p] + t[0]; xp[1] = xpos[3 * p + 1] + t[1]; xp[2] = xpos[3 * p + 2] + t[2];
+        quatmul(xq, xquat + 4 * p, br.quat);
+        for (int jj = 0; jj < jn; jj++) {
+          const int j = ja + jj;
+          float jp[3], ja3[3], q0;
+          int qa;
+          if (jj == 0) {
+            for (int k = 0; k < 3; k++) { jp[k] = br.jpos[k]; ja3[k] = br.jaxis[k]; }
+            qa = br.qadr;
+            q0 = br.q0;
+          } else {
+            for (int k = 0; k < 3; k++) { jp[k] = m.jnt_pos[3 * j + k]; ja3[k] = m.jnt_axis[3 * j + k]; }
+            qa = m.jnt_qposadr[j];
+            q0 = m.qpos0[qa];
+          }
+          float R[9];
+          quat2mat(R, xq);
+          matvec3(t, R, jp);
+          float anc[3] = {t[0] + xp[0], t[1] + xp[1], t[2] + xp[2]};
+          float ax[3];
+          matvec3(ax, R, ja3);
+          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
+          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
+          float ang = qpos[qa] - q0;
+          float sn, co;
+          sincosf(0.5f * ang, &sn, &co);
+          float ql[4] = {co, ja3[0] * sn, ja3[1] * sn, ja3[2] * sn};
+          quatmul(xq, xq, ql);
+          quatnorm(xq);
+          quat2mat(R, xq);
+          matvec3(t, R, jp);
+          xp[0] = anc[0] - t[0]; xp[1] = anc[1] - t[1]; xp[2] = anc[2] - t[2];
+        }
+      }
+      float R[9];
+      quat2mat(R, xq);
+      for (int e = 0; e < 3; e++) xpos[3 * b + e] = xp[e];
+      for (int e = 0; e < 4; e++) xquat[4 * b + e] = xq[e];
+      for (int e = 0; e < 9; e++) xmat[9 * b + e] = R[e];
+      float t[3];
+      matvec3(t, R, br.ipos);
+      for (int e = 0; e < 3; e++) xipos[3 * b + e] = xp[e] + t[e];
+    }
+    SYNC();
+  }
+}
+
+template <class Ctx>
+__device__ __forceinline__ void com_pos(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* xipos = c.f(c.L.xipos);
+  float* xmat = c.f(c.L.xmat);
+  float* rcom = c.f(c.L.rcom);
+  // subtree com of every root (only roots are needed as com-frame origins)
+  for (int r = 0; r < c.nroot; r++) {
+    float s0 = 0, s1 = 0, s2 = 0, sm = 0;
+    for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
+      if (m.body_rootidx[b] != r) continue;
+      float ms = m.body_mass[b];
+      s0 += ms * xipos[3 * b]; s1 += ms * xipos[3 * b + 1]; s2 += ms * xipos[3 * b + 2]; sm += ms;
+    }
+    s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); sm = wave_sum(sm);
+    if (LANE == 0) {
+      int rb = m.root_body[r];
+      if (sm > 1e-15f) { rcom[3 * r] = s0 / sm; rcom[3 * r + 1] = s1 / sm; rcom[3 * r + 2] = s2 / sm; }
+      else { rcom[3 * r] = xipos[3 * rb]; rcom[3 * r + 1] = xipos[3 * rb + 1]; rcom[3 * r + 2] = xipos[3 * rb + 2]; }
+    }
+  }
+  SYNC();
+  float* cinert = c.f(c.L.cinert);
+  for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
+    float Rb[9];
+    matmul3(Rb, xmat + 9 * b, m.body_imat + 9 * b);
+    const float* I = m.body_inertia + 3 * b;
+    float mass = m.body_mass[b];
+    const float* rc = rcom + 3 * m.body_rootidx[b];
+    float off[3] = {xipos[3 * b] - rc[0], xipos[3 * b + 1] - rc[1], xipos[3 * b + 2] - rc[2]};
+    float Iw[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++)
+        Iw[3 * i + j] = Rb[3 * i] * I[0] * Rb[3 * j] + Rb[3 * i + 1] * I[1] * Rb[3 * j + 1] +
+                        Rb[3 * i + 2] * I[2] * Rb[3 * j + 2];
+    float dd = dot3(off, off);
+    float* ci = cinert + 10 * b;
+    ci[0] = Iw[0] + mass * (dd - off[0] * off[0]);
+    ci[1] = Iw[4] + mass * (dd - off[1] * off[1]);
+    ci[2] = Iw[8] + mass * (dd - off[2] * off[2]);
+    ci[3] = Iw[1] - mass * off[0] * off[1];
+    ci[4] = Iw[2] - mass * off[0] * off[2];
+    ci[5] = Iw[5] - mass * off[1] * off[2];
+    ci[6] = mass * off[0]; ci[7] = mass * off[1]; ci[8] = mass * off[2];
+    ci[9] = mass;
+  }
+  float* cdof = c.f(c.L.cdof);
+  float* xanchor = c.f(c.L.xanchor);
+  float* xaxis = c.f(c.L.xaxis);
+  for (int d = LANE; d < c.nv; d += DX_WAVE) {
+    const float4 dr = m.dof_rec[2 * d];
+    const int b = __float_as_int(dr.x), j = __float_as_int(dr.y), tk = __float_as_int(dr.w);
+    const float* rc = rcom + 3 * __float_as_int(dr.z);
+    float off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
+    float* cd = cdof + 6 * d;
+    if ((tk & 255) == DXJ_FREE) {
+      int k = tk >> 8;
+      if (k < 3) {
+        for (int e = 0; e < 6; e++) cd[e] = 0;
+        cd[3 + k] = 1;
+      } else {
+        const float* R = xmat + 9 * b;
+        float ax[3] = {R[k - 3], R[3 + k - 3], R[6 + k - 3]};
+        cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+        cross3(cd + 3, ax, off);
+      }
+    } else {
+      const float* ax = xaxis + 3 * j;
+      cd[0] = ax[0]; cd[1] = ax[1]; cd[2] = ax[2];
+      cross3(cd + 3, ax, off);
+    }
+  }
+  SYNC();
+}
+
+template <class Ctx>
+__device__ __forceinline__ void tendon_lengths(const Ctx& c) {
+  const DevModel& m = c.m;
+  float* qpos = c.f(c.L.qpos);
+  float* tl = c.f(c.L.ten_len);
+  for (int t = LANE; t < c.ntendon; t += DX_WAVE) {
+    float len = 0;
+    for (int w = m.tendon_adr[t]; w < m.tendon_adr[t] + m.tendon_num[t]; w++)
+      len += m.wrap_coef[w] * qpos[m.wrap_qadr[w]];
+    tl[t] = len;
+  }
+  SYNC();
+  float* al = c.f(c.L.act_len);
+  for (int i = LANE; i < c.nu; i += DX_WAVE) {
+    float g = m.actuator_gear[i];
+    al[i] = m.actuator_trntype[i] == 0 ? g * qpos[m.jnt_qposadr[m.actuator_trnid[i]]]
+                                       : g * tl[m.actuator_trnid[i]];
+  }
+}
+
+// Symmetric nv x nv matrices (M, the Newton Hessian, Cholesky factors) are stored
+// as packed lower triangles, row-major: (i, j <= i) -> ti(i) + j.
+__device__ __forceinline__ int ti(int i) { return (i * (i + 1)) >> 1; }
+
+template <class Ctx>
+__device__ __forceinline__ void crb_mass(const Ctx& c) {
+  const DevModel& m = c.m;
+  int nv = c.nv;
+  float* crb = c.f(c.L.scr);
+  float* cinert = c.f(c.L.cinert);
+  float* M = c.f(c.L.M);
+  float* cdof = c.f(c.L.cdof);
+  for (int k = LANE; k < 10 * c.nbody; k += DX_WAVE) crb[k] = cinert[k];
+  for (int k = LANE; k < ti(nv); k += DX_WAVE) M[k] = 0;
+  SYNC();
+  BodyRec br;
+  const bool act = load_body(c, br);
+  for (int lv = c.nlevel; lv >= 2; lv--) {
+    if (act && br.depth == lv && br.parent > 0)
+      for (int e = 0; e < 10; e++) atomicAdd(crb + 10 * br.parent + e, crb[10 * LANE + e]);
+    SYNC();
+  }
+  // row i: j over the dof's ancestors (incl. itself), a bit mask from dof_rec
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    const float4 d0 = m.dof_rec[2 * i], d1 = m.dof_rec[2 * i + 1];
+    float f[6];
+    mul_inert(f, crb + 10 * __float_as_int(d0.x), cdof + 6 * i);
+    uint64_t anc = (uint64_t)(uint32_t)__float_as_int(d1.z) | ((uint64_t)(uint32_t)__float_as_int(d1.w) << 32);
+    while (anc) {
+      int j = __ffsll((long long)anc) - 1;
+      anc &= anc - 1;
+      M[ti(i) + j] = dot6(cdof + 6 * j, f);
+    }
+    M[ti(i) + i] += d1.x;
+  }
+  SYNC();
+}
+
+// In-place dense Cholesky (lower, row-major) of the n x n matrix A, one wave.
+// Column k: lanes scale the sub-diagonal of column k, then update the trailing
+// lower triangle; entry t of a w x w trailing triangle maps to (ii, jj) through
+// the LDS table tri[t] = ii << 8 | jj (built once per launch), so the update is
+// branch-free and balanced over the 64 lanes.  Two barriers per column.
+__device__ __forceinline__ void wave_cholesky(float* A, int n, const unsigned short* tri) {
+  for (int k = 0; k < n; k++) {
+    float d = sqrtf(fmaxf(A[ti(k) + k], 1e-30f));
+    float inv = 1.0f / d;
+    for (int i = k + 1 + LANE; i < n; i += DX_WAVE) A[ti(i) + k] *= inv;
+    SYNC();
+    if (LANE == 0) A[ti(k) + k] = d;
+    int w = n - k - 1;
+    int tot = w * (w + 1) / 2;
+    for (int t = LANE; t < tot; t += DX_WAVE) {
+      int e = tri[t];
+      int i = k + 1 + (e >> 8), j = k + 1 + (e & 255);
+      A[ti(i) + j] -= A[ti(i) + k] * A[ti(j) + k];
+    }
+    SYNC();
+  }
+}
+// Solve (L L^T) x = b; x holds b on entry (LDS).  Lane i keeps x_i in a register;
+// the dependent chain uses readlane broadcasts and no barriers.  n <= 64.
+__device__ __forceinline__ void wave_chol_solve(const float* A, float* x, int n) {
+  float xi = LANE < n ? x[LANE] : 0.f;
+  for (int k = 0; k < n; k++) {
+    float lik = LANE > k && LANE < n ? A[ti(LANE) + k] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[ti(k) + k];
+    if (LANE == k) xi = v;
+    xi -= lik * v;
+  }
+  for (int k = n - 1; k >= 0; k--) {
+    float lki = LANE < k ? A[ti(k) + LANE] : 0.f;
+    float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xi), k)) / A[ti(k) + k];
+    if (LANE == k) xi = v;
+    xi -= lki * v;
+  }
+  SYNC();
+  if (LANE < n) x[LANE] = xi;
+  SYNC();
+}
+
+// Cholesky solve for n <= 32 on the matrix cores.  The matrix, padded to 32 x 32 with
+// an identity block, lives in the 16 accumulator VGPRs of v_mfma_f32_32x32x2_f32
+// (lane l, VGPR v holds C[8 (v/4) + 4 (l/32) + v%4][l%32]; probe:
+// tools/probes/mfma_layout.hip).  Right-looking, two columns per step: rows k, k+1
+// are one VGPR pair in one half-wave, broadcast to both halves by v_permlane32_swap
+// (symmetry makes them the columns); the 2 x 2 diagonal block is factored from
+// three readlanes; the panel (L[:,k], L[:,k+1]) is the 32 x 2 A operand and its
+// transpose the B operand of ONE MFMA that applies the rank-2 update to the whole
+// trailing matrix.  16 steps instead of 32 columns of ~31 readlanes each.  The
+// substitutions then run on lane rows of L (lane i holds L[i][k] in Lr[k]) with
+// readlane/writelane; the backward one reads L's columns after an LDS transpose
+// through T (packed, may alias A).
+// A (+ hs*dadd on the diagonal, if dadd) -> x = A^-1 x.
+__device__ __forceinline__ float rl(float v, int k) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+// llvm.amdgcn.writelane (no clang builtin in this toolchain)
+extern "C" __device__ int dx_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ float wl(float v, float s, int k) {  // v with lane k := s
+  return __int_as_float(dx_writelane_i32(__float_as_int(s), k, __float_as_int(v)));
+}
+typedef float dx_f16v __attribute__((ext_vector_type(16)));
+// v with its lower (up = false) or upper (up = true) half-wave copied into both halves
+__device__ __forceinline__ float half_dup(float v, bool up) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(up ? r[1] : r[0]);
+}
+__device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const DXG float* dadd, float hs,
+                                                  float* x, float* T) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  dx_f16v C;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    const int ra = max(i, j), rb = min(i, j);
+    const bool in = i < n && j < n;
+    float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
+    if (dadd && i == j && in) e += hs * dadd[i];
+    C[v] = e;
+  }
+  float b = l < n ? x[l] : 0.f;
+  SYNC();  // A may alias T
+  float Lr[32];  // lane j: L[j][k], strictly below the diagonal
+  float dinv = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // C[k][j], C[k+1][j]
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
+    const float l21 = rl(rk1, k) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    dinv = wl(dinv, i11, k);
+    dinv = wl(dinv, i22, k + 1);
+    const float lk = rk * i11;                  // L[j][k]   (j > k)
+    const float lk1 = (rk1 - lk * l21) * i22;   // L[j][k+1] (j > k + 1)
+    Lr[k] = j > k ? lk : 0.f;
+    Lr[k + 1] = j > k + 1 ? lk1 : 0.f;
+    const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;  // panel: A[j][hi], B[hi][j]
+    C = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C, 0, 0, 0);
+  }
+  // strictly-lower row -> T (packed)
+  const int i = l;
+#pragma unroll
+  for (int k = 0; k < 32; k++)
+    if (k < i && i < n) T[ti(i) + k] = Lr[k];
+  // forward: L y = b
+  float y = 0.f;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    float yk = rl(b, k) * rl(dinv, k);
+    y = wl(y, yk, k);
+    b = fmaf(-Lr[k], yk, b);
+  }
+  SYNC();
+  // column i of L (below the diagonal) -> Lr; rows >= n of T are never written
+  const int ic = min(i, n - 1);
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    float v = T[ti(k) + ic];
+    Lr[k] = ic < k && k < n ? v : 0.f;
+  }
+  // backward: L^T x = y
+  float xo = 0.f;
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    float xk = rl(y, k) * rl(dinv, k);
+    xo = wl(xo, xk, k);
+    y = fmaf(-Lr[k], xk, y);
+  }
+  if (i < n) x[i] = xo;
+  SYNC();
+}

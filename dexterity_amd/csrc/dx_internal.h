@@ -164,3 +164,24 @@ int dx_spec_find(const DevModel& d, const Lds& L);
 hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);
+
+// dx_ik.hip: site Jacobians and batched damped-least-squares IK (host side).
+struct IkDev {
+  int mode;                  // 0: IK attempts (one wave per (env, attempt)); 1: site Jacobians
+  int nsite, njoint, max_steps, early_stop, nattempt, stop_on_first;
+  float tol, reg, gain, progress;
+  uint64_t seed;
+  int blk;                   // LDS word offset of the IK block (after the model's layout)
+  const int* sites;          // [nsite]
+  const int* joints;         // [njoint]
+  const float* targets;      // [nenv][nsite][3]
+  float* att_qpos;           // [nenv][nattempt][njoint]
+  float* att_err;            // [nenv][nattempt][nsite]
+  int* att_steps;            // [nenv][nattempt]
+  float *jacp, *jacr;        // mode 1: [nenv][nsite][3][nv] (either may be null)
+};
+int dx_ik_lds_words(const DevModel& d, int nsite);
+hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+                        const Lds& L, const IkDev& P);
+hipError_t dx_launch_ik_select(int nenv, hipStream_t stream, const DevModel& m, const IkDev& P, float* qpos_out,
+                               int* success, float* err_out, int* attempt_out, int* steps_out);

@@ -125,6 +125,17 @@ class BatchedPhysics:
     def set_watch(self, geom: int, body: int) -> None:
         _lib.check(_lib.load().dx_set_watch(self.ptr, geom, body))
 
+    def jac_site(self, sites, rotational: bool = True):
+        """mj_jacSite for every env at its current qpos (utils/mujoco_utils.py:38-73,
+        compute_object_6d_jacobian): (jacp, jacr) of shape [B, nsite, 3, nv]."""
+        s = np.ascontiguousarray(sites, dtype=np.int32).reshape(-1)
+        shape = (self.nenv, len(s), 3, self.model.nv)
+        jp = np.empty(shape, np.float32)
+        jr = np.empty(shape, np.float32) if rotational else None
+        _lib.check(_lib.load().dx_jac_site(self.ptr, s.ctypes.data, len(s), jp.ctypes.data,
+                                           None if jr is None else jr.ctypes.data))
+        return jp, jr
+
     def debug(self, enable: bool = True) -> None:
         _lib.check(_lib.load().dx_debug_enable(self.ptr, int(enable)))
 

@@ -185,6 +185,48 @@ int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
  * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */
 int dx_env_pack_outputs(dx_env* e, float* dst_dev);
 
+/* Kinematic queries and batched inverse kinematics ---------------------- */
+/* mj_jacSite (utils/mujoco_utils.py:67-73, compute_object_6d_jacobian) for every env
+ * at its current qpos (kinematics + com positions are recomputed first; the batch's
+ * state is not modified).  jacp / jacr: [nenv][nsite][3][nv] f32, host or device
+ * memory; either may be null. */
+int dx_jac_site(dx_batch* b, const int32_t* sites, int32_t nsite, float* jacp, float* jacr);
+
+/* IKSolver.solve (inverse_kinematics/ik_solver.py:71-167) for every env of a batch.
+ * Each attempt integrates damped-least-squares joint velocities
+ * (controllers/dls/dls.py:43-77: (J^T J + reg I) qdot = J^T twist, twist = gain *
+ * (target - site) / 1 s) with mj_integratePos over dt = 1 s, clips the solved
+ * joints to their range, and re-runs kinematics, for at most max_steps steps
+ * (ik_solver.py:169-236; early stop when every site is within linear_tol, abort
+ * when error / progress > progress_threshold for any site).  Attempt 0 starts the
+ * solved joints at their midrange, attempt a > 0 uniformly within their range
+ * (counter-based RNG keyed by (seed, env, a); the reference draws from numpy's
+ * global stream, so individual random starts are not seed-identical); the other
+ * qpos entries come from the batch.  The attempts run in parallel, one wavefront
+ * each; the selection follows ik_solver.py:132-152: among attempts with every
+ * error <= linear_tol, the first one (stop_on_first_successful_attempt) or the one
+ * closest to the midrange (first on ties).  3 * nsite <= 32, njoint <= 64. */
+typedef struct dx_ik_options {
+  float linear_tol;          /* 1e-3  (ik_solver.py:73)                 */
+  float regularization;      /* 1e-5  (_REGULARIZATION_WEIGHT, :24)     */
+  float gain;                /* 0.95  (_LINEAR_VELOCITY_GAIN, :18)      */
+  float progress_threshold;  /* 20    (_PROGRESS_THRESHOLD, :29)        */
+  int32_t max_steps;         /* 100                                     */
+  int32_t early_stop;        /* 0                                       */
+  int32_t num_attempts;      /* 30                                      */
+  int32_t stop_on_first;     /* 0 (stop_on_first_successful_attempt)    */
+  uint64_t seed;
+} dx_ik_options;
+/* targets [nenv][nsite][3]; outputs (host or device memory, any may be null):
+ * qpos_out [nenv][njoint] (the selected attempt's solved joints; when no attempt
+ * succeeded -- the reference returns None -- the last attempt's), success [nenv]
+ * (int32 0/1), linear_err [nenv][nsite] (of the returned joints), attempt [nenv]
+ * (int32 index of the returned attempt), steps [nenv] (int32 integration steps it
+ * took). */
+int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t* sites, int32_t nsite,
+                const int32_t* joints, int32_t njoint, const float* targets, float* qpos_out,
+                int32_t* success, float* linear_err, int32_t* attempt, int32_t* steps);
+
 /* Timing ---------------------------------------------------------------- */
 /* When enabled, HIP events bracket every step-kernel launch on the batch stream;
  * dx_timing_read syncs, returns the summed kernel time and launch count, and clears. */

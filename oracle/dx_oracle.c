@@ -1602,6 +1602,102 @@ int dxo_kinematics(const dxo_model* m, dxo_data* d) {
   return 0;
 }
 
+/* ------------------------------------------------------------------------ */
+/* kinematic queries and IK (inverse_kinematics/ik_solver.py, controllers/dls)  */
+/* ------------------------------------------------------------------------ */
+int dxo_fk(const dxo_model* m, dxo_data* d) {
+  kinematics(m, d);
+  com_pos(m, d);
+  return 0;
+}
+
+/* mj_jacSite (utils/mujoco_utils.py:67-73): [3][nv] each, after dxo_fk */
+void dxo_jac_site(const dxo_model* m, const dxo_data* d, int site, double* jacp, double* jacr) {
+  jac_point(m, d, m->site_bodyid[site], d->site_xpos + 3 * site, jacp, jacr);
+}
+
+/* One IKSolver._solve_ik attempt (ik_solver.py:169-236) from d->qpos: DLS joint
+ * velocities (dls.py:43-77, (J^T J + reg I) qdot = J^T twist, solved densely as the
+ * reference does), mj_integratePos over 1 s, clip of the solved joints to their
+ * range, mj_normalizeQuat, mj_kinematics + mj_comPos (ik_solver.py:238-250).
+ * opts = {linear_tol, regularization, gain, progress_threshold}.  Returns the steps
+ * taken; err_out[nsite] = the last step's linear errors. */
+int dxo_ik_attempt(const dxo_model* m, dxo_data* d, int nsite, const int* sites, int njoint, const int* joints,
+                   const double* targets, const double* opts, int max_steps, int early_stop, double* err_out) {
+  const int nv = m->nv, nr = 3 * nsite;
+  double* J = (double*)calloc((size_t)nr * nv, 8);
+  double* H = (double*)calloc((size_t)nv * nv, 8);
+  double* jp = (double*)calloc(3 * (size_t)nv, 8);
+  double* rhs = (double*)calloc(nv, 8);
+  double* qd = (double*)calloc(nv, 8);
+  double* prev = (double*)calloc(nr, 8);
+  double* tw = (double*)calloc(nr, 8);
+  double fl = 0;
+  dxo_fk(m, d);
+  for (int s = 0; s < nsite; s++) memcpy(prev + 3 * s, d->site_xpos + 3 * sites[s], 24);
+  int it = 0;
+  while (it < max_steps) {
+    for (int s = 0; s < nsite; s++)
+      for (int e = 0; e < 3; e++) tw[3 * s + e] = opts[2] * (targets[3 * s + e] - d->site_xpos[3 * sites[s] + e]) / 1.0;
+    for (int s = 0; s < nsite; s++) {
+      dxo_jac_site(m, d, sites[s], jp, NULL);
+      memcpy(J + (size_t)3 * s * nv, jp, 24 * (size_t)nv);
+    }
+    for (int i = 0; i < nv; i++) {
+      for (int j = 0; j < nv; j++) {
+        double v = 0;
+        for (int r = 0; r < nr; r++) v += J[r * nv + i] * J[r * nv + j];
+        H[i * nv + j] = v + (i == j ? opts[1] : 0.0);
+      }
+      double v = 0;
+      for (int r = 0; r < nr; r++) v += J[r * nv + i] * tw[r];
+      rhs[i] = v;
+    }
+    cholesky(H, H, nv, &fl);
+    chol_solve(H, qd, rhs, nv, &fl);
+    /* mj_integratePos(qpos, qd, 1) */
+    for (int j = 0; j < m->njnt; j++) {
+      int qa = m->jnt_qposadr[j], da = m->jnt_dofadr[j];
+      if (m->jnt_type[j] == JNT_FREE) {
+        for (int k = 0; k < 3; k++) d->qpos[qa + k] += qd[da + k];
+        double* q = d->qpos + qa + 3;
+        const double* w = qd + da + 3;
+        double wn = norm3(w);
+        if (wn > MINVAL) {
+          double sn = sin(0.5 * wn);
+          double dq[4] = {cos(0.5 * wn), w[0] / wn * sn, w[1] / wn * sn, w[2] / wn * sn};
+          quatmul(q, q, dq);
+        }
+        quatnorm(q);
+      } else {
+        d->qpos[qa] += qd[da];
+      }
+    }
+    for (int k = 0; k < njoint; k++) {
+      int j = joints[k], qa = m->jnt_qposadr[j];
+      double lo = m->jnt_range[2 * j], hi = m->jnt_range[2 * j + 1];
+      d->qpos[qa] = d->qpos[qa] < lo ? lo : d->qpos[qa] > hi ? hi : d->qpos[qa];
+    }
+    dxo_fk(m, d);
+    it++;
+    int close = 1, stuck = 0;
+    for (int s = 0; s < nsite; s++) {
+      const double* p = d->site_xpos + 3 * sites[s];
+      double e[3], c[3];
+      sub3(e, targets + 3 * s, p);
+      sub3(c, p, prev + 3 * s);
+      double err = norm3(e), chg = norm3(c);
+      err_out[s] = err;
+      if (err > opts[0]) close = 0;
+      if (err / (chg + 1e-10) > opts[3]) stuck = 1;
+      memcpy(prev + 3 * s, p, 24);
+    }
+    if ((early_stop && close) || stuck) break;
+  }
+  free(J); free(H); free(jp); free(rhs); free(qd); free(prev); free(tw);
+  return it;
+}
+
 double* dxo_field(dxo_data* d, const char* name, int* len) {
   const dxo_model* m = d->model;
   int nv = m->nv, nb = m->nbody;

@@ -53,6 +53,16 @@ int dxo_step(const dxo_model* m, dxo_data* d);
 /* Position-only pass (kinematics + collision), as used for observations. */
 int dxo_kinematics(const dxo_model* m, dxo_data* d);
 
+/* mj_kinematics + mj_comPos (no collision). */
+int dxo_fk(const dxo_model* m, dxo_data* d);
+/* mj_jacSite after dxo_fk: jacp / jacr [3][nv] (either may be NULL). */
+void dxo_jac_site(const dxo_model* m, const dxo_data* d, int site, double* jacp, double* jacr);
+/* One IKSolver._solve_ik attempt from d->qpos (ik_solver.py:169-250, dls.py:43-77).
+ * opts = {linear_tol, regularization, gain, progress_threshold}; returns the steps
+ * taken, err_out[nsite] = last linear errors; d->qpos holds the result. */
+int dxo_ik_attempt(const dxo_model* m, dxo_data* d, int nsite, const int* sites, int njoint, const int* joints,
+                   const double* targets, const double* opts, int max_steps, int early_stop, double* err_out);
+
 /* Field access: returns a pointer to the named double array and its length.
  * Names: qpos qvel ctrl qacc qacc_warmstart qacc_smooth qfrc_bias qfrc_passive
  * qfrc_actuator qfrc_applied qfrc_smooth qfrc_constraint xfrc_applied xpos xquat

@@ -56,6 +56,11 @@ def lib():
         L.dxo_flops_reset.argtypes = [vp]
         L.dxo_batch_step.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip]
         L.dxo_batch_step.restype = ip
+        L.dxo_fk.argtypes = [vp, vp]
+        L.dxo_fk.restype = ip
+        L.dxo_jac_site.argtypes = [vp, vp, ip, dp, dp]
+        L.dxo_ik_attempt.argtypes = [vp, vp, ip, vp, ip, vp, dp, dp, ip, ip, dp]
+        L.dxo_ik_attempt.restype = ip
         _lib = L
     return _lib
 
@@ -130,6 +135,31 @@ class OracleData:
             lib().dxo_contact(self.ptr, i, buf)
             out[i] = np.frombuffer(buf, dtype=np.float64)
         return out
+
+    def fk(self):
+        return lib().dxo_fk(self.model.ptr, self.ptr)
+
+    def jac_site(self, site: int):
+        """mj_jacSite after fk(): (jacp [3, nv], jacr [3, nv])."""
+        nv = self.qvel.shape[0]
+        jp, jr = np.zeros((3, nv)), np.zeros((3, nv))
+        dp = ctypes.POINTER(ctypes.c_double)
+        lib().dxo_jac_site(self.model.ptr, self.ptr, site, jp.ctypes.data_as(dp), jr.ctypes.data_as(dp))
+        return jp, jr
+
+    def ik_attempt(self, sites, joints, targets, linear_tol=1e-3, regularization=1e-5, gain=0.95,
+                   progress_threshold=20.0, max_steps=100, early_stop=False):
+        """One IKSolver._solve_ik attempt from the current qpos; returns (steps, errors)."""
+        s = np.ascontiguousarray(sites, dtype=np.int32)
+        j = np.ascontiguousarray(joints, dtype=np.int32)
+        t = np.ascontiguousarray(targets, dtype=np.float64).reshape(-1)
+        o = np.array([linear_tol, regularization, gain, progress_threshold], dtype=np.float64)
+        err = np.zeros(len(s))
+        dp = ctypes.POINTER(ctypes.c_double)
+        steps = lib().dxo_ik_attempt(self.model.ptr, self.ptr, len(s), s.ctypes.data, len(j), j.ctypes.data,
+                                     t.ctypes.data_as(dp), o.ctypes.data_as(dp), max_steps, int(early_stop),
+                                     err.ctypes.data_as(dp))
+        return steps, err
 
     def flops(self) -> np.ndarray:
         buf = (ctypes.c_double * NSTAGE)()
