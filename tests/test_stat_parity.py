@@ -1,0 +1,107 @@
+"""Contact-rich statistical parity: GPU fp32 vs fp64 oracle.
+
+Cube reorientation with a random agent is chaotic: fp32 and fp64 trajectories from the
+same state separate within a fraction of a second once the cube tumbles between the
+fingers, so per-env long-horizon agreement is not a meaningful bar.  What the task
+cares about is the distribution of outcomes, so 1,024 episodes run on both sides from
+identical initial states (hand at qpos0, cube placed per reorient.py:72-78 with a
+uniform random orientation, seed 12345) under identical random actions (uniform in
+ctrlrange, manipulation_test.py:44-45) for 40 control steps (1 s, 200 substeps), and:
+
+  * per env, the first control step (before chaos) agrees: median |qpos| error
+    <= 1e-4, 95th percentile <= 1e-2;
+  * the fall rate (cube below 5 cm, i.e. on the ground, reorient.py:229-235) at every
+    control step agrees within 4 binomial standard errors of a difference of two
+    independent samples (the samples are paired and positively correlated, so this
+    is conservative) plus 0.01;
+  * the mean shaped reward (reorient.py:238-284, against a random goal per env)
+    over all steps agrees within 4 standard errors plus 1 %;
+  * the final distance-to-goal distributions (the quantity the reward shapes) pass a
+    two-sample KS test at p > 1e-3.  (Not the cube height: half the cubes rest on
+    the ground, a point mass at z = 2 cm whose sub-micron offset between a solver
+    stopped at fp32 tolerance and one at 1e-8 dominates a KS statistic.)
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from dexterity_amd import _lib, blob
+from dexterity_amd.mjcf.compiler import CompiledModel
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+N_EP = 1024
+N_STEP = 40
+FALL_Z = 0.05
+
+
+def _rewards(task_ref, goals, qpos, ctrl):
+    return np.array([task_ref.reorient_reward(task_ref.goal_distance(goals[e], qpos[e, 27:31]), ctrl[e])
+                     for e in range(len(goals))])
+
+
+def test_reorient_outcome_statistics(oracle_mod):
+    from dexterity_amd import build, physics
+    from oracle import task_ref
+
+    build.build()
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "shadow_reorient.npz"))
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    xfrc = physics.gravity_compensation(cm, "shadow_hand_e/")
+    rs = np.random.RandomState(12345)
+    qpos = np.tile(cm.qpos0, (N_EP, 1))
+    qpos[:, 24:27] = rs.uniform([-0.025, -0.155, 0.16], [0.025, -0.105, 0.16], size=(N_EP, 3))
+    qpos[:, 27:31] = np.stack([task_ref.uniform_quaternion(rs) for _ in range(N_EP)])
+    goals = np.stack([task_ref.uniform_quaternion(rs) for _ in range(N_EP)])
+    lo, hi = cm.actuator_ctrlrange.T
+    ctrls = rs.uniform(lo, hi, size=(N_STEP, N_EP, cm.nu))
+    # the GPU works in fp32: both sides start from the same fp32-representable state
+    qpos = qpos.astype(np.float32).astype(np.float64)
+    ctrls = ctrls.astype(np.float32).astype(np.float64)
+
+    phys = physics.BatchedPhysics(physics.Model(cm), N_EP)
+    phys.set_xfrc(xfrc)
+    phys.set(_lib.QPOS, qpos)
+    q_o, v_o, w_o = qpos.copy(), np.zeros((N_EP, cm.nv)), np.zeros((N_EP, cm.nv))
+    z_g, z_o, r_g, r_o = [], [], [], []
+    for k in range(N_STEP):
+        phys.set(_lib.CTRL, ctrls[k])
+        phys.step(5)
+        q_g = phys.qpos.astype(np.float64)
+        rc, q_o, v_o, w_o = oracle_mod.batch_step(om, q_o, v_o, ctrls[k], w_o, xfrc, 5)
+        assert rc == 0 and np.isfinite(q_g).all()
+        if k == 0:
+            err = np.abs(q_g - q_o).max(axis=1)
+            print(f"step 1 |qpos| error: median {np.median(err):.2e}, p95 {np.percentile(err, 95):.2e}")
+            assert np.median(err) <= 1e-4 and np.percentile(err, 95) <= 1e-2
+        z_g.append(q_g[:, 26])
+        z_o.append(q_o[:, 26].copy())
+        r_g.append(_rewards(task_ref, goals, q_g, ctrls[k]))
+        r_o.append(_rewards(task_ref, goals, q_o, ctrls[k]))
+    phys.close()
+    z_g, z_o, r_g, r_o = map(np.array, (z_g, z_o, r_g, r_o))
+    f_g, f_o = (z_g < FALL_Z).mean(axis=1), (z_o < FALL_Z).mean(axis=1)
+    p = 0.5 * (f_g + f_o)
+    se = np.sqrt(2 * p * (1 - p) / N_EP)
+    print("fall rate gpu   ", np.round(f_g[4::5], 3))
+    print("fall rate oracle", np.round(f_o[4::5], 3))
+    assert np.all(np.abs(f_g - f_o) <= 4 * se + 0.01), np.abs(f_g - f_o).max()
+    agree = ((z_g[-1] < FALL_Z) == (z_o[-1] < FALL_Z)).mean()
+    print(f"per-episode fall verdict agreement at 1 s: {agree:.3f}")
+    m_g, m_o = r_g.mean(), r_o.mean()
+    # standard error of the per-episode mean reward (episodes independent)
+    se_r = np.sqrt(r_g.mean(axis=0).var() / N_EP + r_o.mean(axis=0).var() / N_EP)
+    print(f"mean shaped reward gpu {m_g:.4f} oracle {m_o:.4f} (se {se_r:.4f})")
+    assert abs(m_g - m_o) <= 4 * se_r + 0.01 * abs(m_o)
+    from scipy.stats import ks_2samp
+
+    fell_g, fell_o = z_g[-1] < FALL_Z, z_o[-1] < FALL_Z
+    print(f"resting height: gpu {np.median(z_g[-1][fell_g]):.7f} oracle {np.median(z_o[-1][fell_o]):.7f}")
+    d_g = np.array([task_ref.goal_distance(goals[e], q_g[e, 27:31]) for e in range(N_EP)])
+    d_o = np.array([task_ref.goal_distance(goals[e], q_o[e, 27:31]) for e in range(N_EP)])
+    ks = ks_2samp(d_g, d_o)
+    print(f"final goal distance KS p = {ks.pvalue:.3f}")
+    assert ks.pvalue > 1e-3
