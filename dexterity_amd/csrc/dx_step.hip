@@ -873,9 +873,9 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   if (LANE == 0) I[I_NCAND] = ng;
   SYNC();
   stage_mark(c, ST_MID);
-  // 3. narrowphase.  Candidate q belongs to 16-lane group q % 4 (static round robin)
-  // and every group walks its own candidates in this one loop, so a group never
-  // waits for another group's pair.  Contacts are written unordered together with
+  // 3. narrowphase.  Four 16-lane groups walk the candidate list in this one loop,
+  // each taking the next unassigned candidate when its pair is done, so a group
+  // never waits for another group's pair.  Contacts are written unordered together with
   // their key (candidate, rank) and put into candidate order below, which gives the
   // list of the serial loop.
   float* con = c.f(c.L.con);
@@ -883,7 +883,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   NpStats st = {0, 0, 0, 0, 0, 0, 0};
   {
     const int grp = LANE >> 4;
-    int q = grp;
+    int q = grp, next = 4;
     bool fresh = true;
     int gp = 0;
     float margin = 0;
@@ -949,10 +949,15 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
         con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
       }
       ncon += c0 + c1 + c2 + c3;
+      // a group that finished its pair takes the next unassigned candidate (in group
+      // order), so a long MPR on one group no longer holds back the others' queues;
+      // the contact keys still sort the list into candidate order below
+      const uint64_t fin = __ballot(done && SL == 0);
       if (done) {
-        q += 4;
+        q = next + __popcll(fin & ((1ull << (LANE & 48)) - 1ull));
         fresh = true;
       }
+      next += __popcll(fin);
     }
   }
   SYNC();
