@@ -15,8 +15,8 @@ LIB_PATH = os.environ.get("DX_LIB") or os.path.join(_HERE, "libdx.so")  # DX_LIB
 
 # dx_field
 QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
-SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND = 6, 7, 8, 9, 10, 11, 12, 13
-INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND)
+SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST = 6, 7, 8, 9, 10, 11, 12, 13, 14
+INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST)
 
 EXPORTS = (
     "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_model_lds_bytes", "dx_field_width",
@@ -34,7 +34,8 @@ STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constra
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
           "qfrc_constraint", "euler", "observe", "io", "matvec", "np_mpr", "jacvec")
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
-            26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc"}
+            26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc",
+            31: "np_trips"}
 NSTAGE = 32
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES = range(7)
 TASK_REORIENT, TASK_REACH = 0, 1

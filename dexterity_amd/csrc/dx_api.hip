@@ -563,7 +563,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, B0 + r4(ntri));
   L.cand_max = 768;
   L.cand = B0;
-  end = std::max(end, L.cand + L.cand_max + 4 * 36);  // + MPR portal points of the 4 groups
+  // + MPR portal points of the 4 groups, then the candidates' pair records (float4
+  // per narrowphase candidate slot: cand_max - 2 * (cand_max / 3) of them)
+  end = std::max(end, L.cand + L.cand_max + 4 * 36 + 4 * (L.cand_max - 2 * (L.cand_max / 3)));
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_jar = take(L.nefc_max); L.efc_jv = take(L.nefc_max);
@@ -681,7 +683,7 @@ extern "C" int dx_field_width(const dx_model* m, int field) {
     case DX_QPOS: return d.nq;
     case DX_QVEL: case DX_QACC_WARMSTART: case DX_QACC: return d.nv;
     case DX_CTRL: return d.nu;
-    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: case DX_NCAND: return 1;
+    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: case DX_NCAND: case DX_STEP_COST: return 1;
     case DX_SITE_XPOS: return 3 * d.nsite;
     case DX_SITE_VEL: return 6 * d.nsite;
     case DX_XPOS: return 3 * d.nbody;
@@ -762,6 +764,8 @@ struct dx_batch {
   DevModel dm;
   DevBatch db;
   int spec;  // specialized step kernel (dx_specs.inc) or -1 for the generic one
+  bool queue;  // mode-0 steps through the substep queue
+  int slots;   // persistent workgroups of a queued launch
   float* xfrc;
   std::vector<void*> allocs;
   bool debug;
@@ -824,6 +828,18 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
     B.order = (const int*)po;
   }
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
+  // substep queue state (DX_NO_QUEUE=1: one workgroup per env for the whole step)
+  b->queue = !getenv("DX_NO_QUEUE");
+  rc |= balloc(b, (void**)&B.qhead, 4);
+  rc |= balloc(b, (void**)&B.progress, E * 4);
+  rc |= balloc(b, (void**)&B.qerr, 4);
+  B.epoch = 0;
+  B.qbase = 0;
+  {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
+    b->slots = ncu * 8;  // resident 64-lane workgroups of the step kernel (2 waves per SIMD)
+  }
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
   if (B.order && dx_launch_order(nenv, b->stream, B.cost, (int*)B.order) != hipSuccess) {  // a permutation
@@ -874,6 +890,7 @@ static void* field_base(dx_batch* b, int field) {
     case DX_GROUND_CONTACT: return B.watch;
     case DX_NITER: return B.niter;
     case DX_NCAND: return B.ncand;
+    case DX_STEP_COST: return B.cost;
   }
   return nullptr;
 }
@@ -943,10 +960,23 @@ static void timing_end(dx_batch* b, hipEvent_t start);
 static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
+  const bool queued = mode == 0 && b->queue && nsub < 32;
+  const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots) : b->nenv;
+  if (queued) {
+    // substep queue: a new progress epoch; the task counter is never reset -- this
+    // launch's tasks are the claims qbase .. qbase + ntask - 1 (mod 2^32)
+    DevBatch& B = b->db;
+    if (++B.epoch >= (1u << 26)) {  // tags wrap: start over from zeroed progress
+      HIPCHK(hipMemsetAsync(B.progress, 0, (size_t)b->nenv * 4, b->stream));
+      B.epoch = 1;
+    }
+  }
   hipEvent_t t0;
   timing_begin(b, &t0);
-  hipError_t e = dx_launch_step(b->spec, b->nenv, lds, b->stream, b->dm, b->db, b->model->lds, nsub, mode);
+  hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
+  // every workgroup of a queued launch makes exactly one claim past the last task
+  if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
   HIPCHK(e);
   // next launch: heaviest environments first (costs just measured)
   if (mode == 0 && b->db.order) HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order));
@@ -1122,8 +1152,15 @@ extern "C" int dx_debug_enable(dx_batch* b, int enable) {
 
 extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats) {
   if (!b || !name || !dst) return fail(DX_EINVAL, "null argument");
-  if (!b->debug) return fail(DX_EINVAL, "debug not enabled");
   DevBatch& B = b->db;
+  if (std::string(name) == "queue_timeouts") {  // int32 bits: 1 if a queued task ever gave up waiting
+    if (nfloats < 1) return fail(DX_EINVAL, "destination too small");
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipMemcpyAsync(dst, B.qerr, 4, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return 0;
+  }
+  if (!b->debug) return fail(DX_EINVAL, "debug not enabled");
   size_t E = b->nenv, nv = b->dm.nv;
   const void* src = nullptr;
   size_t n = 0;
@@ -1447,6 +1484,10 @@ extern "C" int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n) {
   HIPCHK(hipMemcpyAsync(h.data(), b->db.stage_acc, cnt * 8, hipMemcpyDeviceToHost, b->stream));
   HIPCHK(hipMemsetAsync(b->db.stage_acc, 0, cnt * 8, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
+  if ((size_t)n >= cnt) {  // per env: out[env][DX_NSTAGE]
+    memcpy(out, h.data(), cnt * 8);
+    return 0;
+  }
   for (int k = 0; k < std::min(n, DX_NSTAGE); k++) {
     uint64_t t = 0;
     for (int e = 0; e < b->nenv; e++) t += h[(size_t)e * DX_NSTAGE + k];

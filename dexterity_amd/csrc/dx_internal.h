@@ -100,6 +100,13 @@ struct DevBatch {
   unsigned* cost;                 // [nenv] shader cycles / 1024 of the env's last step, or null
   const TaskParams* tp;           // device copies, reach sampling pass only (mode 2)
   const TaskState* ts;
+  // substep queue (mode 3, dx_step.hip step_queue): task counter, per-env progress
+  // tags (epoch * 32 + substeps done), launch epoch, the
+  // counter value of this launch's first task, timeout mark
+  unsigned* qhead;
+  unsigned* progress;
+  unsigned epoch, qbase;
+  int* qerr;
 };
 #define DX_NSTAGE 32
 
@@ -161,7 +168,7 @@ __device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, i
 
 // dx_step.hip: specialized-kernel lookup and launch (host side)
 int dx_spec_find(const DevModel& d, const Lds& L);
-hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);
 

@@ -813,12 +813,16 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   // 2. flattened geom-pair mid-phase: lane t -> (body pair q, geom pair) by binary search
   int* gcand = pref + half;
   int gmax = cmax - 2 * half;
+  // pair records of the surviving candidates, after the four groups' portal points
+  // (dx_api.hip layout reserves 4 * gmax words there)
+  float4* gcrec = (float4*)(c.f(c.L.cand + c.L.cand_max) + 4 * MP_WORDS);
   int ng = 0;
   int total = nbc > 0 ? pref[nbc] : 0;
   for (int base = 0; base < total; base += DX_WAVE) {
     int t = base + LANE;
     bool keep = false;
     int gp = -1;
+    float4 prec = make_float4(0.f, 0.f, 0.f, 0.f);
     if (t < total) {
       int lo = 0, hi = nbc;  // pref[lo] <= t < pref[hi]
       while (hi - lo > 1) {
@@ -827,6 +831,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
       }
       gp = cand[lo] + (t - pref[lo]);
       float4 pr = m.gpair_rec[gp];
+      prec = pr;
       int g1 = __float_as_int(pr.x), g2 = __float_as_int(pr.y);
       keep = !watch_only || g1 == wg || g2 == wg;
       if (keep) {
@@ -863,7 +868,10 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     }
     uint64_t mask = __ballot(keep);
     int pos = __popcll(mask & ((1ull << LANE) - 1ull));
-    if (keep && ng + pos < gmax) gcand[ng + pos] = gp;
+    if (keep && ng + pos < gmax) {
+      gcand[ng + pos] = gp;
+      gcrec[ng + pos] = prec;  // the narrowphase reads the pair record from LDS
+    }
     ng += __popcll(mask);
   }
   if (ng > gmax) {
@@ -894,6 +902,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     for (;;) {
       bool act = q < ng;
       if (__ballot(act) == 0) break;
+      stage_count(c, CNT_NP_TRIPS);
       NpOut o;
       o.wr = false;
       o.rank = 0;
@@ -903,7 +912,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
         bool stepping = !fresh;
         if (fresh) {
           gp = gcand[q];
-          float4 pr = m.gpair_rec[gp];
+          const float4 pr = gcrec[q];
           if (__float_as_int(pr.w)) {
             cnt = narrowphase_prim(c, gp, o, st);
             done = true;
@@ -2107,27 +2116,20 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
 // ------------------------------------------------------------------------ //
 // kernels
 // ------------------------------------------------------------------------ //
-// mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
-template <class SP>
-__device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode) {
-  extern __shared__ float smem[];
-  if ((int)blockIdx.x >= B.nenv) return;
-  // longest-first dispatch: the order kernel sorts envs by their last step's cost
-  int env = B.order ? B.order[blockIdx.x] : (int)blockIdx.x;
-  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-  if (mode == 2 && !B.ts->need[env]) return;
-  CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
+// Per-env pieces shared by the launch-per-env kernel and the substep queue.
+// env_begin: zero the env's LDS block, load its state; returns its time.
+template <class Ctx>
+__device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env) {
   const Lds& L = c.L;
-  int* I = (int*)(smem + L.ints);
-  c.I = I;
-  c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
-  // Zero the whole per-env LDS block once: the Cholesky solve reads a few words past
-  // its packed triangles (padding lanes/columns, multiplied by exact zeros), and
-  // those must be finite rather than whatever an earlier workgroup left behind.
+  float* smem = c.S;
+  // Zero the whole per-env LDS block: the Cholesky solve reads a few words past its
+  // packed triangles (padding lanes/columns, multiplied by exact zeros), and those
+  // must be finite rather than whatever an earlier workgroup left behind.
 #ifndef DX_SKIP_LDS_ZERO  // (defined only by the test that shows why this is needed)
   for (int k = LANE; k < L.total; k += DX_WAVE) smem[k] = 0.f;
 #endif
   SYNC();
+  int* I = c.I;
   if (c.stage_acc && LANE == 0) *(unsigned long long*)(I + 10) = __builtin_amdgcn_s_memtime();
   float* qpos = c.f(L.qpos);
   float* qvel = c.f(L.qvel);
@@ -2151,30 +2153,41 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
       tri[t] = (unsigned short)((i << 8) | (t - i * (i + 1) / 2));
     }
   }
-  float time = B.time[env];
+  const float time = B.time[env];
   SYNC();
-  if (mode == 2) {  // reach sampling pass: new state only, no outputs
-    reach_prep(c, B, env, time);
-    for (int i = LANE; i < c.nq; i += DX_WAVE) B.qpos[(size_t)env * c.nq + i] = qpos[i];
-    for (int i = LANE; i < c.nv; i += DX_WAVE) {
-      B.qvel[(size_t)env * c.nv + i] = qvel[i];
-      B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
-    }
-    if (LANE == 0) B.time[env] = time;
-    return;
+  return time;
+}
+
+template <class Ctx>
+__device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B, int env, float time) {
+  const float* qpos = c.f(c.L.qpos);
+  const float* qvel = c.f(c.L.qvel);
+  const float* ws = c.f(c.L.v5);
+  for (int i = LANE; i < c.nq; i += DX_WAVE) B.qpos[(size_t)env * c.nq + i] = qpos[i];
+  for (int i = LANE; i < c.nv; i += DX_WAVE) {
+    B.qvel[(size_t)env * c.nv + i] = qvel[i];
+    B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
   }
-  int steps = mode == 0 ? nsub : 1;
-  if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
-  for (int s = 0; s < steps; s++) {
-    forward(c, B.xfrc);
-    if (mode == 0) {
-      // warmstart <- solved qacc
-      for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(L.qacc)[i];
-      SYNC();
-      euler(c, &time);
-    }
-  }
-  // debug record of the last forward
+  if (LANE == 0) B.time[env] = time;
+}
+
+// One physics step (mj_step): forward, warm start <- solved qacc, Euler.
+template <class Ctx>
+__device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time) {
+  forward(c, B.xfrc);
+  float* ws = c.f(c.L.v5);
+  for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
+  SYNC();
+  euler(c, &time);
+}
+
+// After the last substep (or a forward): debug record, per-env outputs, the
+// observation pass at the new state, and the state itself.
+template <class Ctx>
+__device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int env, float time) {
+  const DevModel& m = c.m;
+  const Lds& L = c.L;
+  int* I = c.I;
   if (B.dbg_qacc_smooth) {
     for (int i = LANE; i < c.nv; i += DX_WAVE) {
       B.dbg_qacc_smooth[(size_t)env * c.nv + i] = c.f(L.qacc_smooth)[i];
@@ -2210,19 +2223,103 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   stage_mark(c, ST_IO);
   observe(c, B, env);
   stage_mark(c, ST_OBSERVE);
-  for (int i = LANE; i < c.nq; i += DX_WAVE) B.qpos[(size_t)env * c.nq + i] = qpos[i];
-  for (int i = LANE; i < c.nv; i += DX_WAVE) {
-    B.qvel[(size_t)env * c.nv + i] = qvel[i];
-    B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
+  env_store_state(c, B, env, time);
+}
+
+// mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
+// mode 2: reach sampling pass (goal rollouts / joint sampling), state out only
+template <class SP>
+__device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode) {
+  extern __shared__ float smem[];
+  if ((int)blockIdx.x >= B.nenv) return;
+  // longest-first dispatch: the order kernel sorts envs by their last step's cost
+  int env = B.order ? B.order[blockIdx.x] : (int)blockIdx.x;
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+  if (mode == 2 && !B.ts->need[env]) return;
+  CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
+  c.I = (int*)(smem + c.L.ints);
+  c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
+  float time = env_begin(c, B, env);
+  if (mode == 2) {  // reach sampling pass: new state only, no outputs
+    reach_prep(c, B, env, time);
+    env_store_state(c, B, env, time);
+    return;
   }
-  if (LANE == 0) B.time[env] = time;
+  int steps = mode == 0 ? nsub : 1;
+  if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
+  for (int s = 0; s < steps; s++) {
+    if (mode == 0) env_substep(c, B, time);
+    else forward(c, B.xfrc);
+  }
+  env_finish(c, B, env, time);
   if (LANE == 0 && B.cost && mode == 0)
     B.cost[env] = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
 }
 
+// Substep queue (mode 0): one task = one physics step of one environment, claimed in
+// order from a device counter -- substep s of every env (longest-first within the
+// round) before substep s + 1 of any.  The env's state moves through HBM between
+// its tasks (~0.5 KB + its separating-direction cache), so the wave slots stay
+// busy until the last round instead of idling behind the few environments whose
+// control step is 2-3x the mean (a whole control step per workgroup left most of
+// the second round's slots waiting on them).  Task (s, e) waits for (s - 1, e),
+// which was claimed earlier by a running workgroup, so the wait always ends; it is
+// bounded anyway (B.qerr records a timeout).  Hand-off: plain stores, vmcnt(0),
+// agent release, vmcnt(0), relaxed agent flag store; the consumer polls relaxed,
+// then agent acquire + vmcnt(0) before its plain loads (MI355X_MICROARCH.md,
+// inter-workgroup visibility).
+__device__ __forceinline__ unsigned qtag(unsigned epoch, int s) { return epoch * 32u + (unsigned)s; }
+
+template <class SP>
+__device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub) {
+  extern __shared__ float smem[];
+  CtxT<SP> c(m, Lrt, smem, nullptr, nullptr);
+  c.I = (int*)(smem + c.L.ints);
+  const unsigned ntask = (unsigned)B.nenv * (unsigned)nsub;
+  for (;;) {
+    unsigned t = 0;
+    if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - B.qbase;
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= ntask) break;
+    const int s = (int)(t / (unsigned)B.nenv);
+    const int k = (int)(t - (unsigned)s * (unsigned)B.nenv);
+    const int env = B.order ? B.order[k] : k;
+    if (s > 0) {
+      if (LANE == 0) {
+        unsigned n = 0;
+        while (__hip_atomic_load(B.progress + env, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != qtag(B.epoch, s)) {
+          __builtin_amdgcn_s_sleep(2);
+          if (++n > (1u << 25)) {  // ~seconds: never expected; leave a mark and go on
+            __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    c.stage_acc = B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr;
+    c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
+    float time = env_begin(c, B, env);
+    if (!(B.skip && B.skip[env])) env_substep(c, B, time);  // a freshly reset env is only observed
+    if (s == nsub - 1) env_finish(c, B, env, time);
+    else env_store_state(c, B, env, time);
+    if (LANE == 0 && B.cost) {
+      const unsigned dt = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+      B.cost[env] = s == 0 ? dt : B.cost[env] + dt;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (LANE == 0) __hip_atomic_store(B.progress + env, qtag(B.epoch, s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
-  step_body<SpecRT>(m, B, L, nsub, mode);
+  if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
+  else step_body<SpecRT>(m, B, L, nsub, mode);
 }
 
 // ------------------------------------------------------------------------ //
@@ -2238,7 +2335,8 @@ dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
 template <class SP>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 dx_step_kernel_spec(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
-  step_body<SP>(m, B, L, nsub, mode);
+  if (mode == 3) step_queue<SP>(m, B, L, nsub);
+  else step_body<SP>(m, B, L, nsub, mode);
 }
 
 template <class SP>
@@ -2285,19 +2383,19 @@ hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, i
   return hipGetLastError();
 }
 
-hipError_t dx_launch_step(int spec, int nenv, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
                           const Lds& L, int nsub, int mode) {
   int k = 0;
 #define DX_LAUNCH(SP)                                                                                   \
   if (spec == k) {                                                                                      \
-    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(nenv), dim3(64), lds, stream, m, B, L, nsub, mode); \
+    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
     return hipGetLastError();                                                                           \
   }                                                                                                     \
   k++;
   DX_SPECS(DX_LAUNCH)
 #undef DX_LAUNCH
   (void)k;
-  hipLaunchKernelGGL(dx_step_kernel, dim3(nenv), dim3(64), lds, stream, m, B, L, nsub, mode);
+  hipLaunchKernelGGL(dx_step_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode);
   return hipGetLastError();
 }
 

@@ -148,6 +148,10 @@ class BatchedPhysics:
             "contact": (self.nenv, self.model.ncon_max, 16),
             "efc_count": (self.nenv, 2),
         }
+        if name == "queue_timeouts":
+            out = np.zeros(1, dtype=np.int32)
+            _lib.check(_lib.load().dx_debug_get(self.ptr, name.encode(), out.ctypes.data, 1))
+            return out
         shape = sizes[name]
         out = np.empty(shape, dtype=np.float32)
         _lib.check(_lib.load().dx_debug_get(self.ptr, name.encode(), out.ctypes.data, out.size))

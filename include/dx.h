@@ -70,6 +70,8 @@ enum dx_field {
                            `ground_geom` with dist <= 1e-8 (reorient.py:229-235) */
   DX_NITER = 12,        /* 1  (int32 bits) solver iterations of the last substep */
   DX_NCAND = 13,        /* 1  (int32 bits) narrowphase candidates of the last collision pass */
+  DX_STEP_COST = 14,    /* 1  (uint32 bits) shader cycles / 1024 the env's last dx_step took
+                           (feeds the longest-first dispatch order; 0 if disabled) */
   DX_NFIELD
 };
 
@@ -129,7 +131,9 @@ int dx_sync(dx_batch* b);
  * substep: qacc_smooth, qfrc_bias(+applied), qfrc_actuator, M (nv*nv), contacts. */
 int dx_debug_enable(dx_batch* b, int enable);
 /* name: "qacc_smooth" "qfrc_smooth" "M" "contact" (16 floats/contact: pos3 frame9
- * dist geom1 geom2 condim) "efc_count" ; dst is host memory for all envs. */
+ * dist geom1 geom2 condim) "efc_count" ; dst is host memory for all envs.
+ * "queue_timeouts" (1 word, int32 bits, no dx_debug_enable needed): nonzero if a
+ * task of the substep queue ever stopped waiting for its predecessor. */
 int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
 
 /* Environments: a dx_batch plus on-device task logic ------------------- */
@@ -233,7 +237,8 @@ int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t* sites, int
 int dx_timing_enable(dx_batch* b, int enable);
 int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
 /* Per-stage shader-clock accounting inside the fused step kernel (diagnostics):
- * out[k] = summed s_memtime cycles of stage k over all envs since the last read. */
+ * out[k] = summed s_memtime cycles of stage k over all envs since the last read
+ * (n < nenv * 32), or out[env * 32 + k] per env (n >= nenv * 32). */
 int dx_stage_timing(dx_batch* b, int enable);
 int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n);
 /* Test hook: overwrites the LDS of every CU on `device` with NaN patterns. */

@@ -319,7 +319,32 @@ def test_full_batch_properties(gpu):
     assert np.all(np.isfinite(ts.reward))
     ncon = env.physics.get(_lib.NCON)[:, 0]
     assert (ncon > 0).mean() > 0.5
+    assert env.physics.debug_get("queue_timeouts")[0] == 0
     env.close()
+
+
+def test_substep_queue_matches_per_env_launch(gpu, monkeypatch):
+    """The substep queue (one task per env and physics step, state handed over through
+    HBM between workgroups, dx_step.hip step_queue) gives bit-identical trajectories to
+    one workgroup per env for the whole control step (DX_NO_QUEUE=1), auto-resets,
+    rewards and observations included: 4096 envs, 25 control steps."""
+    from dexterity_amd import manipulation
+
+    outs = []
+    for no_queue in (False, True):
+        if no_queue:
+            monkeypatch.setenv("DX_NO_QUEUE", "1")
+        env = manipulation.load("reorient", "state_dense", seed=5, num_envs=4096)
+        env.reset()
+        for step in range(25):
+            env.step(env.sample_actions(step), device_action=True)
+        ts = env.timestep()
+        outs.append((env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART), ts.reward,
+                     np.concatenate([v.reshape(4096, -1) for v in ts.observation.values()], axis=1)))
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        env.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
 
 
 def _check_reach_rewards(env, ts, dense):

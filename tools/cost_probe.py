@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""Per-env step-cost distribution of the reorient benchmark (diagnostics).
+
+Reads DX_STEP_COST (shader cycles / 1024 per env of the last control step) after a
+warm-up, and estimates how much of the launch the wave slots sit idle: with S wave
+slots (8 per CU) and longest-first dispatch the makespan is bounded below by both
+sum(cost) / S and max(cost).
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dexterity_amd import _lib, manipulation  # noqa: E402
+
+
+def main(nenv=4096, steps=60):
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=nenv, device=0)
+    env.reset()
+    costs = []
+    for i in range(steps):
+        env.step(env.sample_actions(i), device_action=True)
+        if i >= 10:
+            costs.append(env.physics.get(_lib.STEP_COST).ravel().astype(np.float64) * 1024)
+    c = np.array(costs)
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.save("gpurun_out/costs.npy", c.astype(np.float32))
+    slots = 256 * 8
+    per = c.mean(axis=0)
+    print(f"cycles per env-step: mean {c.mean():.3e} p50 {np.median(c):.3e} p90 {np.percentile(c, 90):.3e} "
+          f"p99 {np.percentile(c, 99):.3e} max {c.max():.3e}")
+    print(f"per-step sum/slots {np.mean(c.sum(axis=1) / slots):.3e}  per-step max {np.mean(c.max(axis=1)):.3e}")
+    print("per-env mean cost deciles:", np.round(np.percentile(per, np.arange(0, 101, 10)) / 1e6, 3))
+    # how well the last step's cost predicts this step's (what longest-first relies on)
+    cc = [np.corrcoef(c[t], c[t - 1])[0, 1] for t in range(1, len(c))]
+    print(f"corr(cost_t, cost_t-1) mean {np.mean(cc):.3f}")
+    ranks = []
+    for t in range(1, len(c)):
+        prev_rank = np.argsort(np.argsort(-c[t - 1]))
+        ranks.extend(prev_rank[np.argsort(-c[t])[:20]].tolist())
+    print("previous-step rank of each step's 20 heaviest envs: median", np.median(ranks),
+          "p90", np.percentile(ranks, 90))
+    hist, edges = np.histogram(c.ravel() / 1e6, bins=20)
+    print("hist (Mcycles):", list(zip(np.round(edges[:-1], 2).tolist(), hist.tolist())))
+    env.close()
+
+
+if __name__ == "__main__":
+    main(*[int(a) for a in sys.argv[1:]])

@@ -19,15 +19,16 @@ for i in range(10):
     env.step(env.sample_actions(i), device_action=True)
 env.physics.sync()
 _lib.check(L.dx_stage_timing(env.physics.ptr, 1))
-buf = (ctypes.c_uint64 * _lib.NSTAGE)()
-_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE))
+buf = (ctypes.c_uint64 * (_lib.NSTAGE * B))()
+_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE * B))
 t = time.perf_counter()
 for i in range(steps):
     env.step(env.sample_actions(100 + i), device_action=True)
 env.physics.sync()
 dt = time.perf_counter() - t
-_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE))
-cyc = np.array(list(buf), dtype=np.float64)
+_lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE * B))
+per_env = np.frombuffer(buf, dtype=np.uint64).reshape(B, _lib.NSTAGE).astype(np.float64)
+cyc = per_env.sum(axis=0)
 cnt = {name: cyc[k] / (B * steps * 5) for k, name in _lib.COUNTERS.items()}
 cyc[list(_lib.COUNTERS)] = 0
 tot = cyc.sum()
@@ -38,6 +39,18 @@ for k, name in enumerate(_lib.STAGES):
     print(f"  {name:20s} {100*cyc[k]/tot:6.2f}%  {per[k]:12.0f} cyc/env-substep")
     out[name] = per[k]
 print("narrowphase calls per env-substep", {k: round(v, 3) for k, v in cnt.items()})
+# the heaviest environments bound the launch (longest-first dispatch): their stages
+stage_cols = [k for k in range(len(_lib.STAGES))]
+tot_env = per_env[:, stage_cols].sum(axis=1)
+order = np.argsort(tot_env)
+top = order[-max(1, B // 100):]
+mid = order[B // 2 - B // 100: B // 2 + B // 100]
+print(f"heaviest 1% envs: {tot_env[top].mean() / (steps * 5):.0f} cyc/substep, median band "
+      f"{tot_env[mid].mean() / (steps * 5):.0f}")
+for k in np.argsort(-per_env[top][:, stage_cols].mean(axis=0))[:12]:
+    print(f"  {_lib.STAGES[k]:20s} top1% {per_env[top, k].mean() / (steps * 5):10.0f}   median {per_env[mid, k].mean() / (steps * 5):10.0f}")
+for k, name in _lib.COUNTERS.items():
+    print(f"  {name:16s} top1% {per_env[top, k].mean() / (steps * 5):8.2f}   median {per_env[mid, k].mean() / (steps * 5):8.2f}")
 niter = env.physics.get(_lib.NITER)[:, 0]
 ncon = env.physics.get(_lib.NCON)[:, 0]
 print("niter hist", np.bincount(niter), "ncon mean", ncon.mean(), "max", ncon.max())
