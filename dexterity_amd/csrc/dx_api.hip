@@ -19,7 +19,7 @@
 #include "../../include/dx.h"
 #include "dx_internal.h"
 
-extern "C" __global__ void dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode);
+extern "C" __global__ void dx_step_kernel(const DevModel* mp, DevBatch B, Lds L, int nsub, int mode);
 extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int n);
 
 static thread_local std::string g_err;
@@ -77,6 +77,7 @@ struct dx_model {
   DevModel dm;  // host-side scalars; pointers filled per device
   std::map<int, std::vector<void*>> dev_allocs;
   std::map<int, DevModel> dev_models;
+  std::map<int, const DevModel*> dev_model_ptrs;  // device copy of dev_models[device]
   Lds lds;
   int ncon_max, nefc_max;
 };
@@ -749,6 +750,11 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   allocs.push_back(p);
   HIPCHK(hipMemcpy(p, m->body_chain.data(), m->body_chain.size() * 8, hipMemcpyHostToDevice));
   d.body_chain = (decltype(d.body_chain))p;
+  // the struct itself, for the kernels that read the model through a pointer
+  HIPCHK(hipMalloc(&p, sizeof(DevModel)));
+  allocs.push_back(p);
+  HIPCHK(hipMemcpy(p, &d, sizeof(DevModel), hipMemcpyHostToDevice));
+  m->dev_model_ptrs[device] = (const DevModel*)p;
   m->dev_models[device] = d;
   *out = d;
   return 0;
@@ -762,6 +768,7 @@ struct dx_batch {
   int device, nenv;
   hipStream_t stream;
   DevModel dm;
+  const DevModel* dm_dev;  // the same struct in device memory (kernels read it through this)
   DevBatch db;
   int spec;  // specialized step kernel (dx_specs.inc) or -1 for the generic one
   bool queue;  // mode-0 steps through the substep queue
@@ -799,6 +806,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
     return nullptr;
   }
   if (device_model(m, device, &b->dm) != 0) { delete b; return nullptr; }
+  b->dm_dev = m->dev_model_ptrs[device];
   b->spec = getenv("DX_GENERIC_KERNEL") ? -1 : dx_spec_find(b->dm, m->lds);
   const DevModel& d = b->dm;
   DevBatch& B = b->db;
@@ -973,7 +981,7 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   }
   hipEvent_t t0;
   timing_begin(b, &t0);
-  hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm, b->db, b->model->lds, nsub, queued ? 3 : mode);
+  hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
   // every workgroup of a queued launch makes exactly one claim past the last task
   if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
@@ -1045,7 +1053,7 @@ extern "C" int dx_jac_site(dx_batch* b, const int32_t* sites, int32_t nsite, flo
   if (!ds || (jacp && !P.jacp) || (jacr && !P.jacr)) return fail(DX_ENOMEM, "device scratch allocation failed");
   P.sites = ds;
   HIPCHK(hipMemcpyAsync(ds, sites, nsite * 4, hipMemcpyHostToDevice, b->stream));
-  HIPCHK(dx_launch_ik(b->nenv, lds, b->stream, b->dm, b->db, b->model->lds, P));
+  HIPCHK(dx_launch_ik(b->nenv, lds, b->stream, b->dm_dev, b->db, b->model->lds, P));
   if (jacp) HIPCHK(hipMemcpyAsync(jacp, P.jacp, n * 4, hipMemcpyDefault, b->stream));
   if (jacr) HIPCHK(hipMemcpyAsync(jacr, P.jacr, n * 4, hipMemcpyDefault, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
@@ -1105,7 +1113,7 @@ extern "C" int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t*
   P.sites = ds;
   P.joints = dj;
   P.targets = dt;
-  HIPCHK(dx_launch_ik((int)(E * A), lds, b->stream, b->dm, b->db, b->model->lds, P));
+  HIPCHK(dx_launch_ik((int)(E * A), lds, b->stream, b->dm_dev, b->db, b->model->lds, P));
   HIPCHK(dx_launch_ik_select((int)E, b->stream, b->dm, P, oq, os, oe, oa, ot));
   if (qpos_out) HIPCHK(hipMemcpyAsync(qpos_out, oq, E * njoint * 4, hipMemcpyDefault, b->stream));
   if (success) HIPCHK(hipMemcpyAsync(success, os, E * 4, hipMemcpyDefault, b->stream));

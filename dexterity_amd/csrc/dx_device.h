@@ -200,6 +200,10 @@ __device__ __forceinline__ float dot6(const float* a, const float* b) {
 #define DX_DIMS(X) X(nq) X(nv) X(nbody) X(njnt) X(nu) X(ntendon) X(nsite) X(nlevel) X(nroot) \
   X(nfric) X(nlimj) X(nlimt) X(nbpair) X(any_damping) X(disable_contact) X(iterations)
 struct SpecRT {};
+// Stages take the model through c.mdl().  (Laundering that reference per stage, so
+// each stage re-loads its table pointers instead of the kernel keeping ~100 of them
+// live, cut the SGPR spills 408 -> 331 but not the step time; it is a plain
+// reference.)
 template <class SP>
 struct CtxT {
   const DevModel& m;
@@ -214,6 +218,7 @@ struct CtxT {
   __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
       : m(m_), S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
+  __device__ const DevModel& mdl() const { return m; }
 };
 template <>
 struct CtxT<SpecRT> {
@@ -233,6 +238,7 @@ struct CtxT<SpecRT> {
 #undef DX_X
         S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
+  __device__ const DevModel& mdl() const { return m; }
 };
 // Per-stage cycle accounting (runtime-gated by DevBatch::stage_acc, lane 0 only).
 enum {
@@ -272,7 +278,7 @@ template <class Ctx>
 __device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
   const int b = LANE;
   const bool act = b >= 1 && b < c.nbody;
-  const DXG float4* R = c.m.body_rec + 8 * (act ? b : 0);
+  const DXG float4* R = c.mdl().body_rec + 8 * (act ? b : 0);
   const float4 a = R[0], p = R[1], q = R[2], i = R[3], jp = R[4], jx = R[5], d = R[6];
   r.parent = __float_as_int(a.x);
   r.depth = act ? __float_as_int(a.y) : -1;
@@ -296,7 +302,7 @@ __device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
 
 template <class Ctx>
 __device__ __forceinline__ void kinematics(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float* qpos = c.f(c.L.qpos);
   float* xpos = c.f(c.L.xpos);
   float* xquat = c.f(c.L.xquat);
@@ -376,7 +382,7 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
 
 template <class Ctx>
 __device__ __forceinline__ void com_pos(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float* xipos = c.f(c.L.xipos);
   float* xmat = c.f(c.L.xmat);
   float* rcom = c.f(c.L.rcom);
@@ -451,7 +457,7 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
 
 template <class Ctx>
 __device__ __forceinline__ void tendon_lengths(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float* qpos = c.f(c.L.qpos);
   float* tl = c.f(c.L.ten_len);
   for (int t = LANE; t < c.ntendon; t += DX_WAVE) {
@@ -475,7 +481,7 @@ __device__ __forceinline__ int ti(int i) { return (i * (i + 1)) >> 1; }
 
 template <class Ctx>
 __device__ __forceinline__ void crb_mass(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   float* crb = c.f(c.L.scr);
   float* cinert = c.f(c.L.cinert);

@@ -40,7 +40,7 @@ int dx_ik_lds_words(const DevModel& d, int) { return ik_lds(0, d.nv).total; }
 // (site_xpos, as geometry.PoseStamped(frame=site).get_world_pose reads it)
 template <class Ctx>
 __device__ __forceinline__ void sites_to_lds(const Ctx& c, const IkDev& P, float* pt) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   if (LANE < 3 * P.nsite) {
     const int s = LANE / 3, e = LANE - 3 * s;
     const int sid = P.sites[s];
@@ -58,7 +58,7 @@ __device__ __forceinline__ void sites_to_lds(const Ctx& c, const IkDev& P, float
 // jacp = cdof_lin + cdof_ang x (site - subtree_com[root]), jacr = cdof_ang.
 template <class Ctx>
 __device__ __forceinline__ void site_jacobian(const Ctx& c, const IkDev& P, const float* pt, float* J, bool rot) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   const int nv = c.nv, n = 3 * P.nsite * nv;
   const float* cdof = c.f(c.L.cdof);
   const float* rcom = c.f(c.L.rcom);
@@ -86,7 +86,7 @@ __device__ __forceinline__ void site_jacobian(const Ctx& c, const IkDev& P, cons
 // solved joints to their range (ik_solver.py:189-194 and 238-250).
 template <class Ctx>
 __device__ __forceinline__ void ik_integrate(const Ctx& c, const IkDev& P, const float* v, float h) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float* qpos = c.f(c.L.qpos);
   for (int j = LANE; j < c.njnt; j += DX_WAVE) {
     const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
@@ -117,8 +117,9 @@ __device__ __forceinline__ void ik_integrate(const Ctx& c, const IkDev& P, const
 
 // mode 0: one IK attempt per workgroup (blockIdx = env * nattempt + attempt);
 // mode 1: the site Jacobians of env blockIdx at its current qpos.
-extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(DevModel m, DevBatch B, Lds L, IkDev P) {
+extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, IkDev P) {
   extern __shared__ float smem[];
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   const int w = (int)blockIdx.x;
   const int env = P.mode == 0 ? w / P.nattempt : w;
   const int att = P.mode == 0 ? w - env * P.nattempt : 0;
@@ -258,7 +259,7 @@ extern "C" __global__ void dx_ik_select_kernel(int nenv, IkDev P, const DXG floa
   if (steps_out) steps_out[env] = P.att_steps[k];
 }
 
-hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B, const Lds& L,
+hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, const Lds& L,
                         const IkDev& P) {
   hipLaunchKernelGGL(dx_ik_kernel, dim3(nwave), dim3(64), lds, stream, m, B, L, P);
   return hipGetLastError();

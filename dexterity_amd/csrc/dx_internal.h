@@ -168,7 +168,7 @@ __device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, i
 
 // dx_step.hip: specialized-kernel lookup and launch (host side)
 int dx_spec_find(const DevModel& d, const Lds& L);
-hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);
 
@@ -188,7 +188,7 @@ struct IkDev {
   float *jacp, *jacr;        // mode 1: [nenv][nsite][3][nv] (either may be null)
 };
 int dx_ik_lds_words(const DevModel& d, int nsite);
-hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                         const Lds& L, const IkDev& P);
 hipError_t dx_launch_ik_select(int nenv, hipStream_t stream, const DevModel& m, const IkDev& P, float* qpos_out,
                                int* success, float* err_out, int* attempt_out, int* steps_out);

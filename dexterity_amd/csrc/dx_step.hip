@@ -32,7 +32,7 @@ struct Shape {
 
 template <class Ctx>
 __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float* mat) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int b = m.geom_bodyid[g];
   const float* xp = c.f(c.L.xpos) + 3 * b;
   const float* xm = c.f(c.L.xmat) + 9 * b;
@@ -44,7 +44,7 @@ __device__ __forceinline__ void geom_pose(const Ctx& c, int g, float* pos, float
 
 template <class Ctx>
 __device__ __forceinline__ void make_shape(const Ctx& c, int g, float half_margin, Shape& s) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   s.type = m.geom_type[g];
   geom_pose(c, g, s.pos, s.mat);
   s.size[0] = m.geom_size[3 * g]; s.size[1] = m.geom_size[3 * g + 1]; s.size[2] = m.geom_size[3 * g + 2];
@@ -169,7 +169,7 @@ __device__ __forceinline__ void find_pos(const MPoint& P0, const MPoint& P1, con
 // Shape of geom g from its record (two memory round trips: record, then body pose in LDS).
 template <class Ctx>
 __device__ __forceinline__ void make_shape_rec(const Ctx& c, int g, float half_margin, Shape& s) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   const DXG float4* r = m.geom_rec + 8 * g;
   float4 r0 = r[0], r1 = r[1], r2 = r[2], r3 = r[3], r4 = r[4], r5 = r[5], r6 = r[6];
   s.type = __float_as_int(r0.x);
@@ -631,7 +631,7 @@ __device__ __forceinline__ bool pair_is_prim(const DevModel& m, int gp) {
 // contact count (group-uniform, at most 4).
 template <class Ctx>
 __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, NpStats& st) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   float margin = m.gpair_margin[gp];
@@ -733,7 +733,7 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
 // watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
 template <class Ctx>
 __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int* I = c.I;
   int* cand = (int*)c.f(c.L.cand);
   int cmax = c.L.cand_max;
@@ -1024,7 +1024,7 @@ __device__ __forceinline__ float impedance(const float* solimp, float violation)
 template <class Ctx>
 __device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float margin, float floss, float diag,
                            const float* solref, const float* solimp, float vel, float rscale, bool fric) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float imp = impedance(solimp, pos - margin);
   float tc = fmaxf(solref[0], 2 * m.timestep), dr = solref[1];
   float dmax = fminf(0.9999f, fmaxf(0.0001f, solimp[1]));
@@ -1044,7 +1044,7 @@ __device__ __forceinline__ void row_params(const Ctx& c, int r, float pos, float
 // sparse contact jacobian (frame rows) -> cj_idx / cj_val; then all rows
 template <class Ctx>
 __device__ __forceinline__ void make_constraint(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   int* I = c.I;
   float* qpos = c.f(c.L.qpos);
@@ -1227,7 +1227,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
 // ------------------------------------------------------------------------ //
 template <class Ctx>
 __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   float* qvel = c.f(c.L.qvel);
   float* cdof = c.f(c.L.cdof);
@@ -1380,7 +1380,7 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
 // frame rows are gathered with DX_DOFMAX independent reads per lane.
 template <class Ctx>
 __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
   const int* meta = (const int*)c.f(c.L.efc_meta);
@@ -1425,7 +1425,7 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
 // sum of the constraint rows' costs at residuals jr (+ g0, the Gauss term)
 template <class Ctx>
 __device__ __forceinline__ float rows_cost(const Ctx& c, const float* jr, float g0) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nefc = c.I[I_NEFC];
   const int* meta = (const int*)c.f(c.L.efc_meta);
   const float* D = c.f(c.L.efc_D);
@@ -1444,7 +1444,7 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const float* jr, float 
 // cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
 template <class Ctx>
 __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   const float* qs = c.f(c.L.qfrc_smooth);
   const float* a0 = c.f(c.L.qacc_smooth);
@@ -1484,7 +1484,7 @@ __device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, floa
 // current jar (force mode) -- lane per dof, deterministic.
 template <class Ctx>
 __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
@@ -1560,7 +1560,7 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
 // H = M + J^T D_active J  (at the current jar)
 template <class Ctx>
 __device__ __forceinline__ void build_hessian(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
@@ -1602,55 +1602,68 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
       for (int j = 0; j <= i; j++) H[ti(i) + j] += hw * tj[i] * tj[j];
     SYNC();
   }
-  // contacts: W = sum_active_edges D c c^T in frame space; H[idx_a][idx_b] += J^T W J
+  // contacts: W = sum_active_edges D c c^T in frame space; H[idx_a][idx_b] += J^T W J.
+  // Lane ci < ncon builds contact ci's W (symmetric: w00, w01, w02, w11, w22); then
+  // the lower-triangle items of every contact's nnz x nnz block are flattened over
+  // the lanes (item t -> contact by a 5-step search over the lanes' prefix counts)
+  // and summed into H with LDS float atomics, so contacts no longer run one after
+  // another (a contact-rich env has ~20 of them).
   const float* con = c.f(c.L.con);
   const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
-  for (int ci = 0; ci < ncon; ci++) {
-    const float* r = con + DX_CON_STRIDE * ci;
-    int row0 = __float_as_int(r[15]);
-    int nnz = __float_as_int(r[14]) & 255;
-    float W[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w22 = 0.f;
+  int nnz = 0, items = 0;
+  if (LANE < ncon) {
+    const float* r = con + DX_CON_STRIDE * LANE;
+    const int row0 = __float_as_int(r[15]);
+    nnz = __float_as_int(r[14]) & 255;
     if ((__float_as_int(r[14]) >> 8) == 1) {
-      float f, hw;
-      if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); W[0] = hw; }
+      if (row0 < nefc) {
+        float f, hw;
+        row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+        w00 = hw;
+      }
     } else {
       for (int e = 0; e < 4; e++) {
-        int row = row0 + e;
+        const int row = row0 + e;
         if (row >= nefc) break;
         float f, hw;
         row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
-        if (hw == 0) continue;
-        int k = 1 + (e >> 1);
-        float mu = r[15 + k] * ((e & 1) ? -1.f : 1.f);
-        W[0] += hw;
-        W[k] += hw * mu;
-        W[3 * k] += hw * mu;
-        W[4 * k] += hw * mu * mu;
+        const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
+        w00 += hw;
+        if (e < 2) { w01 += hw * mu; w11 += hw * mu * mu; }
+        else { w02 += hw * mu; w22 += hw * mu * mu; }
       }
     }
-    if (W[0] == 0 && W[4] == 0 && W[8] == 0) continue;
-    // lower triangle of the contact's nnz x nnz block, item t -> (a >= b); cj_idx is
-    // ascending, so (idx_a, idx_b) is in H's lower triangle.  The entries of one
-    // contact are distinct; SYNC (a compiler barrier) orders consecutive contacts.
-    const int items = nnz * (nnz + 1) / 2;
-    for (int t = LANE; t < items; t += DX_WAVE) {
-      int a = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-      a += (a + 1) * (a + 2) / 2 <= t;
-      a -= a * (a + 1) / 2 > t;
-      int b = t - a * (a + 1) / 2;
-      float ja[3], jb[3];
-      for (int k = 0; k < 3; k++) {
-        ja[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + a];
-        jb[k] = cj_val[(ci * 3 + k) * DX_DOFMAX + b];
-      }
-      float s = 0;
-      for (int p = 0; p < 3; p++)
-        for (int q = 0; q < 3; q++) s += ja[p] * W[3 * p + q] * jb[q];
-      H[ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b]] += s;
-    }
-    SYNC();
+    items = (w00 == 0.f && w11 == 0.f && w22 == 0.f) ? 0 : nnz * (nnz + 1) / 2;
   }
+  const int incl = wave_incl_scan(items);
+  const int excl = incl - items;
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+    const int t = min(base + LANE, total - 1);
+    int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1) {
+      const int mid = ci + st;
+      const int em = __shfl(excl, mid & 63, 64);
+      if (mid < ncon && em <= t) ci = mid;
+    }
+    const int u = t - __shfl(excl, ci, 64);
+    int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+    a += (a + 1) * (a + 2) / 2 <= u;
+    a -= a * (a + 1) / 2 > u;
+    const int b = u - a * (a + 1) / 2;
+    const float c00 = __shfl(w00, ci, 64), c01 = __shfl(w01, ci, 64), c02 = __shfl(w02, ci, 64);
+    const float c11 = __shfl(w11, ci, 64), c22 = __shfl(w22, ci, 64);
+    const float* jv = cj_val + ci * 3 * DX_DOFMAX;
+    const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
+    const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
+    const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
+                      c22 * a2 * b2;
+    if (base + LANE < total) atomicAdd(H + ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b], sum);
+  }
+  SYNC();
 }
 
 // zone of a row's cost at jar: 0 zero, 1 quadratic, 2 / 3 linear friction zones
@@ -1665,7 +1678,7 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 #define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
 template <class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
   mat_vec(c.f(c.L.M), dir, Mdir, nv);
@@ -1734,7 +1747,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
 
 template <class Ctx>
 __device__ __forceinline__ void solve(const Ctx& c) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   float* qacc = c.f(c.L.qacc);
   float* a0 = c.f(c.L.qacc_smooth);
@@ -1834,7 +1847,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
 
 template <class Ctx>
 __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   // Stage order (LDS phases, see dx_api.hip layout): kinematics/com/crb and the
   // velocity stage use the com temporaries; the smooth solve reuses them for its
@@ -1883,7 +1896,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
 
 template <class Ctx>
 __device__ __forceinline__ void euler(const Ctx& c, float* time) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   int nv = c.nv;
   float h = m.timestep;
   float* qacc = c.f(c.L.qacc);
@@ -1937,7 +1950,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
 // observation pass at the new state: kinematics, com, velocities, sites, watch contact
 template <class Ctx>
 __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   kinematics(c);
   com_pos(c);
   // cvel (no forces)
@@ -2000,7 +2013,7 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
 // t % 3 of tip t / 3 (site_xpos of dexterous_hand.py:286-291).
 template <class Ctx>
 __device__ __forceinline__ float tip_coord(const Ctx& c, const TaskParams& P) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   float gc = 0;
   if (LANE < 3 * P.ntips) {
     int t = LANE / 3, e = LANE - 3 * t;
@@ -2185,7 +2198,7 @@ __device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, flo
 // observation pass at the new state, and the state itself.
 template <class Ctx>
 __device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int env, float time) {
-  const DevModel& m = c.m;
+  const DevModel& m = c.mdl();
   const Lds& L = c.L;
   int* I = c.I;
   if (B.dbg_qacc_smooth) {
@@ -2316,8 +2329,11 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   }
 }
 
+// The model struct is read through a device pointer (dx_api.hip device_model) in
+// the constant address space rather than passed by value in the kernarg segment.
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+dx_step_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
   else step_body<SpecRT>(m, B, L, nsub, mode);
 }
@@ -2334,7 +2350,8 @@ dx_step_kernel(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
 
 template <class SP>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-dx_step_kernel_spec(DevModel m, DevBatch B, Lds L, int nsub, int mode) {
+dx_step_kernel_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   if (mode == 3) step_queue<SP>(m, B, L, nsub);
   else step_body<SP>(m, B, L, nsub, mode);
 }
@@ -2383,7 +2400,7 @@ hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, i
   return hipGetLastError();
 }
 
-hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel& m, const DevBatch& B,
+hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B,
                           const Lds& L, int nsub, int mode) {
   int k = 0;
 #define DX_LAUNCH(SP)                                                                                   \

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Throughput of every GPU configuration of BASELINE.json on one MI355X (diagnostics).
+
+bench.py measures the headline (config 3); this script adds the other single-GPU
+configs, one JSON line each:
+  config 2  reach_shadow.state_dense (contacts disabled), 1024 envs; also Adroit reach
+  config 3  reorient.state_dense, 4096 envs (same workload as bench.py)
+  config 5  bimanual handover physics (two Shadow hands + cube, nv 54), 4096 envs,
+            random actions held for 5 physics substeps per control step
+Timed regions hold inputs in HBM (device-side actions), as in bench.py.
+"""
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _kernel_ms(L, ptr):
+    kt, kn = ctypes.c_double(), ctypes.c_int32()
+    L.dx_timing_read(ptr, ctypes.byref(kt), ctypes.byref(kn))
+    return kt.value / max(1, kn.value), kn.value
+
+
+def env_config(name, domain, task, nenv, steps=50, warmup=10):
+    from dexterity_amd import _lib, manipulation
+
+    L = _lib.load()
+    env = manipulation.load(domain, task, seed=7, num_envs=nenv)
+    env.reset()
+    for i in range(warmup):
+        env.step(env.sample_actions(i), device_action=True)
+    env.physics.sync()
+    L.dx_timing_enable(env.physics.ptr, 1)
+    _kernel_ms(L, env.physics.ptr)
+    t = time.perf_counter()
+    for i in range(steps):
+        env.step(env.sample_actions(warmup + i), device_action=True)
+    env.physics.sync()
+    dt = time.perf_counter() - t
+    kms, kn = _kernel_ms(L, env.physics.ptr)
+    env.close()
+    return {"config": name, "envs": nenv, "env_steps_per_s": round(nenv * steps / dt, 1),
+            "ms_per_step": round(dt / steps * 1e3, 4), "step_kernel_ms_avg": round(kms, 4),
+            "step_kernel_launches_per_step": kn / steps}
+
+
+def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
+    import torch
+
+    from dexterity_amd import _lib, physics
+    from dexterity_amd.mjcf.compiler import CompiledModel
+
+    L = _lib.load()
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "bimanual_handover.npz"))
+    model = physics.Model(cm)
+    phys = physics.BatchedPhysics(model, nenv)
+    phys.set_xfrc(physics.gravity_compensation(cm, "shadow_hand_"))
+    q0 = np.tile(cm.qpos0, (nenv, 1))
+    q0[:, 48:51] += np.random.RandomState(0).uniform(-0.02, 0.02, size=(nenv, 3)) * [1, 1, 0]
+    phys.set(_lib.QPOS, q0)
+    lo, hi = cm.actuator_ctrlrange.T
+    acts = torch.tensor(np.random.RandomState(1).uniform(lo, hi, size=(warmup + steps, nenv, cm.nu)),
+                        dtype=torch.float32, device="cuda:0")
+    torch.cuda.synchronize()
+
+    def one(i):
+        phys.set_device(_lib.CTRL, acts[i].data_ptr(), 0, nenv)
+        phys.step(nsub)
+
+    for i in range(warmup):
+        one(i)
+    phys.sync()
+    L.dx_timing_enable(phys.ptr, 1)
+    _kernel_ms(L, phys.ptr)
+    t = time.perf_counter()
+    for i in range(steps):
+        one(warmup + i)
+    phys.sync()
+    dt = time.perf_counter() - t
+    kms, _ = _kernel_ms(L, phys.ptr)
+    ncon = phys.get(_lib.NCON)[:, 0]
+    ok = bool(np.isfinite(phys.qpos).all())
+    phys.close()
+    return {"config": "5 bimanual handover physics (nv 54)", "envs": nenv,
+            "env_steps_per_s": round(nenv * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
+            "step_kernel_ms_avg": round(kms, 4), "substeps": nsub, "mean_ncon": float(ncon.mean()),
+            "finite": ok}
+
+
+def main():
+    import torch  # noqa: F401  (one HIP runtime for torch and libdx)
+
+    out = [
+        env_config("2 reach_shadow.state_dense (no contacts)", "reach_shadow", "state_dense", 1024),
+        env_config("2' reach.state_dense (Adroit)", "reach", "state_dense", 1024),
+        env_config("3 reorient.state_dense", "reorient", "state_dense", 4096),
+        bimanual(),
+    ]
+    for o in out:
+        print(json.dumps(o), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -51,6 +51,12 @@ for k in np.argsort(-per_env[top][:, stage_cols].mean(axis=0))[:12]:
     print(f"  {_lib.STAGES[k]:20s} top1% {per_env[top, k].mean() / (steps * 5):10.0f}   median {per_env[mid, k].mean() / (steps * 5):10.0f}")
 for k, name in _lib.COUNTERS.items():
     print(f"  {name:16s} top1% {per_env[top, k].mean() / (steps * 5):8.2f}   median {per_env[mid, k].mean() / (steps * 5):8.2f}")
+# the four heaviest single environments (with steps = 1: the heaviest env-steps)
+for e in order[-4:][::-1]:
+    parts = sorted(((per_env[e, k] / (steps * 5), _lib.STAGES[k]) for k in stage_cols), reverse=True)[:6]
+    cnts = {name: round(per_env[e, k] / (steps * 5), 1) for k, name in _lib.COUNTERS.items()
+            if name in ("mpr", "mpr_support", "mpr_hit", "np_trips", "newton_iter", "linesearch_iter", "nefc")}
+    print(f"  env {e}: {tot_env[e] / (steps * 5):.0f} cyc/substep;", ", ".join(f"{n} {v:.0f}" for v, n in parts), cnts)
 niter = env.physics.get(_lib.NITER)[:, 0]
 ncon = env.physics.get(_lib.NCON)[:, 0]
 print("niter hist", np.bincount(niter), "ncon mean", ncon.mean(), "max", ncon.max())
