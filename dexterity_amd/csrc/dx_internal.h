@@ -15,6 +15,10 @@
 // (key while sorting), 15 first efc row, 16-17 friction (mu1, mu2), 18-19 dof support mask
 #define DX_MAX_NV 64      // dof bitmasks are uint64
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
+#ifndef DX_NPG
+#define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
+#endif
+#define DX_NGRP (DX_WAVE / DX_NPG)
 
 enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };
 enum { DXJ_FREE = 0, DXJ_HINGE = 3 };

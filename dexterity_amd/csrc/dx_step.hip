@@ -194,22 +194,24 @@ __device__ __forceinline__ void make_shape_rec(const Ctx& c, int g, float half_m
   s.margin = half_margin;
 }
 
-// Narrowphase runs four candidate pairs per wave, one per 16-lane group (a DPP
+// Narrowphase runs DX_NGRP candidate pairs per wave, one per DX_NPG-lane group (part of a DPP
 // row).  Every lane of a group runs the same MPR control flow for its pair; the
 // groups diverge only through the exec mask.
-#define SL (LANE & 15)
+// DX_NPG (dx_internal.h) lanes per group: 8 (two groups per DPP row) or 16.
+#define SL (LANE & (DX_NPG - 1))
+#define GBASE (LANE & (DX_WAVE - DX_NPG))  // first lane of this lane's group
 __device__ __forceinline__ float row_max_f(float m) {
-  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));   // quad_perm [1,0,3,2]
-  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));   // quad_perm [2,3,0,1]
-  m = fmaxf(m, dpp_f<0x141, 0xF>(m));  // row_half_mirror
-  m = fmaxf(m, dpp_f<0x140, 0xF>(m));  // row_mirror
+  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));                      // quad_perm [1,0,3,2]
+  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));                      // quad_perm [2,3,0,1]
+  m = fmaxf(m, dpp_f<0x141, 0xF>(m));                     // row_half_mirror (8 lanes)
+  if (DX_NPG == 16) m = fmaxf(m, dpp_f<0x140, 0xF>(m));   // row_mirror (16 lanes)
   return m;
 }
 __device__ __forceinline__ int row_min_i(int m) {
   m = min(m, dpp_i<0xB1, 0xF>(m));
   m = min(m, dpp_i<0x4E, 0xF>(m));
   m = min(m, dpp_i<0x141, 0xF>(m));
-  m = min(m, dpp_i<0x140, 0xF>(m));
+  if (DX_NPG == 16) m = min(m, dpp_i<0x140, 0xF>(m));
   return m;
 }
 
@@ -256,7 +258,7 @@ __device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i,
 __device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
   float vmax = row_max_f(h.d);
   int bi = row_min_i(h.d == vmax ? h.i : 0x7fffffff);
-  int src = (LANE & 48) | (bi & 15);
+  int src = GBASE | (bi & (DX_NPG - 1));
   lp[0] = __shfl(h.x, src, 64);
   lp[1] = __shfl(h.y, src, 64);
   lp[2] = __shfl(h.z, src, 64);
@@ -292,7 +294,7 @@ __device__ __forceinline__ void hull_span(const Shape& s, const float* ld, const
   }
 }
 
-// Support points of A along dir and of B along -dir, by one 16-lane group.  Both
+// Support points of A along dir and of B along -dir, by one lane group.  Both
 // hulls (or their direction cells, <= 64 slots) are scanned in the same pass from L2:
 // eight float4 loads in flight per lane, one memory round trip.
 __device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, const float* dir, float* outA,
@@ -308,16 +310,16 @@ __device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, con
   HullBest hA = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff}, hB = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
   const int n = max(nA, nB);
   for (int base = 0; base < n; base += 64) {
-    float4 va[4], vb[4];
+    float4 va[64 / DX_NPG], vb[64 / DX_NPG];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      int i = base + u * 16 + SL;
+    for (int u = 0; u < 64 / DX_NPG; u++) {
+      int i = base + u * DX_NPG + SL;
       va[u] = VA[i < nA ? i : 0];
       vb[u] = VB[i < nB ? i : 0];
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      int i = base + u * 16 + SL;
+    for (int u = 0; u < 64 / DX_NPG; u++) {
+      int i = base + u * DX_NPG + SL;
       hull_take(hA, va[u], va[u].x * la[0] + va[u].y * la[1] + va[u].z * la[2], i,
                 i < nA && __float_as_int(va[u].w) >= 0);
       hull_take(hB, vb[u], vb[u].x * lb[0] + vb[u].y * lb[1] + vb[u].z * lb[2], i,
@@ -340,15 +342,15 @@ __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, fl
     hull_span(s, ld, V, cnt);
     HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
     for (int base = 0; base < cnt; base += 64) {
-      float4 v[4];
+      float4 v[64 / DX_NPG];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        int i = base + u * 16 + SL;
+      for (int u = 0; u < 64 / DX_NPG; u++) {
+        int i = base + u * DX_NPG + SL;
         v[u] = V[i < cnt ? i : 0];
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        int i = base + u * 16 + SL;
+      for (int u = 0; u < 64 / DX_NPG; u++) {
+        int i = base + u * DX_NPG + SL;
         hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], i,
                   i < cnt && __float_as_int(v[u].w) >= 0);
       }
@@ -364,7 +366,7 @@ struct NpStats { int support, mpr, hit, plane_box, plane_convex, capsule, maxit;
 
 // MPR penetration on A - B (libccd ccdMPRPenetration structure, see the oracle's
 // mpr_penetration) as a resumable state machine: one support evaluation per
-// mpr_step, so the four 16-lane groups of a wave -- each on its own pair and in its
+// mpr_step, so the lane groups of a wave -- each on its own pair and in its
 // own MPR phase -- share every support pass.  The portal points live in LDS (36
 // words per group: P0..P3 = v, a, b): kept in registers, every divergent phase
 // branch re-materialised all 36 of them at its join.
@@ -627,7 +629,7 @@ __device__ __forceinline__ bool pair_is_prim(const DevModel& m, int gp) {
   int t1 = m.geom_type[m.gpair_geom[2 * gp]], t2 = m.geom_type[m.gpair_geom[2 * gp + 1]];
   return t1 == DXG_PLANE || (t1 == DXG_CAPSULE && t2 == DXG_CAPSULE);
 }
-// Primitive narrowphase of one geom pair by one 16-lane group; returns the group's
+// Primitive narrowphase of one geom pair by one lane group; returns the group's
 // contact count (group-uniform, at most 4).
 template <class Ctx>
 __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, NpStats& st) {
@@ -665,7 +667,7 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
         dist = dot3(r, n);
         hit = dist <= margin;
       }
-      unsigned gm = (unsigned)((__ballot(hit) >> (LANE & 48)) & 0xFFFFull);
+      unsigned gm = (unsigned)((__ballot(hit) >> GBASE) & ((1ull << DX_NPG) - 1ull));
       int rank = __popc(gm & ((1u << SL) - 1u));
       o.wr = hit && rank < 4;
       o.rank = rank;
@@ -815,7 +817,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int gmax = cmax - 2 * half;
   // pair records of the surviving candidates, after the four groups' portal points
   // (dx_api.hip layout reserves 4 * gmax words there)
-  float4* gcrec = (float4*)(c.f(c.L.cand + c.L.cand_max) + 4 * MP_WORDS);
+  float4* gcrec = (float4*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP * MP_WORDS);
   int ng = 0;
   int total = nbc > 0 ? pref[nbc] : 0;
   for (int base = 0; base < total; base += DX_WAVE) {
@@ -881,7 +883,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   if (LANE == 0) I[I_NCAND] = ng;
   SYNC();
   stage_mark(c, ST_MID);
-  // 3. narrowphase.  Four 16-lane groups walk the candidate list in this one loop,
+  // 3. narrowphase.  DX_NGRP lane groups walk the candidate list in this one loop,
   // each taking the next unassigned candidate when its pair is done, so a group
   // never waits for another group's pair.  Contacts are written unordered together with
   // their key (candidate, rank) and put into candidate order below, which gives the
@@ -890,8 +892,8 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int ncon = 0;
   NpStats st = {0, 0, 0, 0, 0, 0, 0};
   {
-    const int grp = LANE >> 4;
-    int q = grp, next = 4;
+    const int grp = LANE / DX_NPG;
+    int q = grp, next = DX_NGRP;
     bool fresh = true;
     int gp = 0;
     float margin = 0;
@@ -949,21 +951,21 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
           }
         }
       }
-      int c0 = __builtin_amdgcn_readlane(cnt, 0), c1 = __builtin_amdgcn_readlane(cnt, 16);
-      int c2 = __builtin_amdgcn_readlane(cnt, 32), c3 = __builtin_amdgcn_readlane(cnt, 48);
-      int pre = grp == 0 ? 0 : grp == 1 ? c0 : grp == 2 ? c0 + c1 : c0 + c1 + c2;
+      // contacts of the groups before this one (cnt is uniform within a group)
+      const int cinc = wave_incl_scan(SL == 0 ? cnt : 0);
+      const int pre = __shfl(cinc, GBASE, 64) - cnt;
       int slot = ncon + pre + o.rank;
       if (o.wr && slot < DX_NCON_MAX) {
         write_contact(con, slot, o.pos, o.n, o.dist, gp);
         con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
       }
-      ncon += c0 + c1 + c2 + c3;
+      ncon += __builtin_amdgcn_readlane(cinc, 63);
       // a group that finished its pair takes the next unassigned candidate (in group
       // order), so a long MPR on one group no longer holds back the others' queues;
       // the contact keys still sort the list into candidate order below
       const uint64_t fin = __ballot(done && SL == 0);
       if (done) {
-        q = next + __popcll(fin & ((1ull << (LANE & 48)) - 1ull));
+        q = next + __popcll(fin & ((1ull << GBASE) - 1ull));
         fresh = true;
       }
       next += __popcll(fin);
