@@ -576,7 +576,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.cw = take(3 * DX_NCON_MAX);
   end = std::max(end, off);
   L.H = U0;
-  L.total = end;
+  L.total = (end + 3) & ~3;  // the kernels zero it with 16-byte stores
   m->ncon_max = DX_NCON_MAX;
   m->nefc_max = L.nefc_max;
   if (L.nefc_max > 5 * 64) {  // line-search register slots (dx_step.hip DX_LS_SLOTS)

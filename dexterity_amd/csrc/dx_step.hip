@@ -2141,7 +2141,8 @@ __device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env) {
   // packed triangles (padding lanes/columns, multiplied by exact zeros), and those
   // must be finite rather than whatever an earlier workgroup left behind.
 #ifndef DX_SKIP_LDS_ZERO  // (defined only by the test that shows why this is needed)
-  for (int k = LANE; k < L.total; k += DX_WAVE) smem[k] = 0.f;
+  for (int k = 4 * LANE; k < L.total; k += 4 * DX_WAVE)  // L.total is a multiple of 4
+    *(float4*)(smem + k) = make_float4(0.f, 0.f, 0.f, 0.f);
 #endif
   SYNC();
   int* I = c.I;
