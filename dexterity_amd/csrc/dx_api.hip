@@ -551,7 +551,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.con = take(DX_NCON_MAX * DX_CON_STRIDE);
   L.nefc_max = d.nfric + 2 * d.nlimj + 2 * d.nlimt + 4 * DX_NCON_MAX;
   L.efc_fl = take(std::max(d.nfric, 1)); L.efc_Rf = take(std::max(d.nfric, 1));
-  L.tri = nv > 32 ? take((ntri + 1) / 2) : 0;
+  L.tri = 0;  // (was the wave Cholesky's index table; n > 32 now factors on the matrix cores)
   const int U0 = off;
   L.xpos = take(3 * nb); L.xmat = take(9 * nb); L.xipos = take(3 * nb);
   L.rcom = take(3 * std::max(d.nroot, 1)); L.cdof = take(6 * nv);

@@ -650,3 +650,119 @@ __device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const D
   if (i < n) x[i] = xo;
   SYNC();
 }
+
+// Cholesky solve for 32 < n <= 64 on the matrix cores (two-hand scenes, nv 54).  The
+// padded 64 x 64 matrix is three 32 x 32 accumulator tiles: C11 (rows/cols 0-31),
+// C12 (rows 0-31, cols 32-63, i.e. the transpose of the lower off-diagonal block)
+// and C22 (rows/cols 32-63, identity padding past n).  Right-looking, two columns
+// per step as in mfma_chol_solve32: for k < 32 rows k, k+1 of C11 give the panel's
+// rows 0-31 and rows k, k+1 of C12 its rows 32-63 (symmetry again), and three MFMAs
+// apply the rank-2 update to C11, C12 and C22; columns 32-63 then factor C22 alone.
+// L goes to T (packed rows, ti(n) words, may alias A) as it is produced, and both
+// substitutions run with lane = row (0-63) on readlane / writelane chains.
+__device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const DXG float* dadd, float hs,
+                                                  float* x, float* T) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  dx_f16v C11, C12, C22;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    {  // C11: A[i][j]
+      const int ra = max(i, j), rb = min(i, j);
+      float e = A[ti(ra) + rb];  // i, j < 32 < n
+      if (dadd && i == j) e += hs * dadd[i];
+      C11[v] = e;
+    }
+    {  // C12: A[i][32 + j] = A[32 + j][i]
+      const int r = 32 + j;
+      C12[v] = r < n ? A[ti(r) + i] : 0.f;
+    }
+    {  // C22: A[32 + i][32 + j]
+      const int ri = 32 + i, rj = 32 + j;
+      const bool in = ri < n && rj < n;
+      const int ra = max(ri, rj), rb = min(ri, rj);
+      float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
+      if (dadd && i == j && in) e += hs * dadd[ri];
+      C22[v] = e;
+    }
+  }
+  float b = l < n ? x[l] : 0.f;
+  SYNC();  // A may alias T
+  float dinv = 0.f;  // lane k: 1 / L[k][k]
+  // columns 0..31
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C11[vk], up), rk1 = half_dup(C11[vk + 1], up);  // A[j][k], A[j][k+1]
+    const float sk = half_dup(C12[vk], up), sk1 = half_dup(C12[vk + 1], up);  // A[32+j][k], A[32+j][k+1]
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
+    const float l21 = rl(rk1, k) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    dinv = wl(dinv, i11, k);
+    dinv = wl(dinv, i22, k + 1);
+    const float lk = rk * i11, lk1 = (rk1 - lk * l21) * i22;  // L[j][k], L[j][k+1]
+    const float mk = sk * i11, mk1 = (sk1 - mk * l21) * i22;  // L[32+j][k], L[32+j][k+1]
+    if (hi == 0) {
+      if (j > k) T[ti(j) + k] = lk;
+      if (j > k + 1) T[ti(j) + k + 1] = lk1;
+    } else if (32 + j < n) {
+      T[ti(32 + j) + k] = mk;
+      T[ti(32 + j) + k + 1] = mk1;
+    }
+    const float pa = j > k + 1 ? (hi ? lk1 : lk) : 0.f;
+    const float pb = hi ? mk1 : mk;
+    C11 = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa, pa, C11, 0, 0, 0);
+    C12 = __builtin_amdgcn_mfma_f32_32x32x2f32(-pa, pb, C12, 0, 0, 0);
+    C22 = __builtin_amdgcn_mfma_f32_32x32x2f32(-pb, pb, C22, 0, 0, 0);
+  }
+  // columns 32..63: the trailing tile alone
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C22[vk], up), rk1 = half_dup(C22[vk + 1], up);
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
+    const float l21 = rl(rk1, k) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    dinv = wl(dinv, i11, 32 + k);
+    dinv = wl(dinv, i22, 32 + k + 1);
+    const float lk = rk * i11, lk1 = (rk1 - lk * l21) * i22;  // L[32+j][32+k], L[32+j][32+k+1]
+    if (hi == 0 && 32 + j < n) {
+      if (j > k) T[ti(32 + j) + 32 + k] = lk;
+      if (j > k + 1) T[ti(32 + j) + 32 + k + 1] = lk1;
+    }
+    const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;
+    C22 = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C22, 0, 0, 0);
+  }
+  SYNC();
+  const int i = l;
+  // forward: L y = b (lane i holds b_i, then y_i)
+  float y = 0.f;
+  for (int k = 0; k < n; k++) {
+    const float lik = i > k && i < n ? T[ti(i) + k] : 0.f;
+    const float yk = rl(b, k) * rl(dinv, k);
+    y = wl(y, yk, k);
+    b = fmaf(-lik, yk, b);
+  }
+  // backward: L^T x = y
+  float xo = 0.f;
+  for (int k = n - 1; k >= 0; k--) {
+    const float lki = i < k ? T[ti(k) + i] : 0.f;
+    const float xk = rl(y, k) * rl(dinv, k);
+    xo = wl(xo, xk, k);
+    y = fmaf(-lki, xk, y);
+  }
+  SYNC();
+  if (i < n) x[i] = xo;
+  SYNC();
+}
+
+// x <- (A + hs * diag(dadd))^-1 x for a packed lower-triangle A (LDS), n <= 64;
+// T: ti(max(n, 32)) words of LDS scratch, may alias A.
+__device__ __forceinline__ void chol_solve(const float* A, int n, const DXG float* dadd, float hs, float* x,
+                                           float* T) {
+  if (n <= 32) mfma_chol_solve32(A, n, dadd, hs, x, T);
+  else mfma_chol_solve64(A, n, dadd, hs, x, T);
+}

@@ -1806,12 +1806,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     float* H = c.f(c.L.H);
     for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
     SYNC();
-    if (nv <= 32) {
-      mfma_chol_solve32(H, nv, nullptr, 0.f, dir, H);
-    } else {
-      wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
-      wave_chol_solve(H, dir, nv);
-    }
+    chol_solve(H, nv, nullptr, 0.f, dir, H);
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float alpha = line_search(c, qacc, Ma, dir, &changed);
@@ -1871,15 +1866,8 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   float* a0 = c.f(c.L.qacc_smooth);
   const float* qs = c.f(c.L.qfrc_smooth);
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
-  if (nv <= 32) {
-    SYNC();
-    mfma_chol_solve32(M, nv, nullptr, 0.f, a0, H);
-  } else {
-    for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
-    SYNC();
-    wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
-    wave_chol_solve(H, a0, nv);
-  }
+  SYNC();
+  chol_solve(M, nv, nullptr, 0.f, a0, H);
   stage_mark(c, ST_SMOOTH);
   collision(c, 0, -1, -1);
   make_constraint(c);
@@ -1909,17 +1897,8 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
     float* H = c.f(c.L.H);
     const float* M = c.f(c.L.M);
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
-    if (nv <= 32) {
-      SYNC();
-      mfma_chol_solve32(M, nv, m.dof_damping, h, acc, H);
-    } else {
-      for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
-      SYNC();
-      for (int i = LANE; i < nv; i += DX_WAVE) H[ti(i) + i] += h * m.dof_damping[i];
-      SYNC();
-      wave_cholesky(H, nv, (const unsigned short*)c.f(c.L.tri));
-      wave_chol_solve(H, acc, nv);
-    }
+    SYNC();
+    chol_solve(M, nv, m.dof_damping, h, acc, H);
   } else {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
     SYNC();
@@ -2158,17 +2137,6 @@ __device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env) {
   }
   for (int i = LANE; i < c.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * c.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
-  if (c.nv > 32) {
-    // lower-triangle index table for wave_cholesky: t -> (i << 8 | j), row-major
-    unsigned short* tri = (unsigned short*)c.f(L.tri);
-    int T = c.nv * (c.nv + 1) / 2;
-    for (int t = LANE; t < T; t += DX_WAVE) {
-      int i = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-      while ((i + 1) * (i + 2) / 2 <= t) i++;
-      while (i * (i + 1) / 2 > t) i--;
-      tri[t] = (unsigned short)((i << 8) | (t - i * (i + 1) / 2));
-    }
-  }
   const float time = B.time[env];
   SYNC();
   return time;
