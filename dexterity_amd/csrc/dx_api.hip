@@ -395,8 +395,10 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   }
   // collision culling records: per geom {type, body}{bsphere (body frame)}{obb centre,
   // R (body <- box), half extents; planes: point, normal} and per body pair {b1, b2,
-  // first geom pair, count}{sphere 1}{sphere 2}{margin, plane geom, plane body}{plane
-  // point}{plane normal} (body frames) -- one memory round trip per culling item
+  // first geom pair, count}{sphere 1}{sphere 2}{margin, plane geom, plane body, box
+  // margin}{plane point | box 1 centre, half x}{plane normal | box 1 half y z, box 2
+  // centre x y}{box 2 centre z, half extents} (body frames) -- one memory round trip
+  // per culling item
   {
     auto& gt = m->hi["geom_type"]; auto& gb = m->hi["geom_bodyid"];
     auto& gbs = m->hf["geom_bsphere_b"]; auto& gob = m->hf["geom_obb_b"];
@@ -420,9 +422,10 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     auto& bb = m->hi["bpair_body"]; auto& ba = m->hi["bpair_adr"]; auto& bnum = m->hi["bpair_num"];
     auto& bpl = m->hi["bpair_plane"]; auto& bs = m->hf["bpair_sphere"]; auto& pm = m->hf["gpair_margin"];
     int nbp = (int)bnum.size();
-    std::vector<float> br(24 * std::max(nbp, 1), 0.f);
+    auto& gpg = m->hi["gpair_geom"];
+    std::vector<float> br(28 * std::max(nbp, 1), 0.f);
     for (int k = 0; k < nbp; k++) {
-      float* r = br.data() + 24 * k;
+      float* r = br.data() + 28 * k;
       int iv[4] = {bb[2 * k], bb[2 * k + 1], ba[k], bnum[k]};
       memcpy(r, iv, 16);
       for (int e = 0; e < 8; e++) r[4 + e] = bs[8 * k + e];
@@ -430,8 +433,44 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
       int pg = bpl[k], pb = pg >= 0 ? gb[pg] : 0;
       memcpy(r + 13, &pg, 4);
       memcpy(r + 14, &pb, 4);
-      if (pg >= 0)
+      if (pg >= 0) {
         for (int e = 0; e < 3; e++) { r[16 + e] = gp[3 * pg + e]; r[20 + e] = gm[9 * pg + 3 * e + 2]; }
+      } else {
+        // Box cull: per side, the body-frame box around the OBBs (geom_obb_b) of that
+        // side's geoms in this pair, grown by a little, and the largest geom-pair
+        // margin.  Geom pairs whose OBBs overlap have overlapping boxes, so a pair the
+        // boxes separate has no geom pair the mid-phase would keep.
+        double lo[2][3] = {{1e30, 1e30, 1e30}, {1e30, 1e30, 1e30}};
+        double hi[2][3] = {{-1e30, -1e30, -1e30}, {-1e30, -1e30, -1e30}};
+        double mmax = 0;
+        for (int q = ba[k]; q < ba[k] + bnum[k]; q++) {
+          mmax = std::max(mmax, (double)pm[q]);
+          for (int t = 0; t < 2; t++) {
+            int g = gpg[2 * q + t];
+            int side = gb[g] == bb[2 * k] ? 0 : 1;
+            const float* o = gob.data() + 15 * g;
+            for (int cnr = 0; cnr < 8; cnr++) {
+              double sgn[3] = {(cnr & 1) ? 1.0 : -1.0, (cnr & 2) ? 1.0 : -1.0, (cnr & 4) ? 1.0 : -1.0};
+              for (int i = 0; i < 3; i++) {
+                double v = o[i];
+                for (int jj = 0; jj < 3; jj++) v += (double)o[3 + 3 * i + jj] * sgn[jj] * o[12 + jj];
+                lo[side][i] = std::min(lo[side][i], v);
+                hi[side][i] = std::max(hi[side][i], v);
+              }
+            }
+          }
+        }
+        float c[2][3], e[2][3];
+        for (int side = 0; side < 2; side++)
+          for (int i = 0; i < 3; i++) {
+            c[side][i] = (float)(0.5 * (lo[side][i] + hi[side][i]));
+            e[side][i] = (float)(0.5 * (hi[side][i] - lo[side][i]) * (1.0 + 1e-4) + 1e-5);
+          }
+        r[15] = (float)mmax;
+        const float rec[12] = {c[0][0], c[0][1], c[0][2], e[0][0], e[0][1], e[0][2],
+                               c[1][0], c[1][1], c[1][2], e[1][0], e[1][1], e[1][2]};
+        for (int i = 0; i < 12; i++) r[16 + i] = rec[i];
+      }
     }
     m->hf["bpair_rec"] = br;
   }

@@ -246,7 +246,8 @@ enum {
   ST_NEWTON_GRAD, ST_NEWTON_HESS, ST_NEWTON_CHOL, ST_NEWTON_LS, ST_QFRC, ST_EULER, ST_OBSERVE, ST_IO,
   ST_MATVEC, ST_NP_MPR, ST_JACVEC,
   CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
-  CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC, CNT_NP_TRIPS  // event counters, not cycles
+  CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC, CNT_NP_TRIPS, CNT_BROAD_KEEP, CNT_MID_PAIRS,
+  CNT_MID_KEEP  // event counters, not cycles
 };
 template <class Ctx>
 __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {

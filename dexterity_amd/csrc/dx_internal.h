@@ -64,7 +64,7 @@ struct DevModel {
   // bin_cap, vert4 offset, bin4 offset, -}{size, -}{pos, -}{mat 9, center 3, -};
   // gpair_rec [ngpair] = {g1, g2, margin, primitive-pair flag}
   const DXG float4 *geom_rec, *gpair_rec;
-  // culling records (dx_api.hip): geom_crec [ngeom][6], bpair_rec [nbpair][6] float4
+  // culling records (dx_api.hip): geom_crec [ngeom][6], bpair_rec [nbpair][7] float4
   const DXG float4 *geom_crec, *bpair_rec;
   // tree records (dx_api.hip): body_rec [nbody][8] float4, dof_rec [nv][2] float4
   const DXG float4 *body_rec, *dof_rec;
@@ -112,7 +112,7 @@ struct DevBatch {
   unsigned epoch, qbase;
   int* qerr;
 };
-#define DX_NSTAGE 32
+#define DX_NSTAGE 40
 
 // Offsets (in 4-byte words) of every per-env LDS array.
 struct Lds {

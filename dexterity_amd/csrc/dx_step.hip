@@ -595,6 +595,16 @@ __device__ __forceinline__ bool obb_overlap(const float* o1, const float* xp1, c
   return true;
 }
 
+// Overlap of two boxes given in their bodies' frames (axes = body axes): centre c,
+// half extents e, body pose (xp, xm); the 15-axis SAT of obb_overlap.
+__device__ __forceinline__ bool box_overlap(const float* c1, const float* e1, const float* xp1, const float* xm1,
+                                            const float* c2, const float* e2, const float* xp2, const float* xm2,
+                                            float margin) {
+  const float o1[15] = {c1[0], c1[1], c1[2], 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f, e1[0], e1[1], e1[2]};
+  const float o2[15] = {c2[0], c2[1], c2[2], 1.f, 0.f, 0.f, 0.f, 1.f, 0.f, 0.f, 0.f, 1.f, e2[0], e2[1], e2[2]};
+  return obb_overlap(o1, xp1, xm1, o2, xp2, xm2, margin);
+}
+
 // Appends one contact record (called by a single lane).
 __device__ __forceinline__ void write_contact(float* con, int slot, const float* pos, const float* n, float dist, int gp) {
   float* r = con + DX_CON_STRIDE * slot;
@@ -744,32 +754,69 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   if (c.disable_contact) return;
   float* xpos = c.f(c.L.xpos);
   float* xmat = c.f(c.L.xmat);
-  // 1. body-pair cull -> cand[0..nbc) body-pair ids, pref[0..nbc] prefix of geom-pair counts
+  // 1. body-pair cull -> cand[0..nbc) body-pair ids, pref[0..nbc] prefix of geom-pair counts.
+  // Bounding spheres (and planes) over all body pairs, lane per pair; the survivors go
+  // to a list, and one pass over the list applies the box test (dx_api.hip bpair_rec)
+  // and compacts: the box SAT then runs on ~1 chunk of survivors, not on every chunk.
   int half = cmax / 3;
   int* pref = cand + half;
   int nbc = 0, ngp = 0;
+  int* sl = (int*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP * MP_WORDS);  // the pair-record area, unused yet
+  const int slcap = 4 * (cmax - 2 * half);
+  int nsl = 0;
+  auto flush = [&]() {
+    for (int b0 = 0; b0 < nsl; b0 += DX_WAVE) {
+      const int k = b0 + LANE;
+      bool keep = false;
+      int cnt = 0, adr = 0;
+      if (k < nsl) {
+        const int e = sl[k];
+        const DXG float4* R = m.bpair_rec + 7 * (e & 0x7fffffff);
+        const float4 r0 = R[0], r3 = R[3], r4 = R[4], r5 = R[5], r6 = R[6];
+        keep = true;
+        if (e < 0) {  // sphere-tested pair: boxes around its geoms' OBBs
+          const int b1 = __float_as_int(r0.x), b2 = __float_as_int(r0.y);
+          const float b1c[3] = {r4.x, r4.y, r4.z}, b1e[3] = {r4.w, r5.x, r5.y};
+          const float b2c[3] = {r5.z, r5.w, r6.x}, b2e[3] = {r6.y, r6.z, r6.w};
+          keep = box_overlap(b1c, b1e, xpos + 3 * b1, xmat + 9 * b1, b2c, b2e, xpos + 3 * b2, xmat + 9 * b2, r3.w);
+        }
+        adr = __float_as_int(r0.z);
+        cnt = keep ? __float_as_int(r0.w) : 0;
+      }
+      uint64_t mask = __ballot(keep);
+      int pos = __popcll(mask & ((1ull << LANE) - 1ull));
+      int inc = wave_incl_scan(cnt);
+      int off = inc - cnt;
+      if (keep && nbc + pos < half) {
+        cand[nbc + pos] = adr;  // first geom pair of the body pair
+        pref[nbc + pos] = ngp + off;
+      }
+      nbc += __popcll(mask);
+      ngp += __builtin_amdgcn_readlane(inc, 63);
+    }
+    nsl = 0;
+    SYNC();
+  };
   // the next chunk's records are loaded while this chunk is tested (one memory
   // round trip in flight across chunk boundaries)
   float4 nx[6];
   {
     const int bp0 = min(LANE, c.nbpair - 1);
-    const DXG float4* R = m.bpair_rec + 6 * max(bp0, 0);
+    const DXG float4* R = m.bpair_rec + 7 * max(bp0, 0);
 #pragma unroll
     for (int k = 0; k < 6; k++) nx[k] = R[k];
   }
   for (int base = 0; base < c.nbpair; base += DX_WAVE) {
     int bp = base + LANE;
-    bool keep = false;
-    int cnt = 0, adr = 0;
+    bool keep = false, box = false;
     const float4 r0 = nx[0], s1 = nx[1], s2 = nx[2], r3 = nx[3], r4 = nx[4], r5 = nx[5];
     if (base + DX_WAVE < c.nbpair) {
-      const DXG float4* R = m.bpair_rec + 6 * min(base + DX_WAVE + LANE, c.nbpair - 1);
+      const DXG float4* R = m.bpair_rec + 7 * min(base + DX_WAVE + LANE, c.nbpair - 1);
 #pragma unroll
       for (int k = 0; k < 6; k++) nx[k] = R[k];
     }
     if (bp < c.nbpair) {
       int b1 = __float_as_int(r0.x), b2 = __float_as_int(r0.y);
-      adr = __float_as_int(r0.z);
       keep = true;
       if (watch_only) keep = (b2 == wb || b1 == wb) && (m.geom_bodyid[wg] == b1 || m.geom_bodyid[wg] == b2);
       float mg = r3.x;
@@ -793,21 +840,18 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
           matvec3(c1, xmat + 9 * b1, s1v);
           for (int k = 0; k < 3; k++) c1[k] += xpos[3 * b1 + k];
           keep = sphere_overlap(c1, s1.w, c2, s2.w, mg);
+          box = true;
         }
       }
-      cnt = keep ? __float_as_int(r0.w) : 0;
     }
     uint64_t mask = __ballot(keep);
     int pos = __popcll(mask & ((1ull << LANE) - 1ull));
-    int inc = wave_incl_scan(cnt);
-    int off = inc - cnt;
-    if (keep && nbc + pos < half) {
-      cand[nbc + pos] = adr;  // first geom pair of the body pair
-      pref[nbc + pos] = ngp + off;
-    }
-    nbc += __popcll(mask);
-    ngp += __builtin_amdgcn_readlane(inc, 63);
+    if (keep) sl[nsl + pos] = box ? (bp | (int)0x80000000) : bp;
+    nsl += __popcll(mask);
+    SYNC();
+    if (nsl > slcap - DX_WAVE) flush();
   }
+  flush();
   if (nbc > half) { nbc = half; if (LANE == 0) I[I_OVF] |= 1; }
   if (LANE == 0) pref[nbc] = ngp;
   SYNC();
@@ -881,6 +925,9 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     ng = gmax;
   }
   if (LANE == 0) I[I_NCAND] = ng;
+  stage_count(c, CNT_BROAD_KEEP, nbc);
+  stage_count(c, CNT_MID_PAIRS, total);
+  stage_count(c, CNT_MID_KEEP, ng);
   SYNC();
   stage_mark(c, ST_MID);
   // 3. narrowphase.  DX_NGRP lane groups walk the candidate list in this one loop,

@@ -238,7 +238,7 @@ int dx_timing_enable(dx_batch* b, int enable);
 int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
 /* Per-stage shader-clock accounting inside the fused step kernel (diagnostics):
  * out[k] = summed s_memtime cycles of stage k over all envs since the last read
- * (n < nenv * 32), or out[env * 32 + k] per env (n >= nenv * 32). */
+ * (n < nenv * 40), or out[env * 40 + k] per env (n >= nenv * 40). */
 int dx_stage_timing(dx_batch* b, int enable);
 int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n);
 /* Test hook: overwrites the LDS of every CU on `device` with NaN patterns. */
