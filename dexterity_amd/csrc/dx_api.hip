@@ -175,6 +175,8 @@ static void build_hull_bins(dx_model* m) {
   std::vector<int> bn(std::max(nmesh, 1), 0), bcap(std::max(nmesh, 1), 0), badr(std::max(nmesh, 1), 0);
   std::vector<float> b4;
   static const int kN[] = {4, 6, 8, 12, 16};
+  const char* env_minn = getenv("DX_HULL_BIN_MINN");  // (experiments: finer cube maps)
+  const int minn = env_minn ? atoi(env_minn) : 4;
   for (int i = 0; i < nmesh; i++) {
     int nv = num[i];
     if (nv <= 64) continue;
@@ -185,6 +187,7 @@ static void build_hull_bins(dx_model* m) {
       R = std::max(R, std::sqrt(V[3 * j] * V[3 * j] + V[3 * j + 1] * V[3 * j + 1] + V[3 * j + 2] * V[3 * j + 2]));
     }
     for (int n : kN) {
+      if (n < minn) continue;
       std::vector<std::vector<int>> cells(6 * n * n);
       int cap = 0;
       for (int f = 0; f < 6 && cap <= 64; f++)
