@@ -739,21 +739,44 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
   }
   SYNC();
   const int i = l;
-  // forward: L y = b (lane i holds b_i, then y_i)
+  // forward: L y = b (lane i holds b_i, then y_i).  L's entries come from LDS eight
+  // columns at a time, loaded before the eight dependent steps that use them.
   float y = 0.f;
-  for (int k = 0; k < n; k++) {
-    const float lik = i > k && i < n ? T[ti(i) + k] : 0.f;
-    const float yk = rl(b, k) * rl(dinv, k);
-    y = wl(y, yk, k);
-    b = fmaf(-lik, yk, b);
+  for (int k0 = 0; k0 < n; k0 += 8) {
+    float lc[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = k0 + u;
+      lc[u] = i > k && i < n ? T[ti(i) + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = min(k0 + u, 63);
+      const float yk = rl(b, k) * rl(dinv, k);
+      if (k0 + u < n) {
+        y = wl(y, yk, k);
+        b = fmaf(-lc[u], yk, b);
+      }
+    }
   }
   // backward: L^T x = y
   float xo = 0.f;
-  for (int k = n - 1; k >= 0; k--) {
-    const float lki = i < k ? T[ti(k) + i] : 0.f;
-    const float xk = rl(y, k) * rl(dinv, k);
-    xo = wl(xo, xk, k);
-    y = fmaf(-lki, xk, y);
+  for (int k1 = n - 1; k1 >= 0; k1 -= 8) {
+    float lc[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = k1 - u;
+      lc[u] = k >= 0 && i < k ? T[ti(k) + i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int k = max(k1 - u, 0);
+      const float xk = rl(y, k) * rl(dinv, k);
+      if (k1 - u >= 0) {
+        xo = wl(xo, xk, k);
+        y = fmaf(-lc[u], xk, y);
+      }
+    }
   }
   SYNC();
   if (i < n) x[i] = xo;
