@@ -1420,13 +1420,19 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
     if (LANE < n) y[LANE] = s;
     return;
   }
-  for (int i = LANE; i < n; i += DX_WAVE) {
-    float s = 0;
-    const float* row = M + ti(i);
-    for (int k = 0; k <= i; k++) s += row[k] * x[k];
-    for (int k = i + 1; k < n; k++) s += M[ti(k) + i] * x[k];
-    y[i] = s;
+  // n <= 64 (DX_MAX_NV): the same unrolled gather over 64 columns, every read
+  // independent of the running sum (the per-lane loops this replaced waited on LDS
+  // once per column)
+  const int i = min(LANE, n - 1);
+  float s = 0;
+#pragma unroll
+  for (int k = 0; k < 64; k++) {
+    int a = max(i, k), b = min(i, k);
+    float xk = k < n ? x[k] : 0.f;
+    float mk = k < n ? M[ti(a) + b] : 0.f;
+    s = fmaf(mk, xk, s);
   }
+  if (LANE < n) y[LANE] = s;
 }
 
 // J x for every row -> out[r]; uses cq as contact-frame scratch.  The contact
