@@ -619,11 +619,11 @@ __device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const D
     const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;  // panel: A[j][hi], B[hi][j]
     C = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C, 0, 0, 0);
   }
-  // strictly-lower row -> T (packed)
+  // strictly-lower row -> T (packed).  Lanes with nothing to store write T[0], the
+  // (0, 0) diagonal slot, which the substitutions never read: no exec-mask branches.
   const int i = l;
 #pragma unroll
-  for (int k = 0; k < 32; k++)
-    if (k < i && i < n) T[ti(i) + k] = Lr[k];
+  for (int k = 0; k < 32; k++) T[(k < i && i < n) ? ti(i) + k : 0] = Lr[k];
   // forward: L y = b
   float y = 0.f;
 #pragma unroll
@@ -705,12 +705,11 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
     dinv = wl(dinv, i22, k + 1);
     const float lk = rk * i11, lk1 = (rk1 - lk * l21) * i22;  // L[j][k], L[j][k+1]
     const float mk = sk * i11, mk1 = (sk1 - mk * l21) * i22;  // L[32+j][k], L[32+j][k+1]
-    if (hi == 0) {
-      if (j > k) T[ti(j) + k] = lk;
-      if (j > k + 1) T[ti(j) + k + 1] = lk1;
-    } else if (32 + j < n) {
-      T[ti(32 + j) + k] = mk;
-      T[ti(32 + j) + k + 1] = mk1;
+    {  // L out (lanes with nothing to store write the never-read diagonal slot T[0])
+      const int r = hi ? 32 + j : j;
+      const bool v0 = hi ? r < n : j > k, v1 = hi ? r < n : j > k + 1;
+      T[v0 ? ti(r) + k : 0] = hi ? mk : lk;
+      T[v1 ? ti(r) + k + 1 : 0] = hi ? mk1 : lk1;
     }
     const float pa = j > k + 1 ? (hi ? lk1 : lk) : 0.f;
     const float pb = hi ? mk1 : mk;
@@ -730,9 +729,10 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
     dinv = wl(dinv, i11, 32 + k);
     dinv = wl(dinv, i22, 32 + k + 1);
     const float lk = rk * i11, lk1 = (rk1 - lk * l21) * i22;  // L[32+j][32+k], L[32+j][32+k+1]
-    if (hi == 0 && 32 + j < n) {
-      if (j > k) T[ti(32 + j) + 32 + k] = lk;
-      if (j > k + 1) T[ti(32 + j) + 32 + k + 1] = lk1;
+    {
+      const bool ok = hi == 0 && 32 + j < n;
+      T[ok && j > k ? ti(32 + j) + 32 + k : 0] = lk;
+      T[ok && j > k + 1 ? ti(32 + j) + 32 + k + 1 : 0] = lk1;
     }
     const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;
     C22 = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C22, 0, 0, 0);
