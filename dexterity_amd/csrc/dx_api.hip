@@ -1365,7 +1365,7 @@ static int env_run(dx_env* e, const float* action) {
   if (e->P.kind == DX_KIND_REACH)
     if (int rc = launch_step(b, 1, 2)) return rc;
   if (int rc = launch_step(b, e->nsub, 0)) return rc;
-  hipLaunchKernelGGL(dx_task_post_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db);
+  hipLaunchKernelGGL(dx_task_post_kernel, dim3((e->P.nenv + 3) / 4), dim3(256), 0, b->stream, e->P, e->S, b->db);  // a wave per env
   HIPCHK(hipGetLastError());
   return 0;
 }

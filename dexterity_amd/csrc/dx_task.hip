@@ -116,8 +116,11 @@ __device__ __forceinline__ float tanh_squared(float x, float margin) {
   return t * t;
 }
 
+// One 64-lane wave per env: lane 0 does the bookkeeping, all lanes write the
+// observation (coalesced; a thread per env wrote 123 floats 492 B apart).
 extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B) {
-  int env = blockIdx.x * blockDim.x + threadIdx.x;
+  const int env = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (env >= P.nenv) return;
   const float* q = B.qpos + (size_t)env * P.nq;
   const float* v = B.qvel + (size_t)env * P.nv;
@@ -145,74 +148,92 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
     dist = quat_distance(g, cur);
     all_close = dist <= P.threshold;
   }
-  bool reset = S.skip[env] != 0;
-  if (reset) {
-    S.step_type[env] = ST_FIRST;
-    S.reward[env] = 0;
-    S.discount[env] = 1;
-  } else {
-    // GoalTask.after_step (task.py:167-185)
-    float time = B.time[env];
-    if (all_close) {
-      S.counter[env] += 1;
-      if (!S.registered[env]) { S.successes[env] += 1; S.registered[env] = 1; }
-    } else if (P.max_time > 0 && time - S.solve_start[env] > P.max_time) {
-      S.exceeded[env] = 1;
-    }
-    // ReOrient.after_step: fall detection (prop-ground contact at the new state)
-    int failure = !reach && P.fall_termination && B.watch && B.watch[env];
-    S.failure[env] = failure;
-    bool success_done = S.successes[env] >= P.successes_needed;
-    bool terminate = success_done || S.exceeded[env] || failure;
-    float r;
-    if (reach) {
-      r = rsum / (float)P.ntips;
+  if (lane == 0) {
+    bool reset = S.skip[env] != 0;
+    if (reset) {
+      S.step_type[env] = ST_FIRST;
+      S.reward[env] = 0;
+      S.discount[env] = 1;
     } else {
-      // reorient.py:238-284: 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
-      float cn = 0;
-      for (int i = 0; i < P.nu; i++) {
-        float c = B.ctrl[(size_t)env * P.nu + i];
-        cn += c * c;
+      // GoalTask.after_step (task.py:167-185)
+      float time = B.time[env];
+      if (all_close) {
+        S.counter[env] += 1;
+        if (!S.registered[env]) { S.successes[env] += 1; S.registered[env] = 1; }
+      } else if (P.max_time > 0 && time - S.solve_start[env] > P.max_time) {
+        S.exceeded[env] = 1;
       }
-      r = P.w_orient * (1.0f / (dist + P.eps)) + P.w_success * (dist <= P.threshold ? 1.0f : 0.0f) + P.w_action * cn;
+      // ReOrient.after_step: fall detection (prop-ground contact at the new state)
+      int failure = !reach && P.fall_termination && B.watch && B.watch[env];
+      S.failure[env] = failure;
+      bool success_done = S.successes[env] >= P.successes_needed;
+      bool terminate = success_done || S.exceeded[env] || failure;
+      float r;
+      if (reach) {
+        r = rsum / (float)P.ntips;
+      } else {
+        // reorient.py:238-284: 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
+        float cn = 0;
+        for (int i = 0; i < P.nu; i++) {
+          float c = B.ctrl[(size_t)env * P.nu + i];
+          cn += c * c;
+        }
+        r = P.w_orient * (1.0f / (dist + P.eps)) + P.w_success * (dist <= P.threshold ? 1.0f : 0.0f) + P.w_action * cn;
+      }
+      S.reward[env] = r;
+      // discount (reorient.py:222-225, task.py:195-204)
+      S.discount[env] = failure ? 1.0f : (success_done ? 0.0f : 1.0f);
+      S.step_type[env] = terminate ? ST_LAST : ST_MID;
     }
-    S.reward[env] = r;
-    // discount (reorient.py:222-225, task.py:195-204)
-    S.discount[env] = failure ? 1.0f : (success_done ? 0.0f : 1.0f);
-    S.step_type[env] = terminate ? ST_LAST : ST_MID;
   }
   // observation (STATE_ONLY), flat layout:
   // [sin/cos(qpos_hand) 2*hand_nq | qvel_hand | tip pos 3*ntips | tip linvel 3*ntips |
   //  reorient: prop pos 3 | prop quat 4 | prop linvel 3 | prop angvel 3 | target quat 4 |
   //  goal (4 quaternion, or 3*ntips fingertip positions for reach)]
   float* o = S.obs + (size_t)env * P.obs_dim;
-  int k = 0;
-  for (int i = 0; i < P.hand_nq; i++) {
-    float s, c;
-    sincosf(q[i], &s, &c);
-    o[k++] = s;
-    o[k++] = c;
+  const float n = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2] + cur[3] * cur[3]);
+  for (int k = lane; k < P.obs_dim; k += 64) {
+    int e = k;
+    float val = 0.f;
+    if (e < 2 * P.hand_nq) {
+      float sn, cs;
+      sincosf(q[e >> 1], &sn, &cs);
+      val = (e & 1) ? cs : sn;
+    } else if ((e -= 2 * P.hand_nq) < P.hand_nv) {
+      val = v[e];
+    } else if ((e -= P.hand_nv) < 3 * P.ntips) {
+      val = B.site_xpos[((size_t)env * P.nsite + P.tip_sites[e / 3]) * 3 + e % 3];
+    } else if ((e -= 3 * P.ntips) < 3 * P.ntips) {
+      val = B.site_vel[((size_t)env * P.nsite + P.tip_sites[e / 3]) * 6 + e % 3];
+    } else {
+      e -= 3 * P.ntips;
+      if (P.prop_qadr >= 0) {
+        if (e < 3) {
+          val = q[P.prop_qadr + e];
+        } else if (e < 7) {
+          val = cur[e - 3] / n;
+        } else if (e < 10) {
+          val = v[P.prop_dadr + e - 7];
+        } else if (e < 13) {
+          // frameangvel: world-frame angular velocity = R(quat) * local omega
+          const float w0 = cur[0] / n, x = cur[1] / n, y = cur[2] / n, z = cur[3] / n;
+          const float* wl = v + P.prop_dadr + 3;
+          const int r = e - 10;
+          const float R0 = r == 0 ? 1 - 2 * (y * y + z * z) : (r == 1 ? 2 * (x * y + w0 * z) : 2 * (x * z - w0 * y));
+          const float R1 = r == 0 ? 2 * (x * y - w0 * z) : (r == 1 ? 1 - 2 * (x * x + z * z) : 2 * (y * z + w0 * x));
+          const float R2 = r == 0 ? 2 * (x * z + w0 * y) : (r == 1 ? 2 * (y * z - w0 * x) : 1 - 2 * (x * x + y * y));
+          val = R0 * wl[0] + R1 * wl[1] + R2 * wl[2];
+        } else if (e < 17) {
+          val = g[e - 13];  // target_prop/orientation (hint cube = goal)
+        } else {
+          val = g[e - 17];  // goal_state
+        }
+      } else {
+        val = g[e];  // goal_state
+      }
+    }
+    o[k] = val;
   }
-  for (int i = 0; i < P.hand_nv; i++) o[k++] = v[i];
-  for (int t = 0; t < P.ntips; t++)
-    for (int e = 0; e < 3; e++) o[k++] = B.site_xpos[((size_t)env * P.nsite + P.tip_sites[t]) * 3 + e];
-  for (int t = 0; t < P.ntips; t++)
-    for (int e = 0; e < 3; e++) o[k++] = B.site_vel[((size_t)env * P.nsite + P.tip_sites[t]) * 6 + e];
-  if (P.prop_qadr >= 0) {
-    for (int e = 0; e < 3; e++) o[k++] = q[P.prop_qadr + e];
-    float n = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2] + cur[3] * cur[3]);
-    for (int e = 0; e < 4; e++) o[k++] = cur[e] / n;
-    for (int e = 0; e < 3; e++) o[k++] = v[P.prop_dadr + e];
-    // frameangvel: world-frame angular velocity = R(quat) * local omega
-    float w0 = cur[0] / n, x = cur[1] / n, y = cur[2] / n, z = cur[3] / n;
-    float R[9] = {1 - 2 * (y * y + z * z), 2 * (x * y - w0 * z), 2 * (x * z + w0 * y),
-                  2 * (x * y + w0 * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w0 * x),
-                  2 * (x * z - w0 * y), 2 * (y * z + w0 * x), 1 - 2 * (x * x + y * y)};
-    const float* wl = v + P.prop_dadr + 3;
-    for (int e = 0; e < 3; e++) o[k++] = R[3 * e] * wl[0] + R[3 * e + 1] * wl[1] + R[3 * e + 2] * wl[2];
-    for (int e = 0; e < 4; e++) o[k++] = g[e];  // target_prop/orientation (hint cube = goal)
-  }
-  for (int e = 0; e < P.goal_dim; e++) o[k++] = g[e];  // goal_state
 }
 
 // Uniform random actions within the actuator ctrlrange: the synthetic agent of
