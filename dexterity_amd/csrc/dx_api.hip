@@ -814,6 +814,7 @@ struct dx_batch {
   DevBatch db;
   int spec;  // specialized step kernel (dx_specs.inc) or -1 for the generic one
   bool queue;  // mode-0 steps through the substep queue
+  int* watch_list = nullptr;  // device copy of DevBatch::watch_pairs
   int slots;   // persistent workgroups of a queued launch
   float* xfrc;
   std::vector<void*> allocs;
@@ -989,10 +990,39 @@ extern "C" int dx_set_xfrc(dx_batch* b, const float* xfrc, int32_t nbody) {
   return 0;
 }
 
+static int set_watch_pairs(dx_batch* b);
+
 extern "C" int dx_set_ground_geom(dx_batch* b, int32_t geom) {
   if (!b) return fail(DX_EINVAL, "null batch");
   if (geom >= b->dm.ngeom) return fail(DX_EINVAL, "geom out of range");
   b->db.watch_geom = geom;
+  return set_watch_pairs(b);
+}
+
+// The body pairs the watch test of the observation pass has to look at: those with
+// `body` on one side and the watched geom's body on the other (as filtered in
+// dx_step.hip collision), listed once here instead of filtered per env and step.
+static int set_watch_pairs(dx_batch* b) {
+  DevBatch& B = b->db;
+  std::vector<int> list;
+  if (B.watch_geom >= 0 && B.watch_body >= 0) {
+    const auto& bb = b->model->hi.at("bpair_body");
+    const int gbody = b->model->hi.at("geom_bodyid")[B.watch_geom];
+    for (int k = 0; k < b->dm.nbpair; k++) {
+      const int b1 = bb[2 * k], b2 = bb[2 * k + 1];
+      if ((b1 == B.watch_body || b2 == B.watch_body) && (gbody == b1 || gbody == b2)) list.push_back(k);
+    }
+  }
+  if (!b->watch_list) {
+    void* p = nullptr;
+    if (balloc(b, &p, (size_t)std::max(b->dm.nbpair, 1) * 4)) return DX_EHIP;
+    b->watch_list = (int*)p;
+  }
+  if (!list.empty())
+    HIPCHK(hipMemcpyAsync(b->watch_list, list.data(), list.size() * 4, hipMemcpyHostToDevice, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  B.watch_pairs = b->watch_list;
+  B.watch_npairs = (int)list.size();
   return 0;
 }
 
@@ -1001,7 +1031,7 @@ extern "C" int dx_set_watch(dx_batch* b, int32_t geom, int32_t body) {
   if (geom >= b->dm.ngeom || body >= b->dm.nbody) return fail(DX_EINVAL, "watch out of range");
   b->db.watch_geom = geom;
   b->db.watch_body = body;
-  return 0;
+  return set_watch_pairs(b);
 }
 
 static void timing_begin(dx_batch* b, hipEvent_t* start);

@@ -95,6 +95,8 @@ struct DevBatch {
   const float* xfrc;  // [nbody*6], shared by all envs (may be null)
   const int* skip;    // [nenv] nonzero: env was just reset, observe only (may be null)
   int watch_geom, watch_body;
+  const int* watch_pairs;  // body pairs that can hold a watched contact (dx_set_watch), or null
+  int watch_npairs;
   // debug (null when disabled)
   float *dbg_qacc_smooth, *dbg_qfrc_smooth, *dbg_M, *dbg_con;
   int* dbg_nefc;

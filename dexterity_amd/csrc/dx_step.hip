@@ -746,7 +746,8 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
 // (whole wave per pair).  Writes contact records into LDS.
 // watch_only: only pairs containing geom `wg` and a geom of body `wb` (observation pass).
 template <class Ctx>
-__device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb) {
+__device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, int wb, const int* wlist = nullptr,
+                                          int wn = 0) {
   const DevModel& m = c.mdl();
   int* I = c.I;
   int* cand = (int*)c.f(c.L.cand);
@@ -802,18 +803,22 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   // the next chunk's records are loaded while this chunk is tested (one memory
   // round trip in flight across chunk boundaries)
   float4 nx[6];
+  // the observation pass's watch test walks only the body pairs that can hold the
+  // watched contact (dx_set_watch builds that list on the host)
+  const int nloop = (watch_only && wlist) ? wn : c.nbpair;
+  auto bpidx = [&](int i) { return (watch_only && wlist) ? wlist[i] : i; };
   {
-    const int bp0 = min(LANE, c.nbpair - 1);
-    const DXG float4* R = m.bpair_rec + 7 * max(bp0, 0);
+    const int i0 = max(min(LANE, nloop - 1), 0);
+    const DXG float4* R = m.bpair_rec + 7 * (nloop > 0 ? bpidx(i0) : 0);
 #pragma unroll
     for (int k = 0; k < 6; k++) nx[k] = R[k];
   }
-  for (int base = 0; base < c.nbpair; base += DX_WAVE) {
-    int bp = base + LANE;
+  for (int base = 0; base < nloop; base += DX_WAVE) {
+    const int bp = base + LANE < nloop ? bpidx(base + LANE) : c.nbpair;
     bool keep = false, box = false;
     const float4 r0 = nx[0], s1 = nx[1], s2 = nx[2], r3 = nx[3], r4 = nx[4], r5 = nx[5];
-    if (base + DX_WAVE < c.nbpair) {
-      const DXG float4* R = m.bpair_rec + 7 * min(base + DX_WAVE + LANE, c.nbpair - 1);
+    if (base + DX_WAVE < nloop) {
+      const DXG float4* R = m.bpair_rec + 7 * bpidx(min(base + DX_WAVE + LANE, nloop - 1));
 #pragma unroll
       for (int k = 0; k < 6; k++) nx[k] = R[k];
     }
@@ -2034,7 +2039,7 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
   for (int k = LANE; k < 4 * c.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * c.nbody + k] = xq[k];
   SYNC();
   if (B.watch_geom >= 0 && B.watch) {
-    collision(c, 1, B.watch_geom, B.watch_body);
+    collision(c, 1, B.watch_geom, B.watch_body, B.watch_pairs, B.watch_npairs);
     int n = c.I[I_NCON];
     const float* con = c.f(c.L.con);
     int hit = 0;

@@ -323,6 +323,53 @@ def test_full_batch_properties(gpu):
     env.close()
 
 
+def test_ground_contact_watch_matches_oracle(gpu, oracle_mod, reorient_setup):
+    """DX_GROUND_CONTACT (ReOrient._is_prop_fallen, reorient.py:229-235 ->
+    has_collision, utils/mujoco_collisions.py:95-119: a prop-ground contact with
+    dist <= 1e-8) against the oracle's contact list, for cubes resting on, sunk into,
+    hovering over and far above the ground, and on the palm."""
+    from dexterity_amd import manipulation
+
+    cm, xfrc, om, states, model = reorient_setup
+    task = manipulation.ReOrient()
+    ground, prop_body = task.ground_geom, task.prop_body
+    pq = task.prop_qadr
+    rs = np.random.RandomState(4)
+    qs = []
+    for z in (0.0199, 0.0195, 0.02, 0.0201, 0.021, 0.03, 0.1):
+        for _ in range(3):
+            q = cm.qpos0.copy()
+            q[pq:pq + 3] = [0.3 + rs.uniform(-0.05, 0.05), 0.3 + rs.uniform(-0.05, 0.05), z]
+            if z < 0.05:  # axis-aligned: a face (four corners) on the ground
+                q[pq + 3:pq + 7] = [1, 0, 0, 0]
+            else:
+                qq = rs.randn(4)
+                q[pq + 3:pq + 7] = qq / np.linalg.norm(qq)
+            qs.append(q)
+    qs.append(states[0][0])  # the cube on the palm
+    qs = np.stack(qs)
+    phys = gpu.BatchedPhysics(model, len(qs))
+    phys.set_watch(ground, prop_body)
+    phys.set(_lib.QPOS, qs)
+    phys.forward()
+    flag = phys.get(_lib.GROUND_CONTACT)[:, 0]
+    prop_geoms = {g for g in range(cm.ngeom) if cm.geom_bodyid[g] == prop_body}
+    expect = []
+    for q in qs:
+        d = oracle_mod.OracleData(om)
+        d.qpos[:] = q.astype(np.float32)
+        d.kinematics()
+        hit = False
+        for con in d.contacts():
+            g1, g2 = int(con[13]), int(con[14])
+            if {g1, g2} & {ground} and ({g1, g2} & prop_geoms) and con[12] <= 1e-8:
+                hit = True
+        expect.append(hit)
+    np.testing.assert_array_equal(flag.astype(bool), np.array(expect))
+    assert np.array(expect).any() and not np.array(expect).all()
+    phys.close()
+
+
 def test_substep_queue_matches_per_env_launch(gpu, monkeypatch):
     """The substep queue (one task per env and physics step, state handed over through
     HBM between workgroups, dx_step.hip step_queue) gives bit-identical trajectories to
