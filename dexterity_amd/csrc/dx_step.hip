@@ -1292,72 +1292,89 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
   float* cvel = c.f(c.L.cvel);
   float* cdd = c.f(c.L.cdof_dot);
   float* cinert = c.f(c.L.cinert);
-  float* cacc = c.f(c.L.scr);
-  float* cfrc = cacc + 6 * c.nbody;
-  if (LANE < 6) { cvel[LANE] = 0; cacc[LANE] = LANE < 3 ? 0.f : -m.gravity[LANE - 3]; }
+  float* qs = c.f(c.L.qfrc_smooth);
+  // The tree recursions of mj_comVel / mj_rne are sums over a body's dof chain (the
+  // dofs on its path to the root, dx_api.hip body_chain), so every dof and every body
+  // is computed at once instead of one tree level after another:
+  //   cdof_dot[d] = (sum of cdof[e] qvel[e] over the chain dofs e before d) x cdof[d]
+  //   cvel[b]     = sum over chain(b) of cdof[e] qvel[e]
+  //   cacc[b]     = -gravity + sum over chain(b) of cdof_dot[e] qvel[e]
+  //   qfrc_bias[d] = cdof[d] . (sum of cfrc over the subtree of d's body)
+  //               = sum over the bodies b whose chain holds d of cdof[d] . cfrc[b]
+  // A free joint's rotational dofs see the velocity after its translation only, and
+  // its translational cdof_dot is zero (mj_comVel).
+  for (int d = LANE; d < nv; d += DX_WAVE) {  // lane = dof
+    const float4 d0 = m.dof_rec[2 * d], d1 = m.dof_rec[2 * d + 1];
+    const int tk = __float_as_int(d0.w), k = tk >> 8;
+    const bool fr = (tk & 255) == DXJ_FREE;
+    const uint64_t anc = (uint64_t)(uint32_t)__float_as_int(d1.z) | ((uint64_t)(uint32_t)__float_as_int(d1.w) << 32);
+    uint64_t mask = anc & ((1ull << (fr ? d - k + 3 : d)) - 1ull);  // d - k + 3 <= d + 3 <= 63 (nv <= 64 model check)
+    float cv[6] = {0, 0, 0, 0, 0, 0};
+    while (mask) {
+      const int e = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const float q = qvel[e];
+#pragma unroll
+      for (int x = 0; x < 6; x++) cv[x] += cdof[6 * e + x] * q;
+    }
+    float o[6];
+    cross_motion(o, cv, cdof + 6 * d);
+#pragma unroll
+    for (int x = 0; x < 6; x++) cdd[6 * d + x] = fr && k < 3 ? 0.f : o[x];
+    qs[d] = -d1.y * qvel[d];  // passive damping; bias and actuation are added below
+  }
+  if (LANE < 6) cvel[LANE] = 0;
   SYNC();
-  BodyRec br;
-  const bool act = load_body(c, br);
-  float f6[6] = {0, 0, 0, 0, 0, 0};  // applied wrench of this lane's body (read up front)
-  if (xfrc && act)
-    for (int e = 0; e < 6; e++) f6[e] = xfrc[6 * LANE + e];
-  for (int lv = 1; lv <= c.nlevel; lv++) {
-    if (act && br.depth == lv) {
-      const int b = LANE, p = br.parent;
-      float cv[6], ca[6];
-      for (int e = 0; e < 6; e++) { cv[e] = cvel[6 * p + e]; ca[e] = cacc[6 * p + e]; }
-      for (int jj = 0; jj < br.jn; jj++) {
-        const int j = br.ja + jj;
-        const int da = jj == 0 ? br.jdof : m.jnt_dofadr[j];
-        const int jt = jj == 0 ? br.jtype : m.jnt_type[j];
-        if (jt == DXJ_FREE) {
-          for (int q = 0; q < 3; q++)
-            for (int e = 0; e < 6; e++) cdd[6 * (da + q) + e] = 0;
-          for (int q = 0; q < 3; q++)
-            for (int e = 0; e < 6; e++) cv[e] += cdof[6 * (da + q) + e] * qvel[da + q];
-          for (int q = 3; q < 6; q++) cross_motion(cdd + 6 * (da + q), cv, cdof + 6 * (da + q));
-          for (int q = 3; q < 6; q++)
-            for (int e = 0; e < 6; e++) cv[e] += cdof[6 * (da + q) + e] * qvel[da + q];
-        } else {
-          cross_motion(cdd + 6 * da, cv, cdof + 6 * da);
-          for (int e = 0; e < 6; e++) cv[e] += cdof[6 * da + e] * qvel[da];
-        }
+  {  // lane = body
+    const int b = LANE;
+    const bool act = b >= 1 && b < c.nbody;
+    const uint64_t ch = act ? m.body_chain[b] : 0ull;
+    float cv[6] = {0, 0, 0, 0, 0, 0};
+    float ca[6] = {0, 0, 0, -m.gravity[0], -m.gravity[1], -m.gravity[2]};
+    for (uint64_t mask = ch; mask; mask &= mask - 1) {
+      const int e = __ffsll((long long)mask) - 1;
+      const float q = qvel[e];
+#pragma unroll
+      for (int x = 0; x < 6; x++) {
+        cv[x] += cdof[6 * e + x] * q;
+        ca[x] += cdd[6 * e + x] * q;
       }
-      for (int d = br.dofadr; d >= 0 && d < br.dofadr + br.dofnum; d++)
-        for (int e = 0; e < 6; e++) ca[e] += cdd[6 * d + e] * qvel[d];
-      for (int e = 0; e < 6; e++) { cvel[6 * b + e] = cv[e]; cacc[6 * b + e] = ca[e]; }
+    }
+    if (act) {
+#pragma unroll
+      for (int x = 0; x < 6; x++) cvel[6 * b + x] = cv[x];
       // body force: I a + v x* I v - applied wrench (as com-frame spatial force)
-      float t1[6], t2[6], t3[6];
+      float t1[6], t2[6], t3[6], f[6];
       mul_inert(t1, cinert + 10 * b, ca);
       mul_inert(t2, cinert + 10 * b, cv);
       cross_force(t3, cv, t2);
-      for (int e = 0; e < 6; e++) cfrc[6 * b + e] = t1[e] + t3[e];
-      if (f6[0] != 0 || f6[1] != 0 || f6[2] != 0 || f6[3] != 0 || f6[4] != 0 || f6[5] != 0) {
-        const float* rc = c.f(c.L.rcom) + 3 * br.rootidx;
-        const float* xi = c.f(c.L.xipos) + 3 * b;
-        float off[3] = {xi[0] - rc[0], xi[1] - rc[1], xi[2] - rc[2]};
-        float tq[3];
-        cross3(tq, off, f6);
-        cfrc[6 * b + 0] -= f6[3] + tq[0];
-        cfrc[6 * b + 1] -= f6[4] + tq[1];
-        cfrc[6 * b + 2] -= f6[5] + tq[2];
-        cfrc[6 * b + 3] -= f6[0];
-        cfrc[6 * b + 4] -= f6[1];
-        cfrc[6 * b + 5] -= f6[2];
+#pragma unroll
+      for (int x = 0; x < 6; x++) f[x] = t1[x] + t3[x];
+      if (xfrc) {
+        float f6[6];
+        for (int x = 0; x < 6; x++) f6[x] = xfrc[6 * b + x];
+        if (f6[0] != 0 || f6[1] != 0 || f6[2] != 0 || f6[3] != 0 || f6[4] != 0 || f6[5] != 0) {
+          const int rootidx = __float_as_int(m.body_rec[8 * b + 3].w);
+          const float* rc = c.f(c.L.rcom) + 3 * rootidx;
+          const float* xi = c.f(c.L.xipos) + 3 * b;
+          float off[3] = {xi[0] - rc[0], xi[1] - rc[1], xi[2] - rc[2]};
+          float tq[3];
+          cross3(tq, off, f6);
+          f[0] -= f6[3] + tq[0];
+          f[1] -= f6[4] + tq[1];
+          f[2] -= f6[5] + tq[2];
+          f[3] -= f6[0];
+          f[4] -= f6[1];
+          f[5] -= f6[2];
+        }
+      }
+      // qfrc_smooth = passive - (bias - applied) + actuator: this body's share of
+      // the bias of every dof on its chain
+      for (uint64_t mask = ch; mask; mask &= mask - 1) {
+        const int e = __ffsll((long long)mask) - 1;
+        atomicAdd(qs + e, -dot6(cdof + 6 * e, f));
       }
     }
-    SYNC();
-  }
-  for (int lv = c.nlevel; lv >= 2; lv--) {
-    if (act && br.depth == lv && br.parent > 0)
-      for (int e = 0; e < 6; e++) atomicAdd(cfrc + 6 * br.parent + e, cfrc[6 * LANE + e]);
-    SYNC();
-  }
-  // qfrc_smooth = passive - (bias - applied) + actuator
-  float* qs = c.f(c.L.qfrc_smooth);
-  for (int d = LANE; d < nv; d += DX_WAVE) {
-    const float4 d0 = m.dof_rec[2 * d], d1 = m.dof_rec[2 * d + 1];
-    qs[d] = -d1.y * qvel[d] - dot6(cdof + 6 * d, cfrc + 6 * __float_as_int(d0.x));
   }
   SYNC();
   float* al = c.f(c.L.act_len);
@@ -2000,20 +2017,21 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
   float* qvel = c.f(c.L.qvel);
   float* cdof = c.f(c.L.cdof);
   float* cvel = c.f(c.L.cvel);
-  if (LANE < 6) cvel[LANE] = 0;
-  SYNC();
-  BodyRec br;
-  const bool act = load_body(c, br);
-  for (int lv = 1; lv <= c.nlevel; lv++) {
-    if (act && br.depth == lv) {
-      float cv[6];
-      for (int e = 0; e < 6; e++) cv[e] = cvel[6 * br.parent + e];
-      for (int d = br.dofadr; d >= 0 && d < br.dofadr + br.dofnum; d++)
-        for (int e = 0; e < 6; e++) cv[e] += cdof[6 * d + e] * qvel[d];
-      for (int e = 0; e < 6; e++) cvel[6 * LANE + e] = cv[e];
+  {  // lane = body: cvel as a sum over the body's dof chain (see velocity_stage)
+    const int b = LANE;
+    if (b < c.nbody) {
+      float cv[6] = {0, 0, 0, 0, 0, 0};
+      for (uint64_t mask = b >= 1 ? m.body_chain[b] : 0ull; mask; mask &= mask - 1) {
+        const int e = __ffsll((long long)mask) - 1;
+        const float q = qvel[e];
+#pragma unroll
+        for (int x = 0; x < 6; x++) cv[x] += cdof[6 * e + x] * q;
+      }
+#pragma unroll
+      for (int x = 0; x < 6; x++) cvel[6 * b + x] = cv[x];
     }
-    SYNC();
   }
+  SYNC();
   float* xpos = c.f(c.L.xpos);
   float* xmat = c.f(c.L.xmat);
   float* rcom = c.f(c.L.rcom);
