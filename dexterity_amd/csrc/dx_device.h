@@ -301,6 +301,14 @@ __device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
   return act;
 }
 
+// Forward kinematics (mj_kinematics) as chain compositions instead of one tree level
+// after another.  Phase 1 (lane = body, all bodies at once): the body's pose in its
+// parent's frame, L_b = body offset o joint rotations (the sincos / normalise work),
+// as an 8-float record {pos, parent, quat} in the xmat slots, plus every joint's
+// anchor/axis in the body's own frame.  Phase 2: x_b = L_root o ... o L_parent o L_b,
+// walking the parent links upward (p <- L_a.pos + L_a.rot p, q <- L_a.quat q): a
+// chain of cheap compositions with no barrier per level.  Phase 3: rotation matrix,
+// inertial frame, joint anchors and axes in the world frame.
 template <class Ctx>
 __device__ __forceinline__ void kinematics(const Ctx& c) {
   const DevModel& m = c.mdl();
@@ -313,72 +321,128 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
   float* xaxis = c.f(c.L.xaxis);
   BodyRec br;
   const bool act = load_body(c, br);
+  const int b = LANE, ja = br.ja, jn = br.jn;
+  const bool fr = act && jn > 0 && br.jtype == DXJ_FREE;
+  float lp[3] = {br.pos[0], br.pos[1], br.pos[2]};
+  float lq[4] = {br.quat[0], br.quat[1], br.quat[2], br.quat[3]};
+  if (act) {
+    if (fr) {
+      const float* q = qpos + br.qadr;
+      lp[0] = q[0]; lp[1] = q[1]; lp[2] = q[2];
+      lq[0] = q[3]; lq[1] = q[4]; lq[2] = q[5]; lq[3] = q[6];
+      quatnorm(lq);
+    } else {
+      for (int jj = 0; jj < jn; jj++) {
+        const int j = ja + jj;
+        float jp[3], ja3[3], q0;
+        int qa;
+        if (jj == 0) {
+          for (int k = 0; k < 3; k++) { jp[k] = br.jpos[k]; ja3[k] = br.jaxis[k]; }
+          qa = br.qadr;
+          q0 = br.q0;
+        } else {
+          for (int k = 0; k < 3; k++) { jp[k] = m.jnt_pos[3 * j + k]; ja3[k] = m.jnt_axis[3 * j + k]; }
+          qa = m.jnt_qposadr[j];
+          q0 = m.qpos0[qa];
+        }
+        float R[9], t[3];
+        quat2mat(R, lq);
+        matvec3(t, R, jp);
+        const float anc[3] = {t[0] + lp[0], t[1] + lp[1], t[2] + lp[2]};
+        if (jj + 1 < jn) {  // anchor / axis in the parent frame, moved to the body frame below
+          float ax[3];
+          matvec3(ax, R, ja3);
+          for (int k = 0; k < 3; k++) { xanchor[3 * j + k] = anc[k]; xaxis[3 * j + k] = ax[k]; }
+        }
+        float sn, co;
+        sincosf(0.5f * (qpos[qa] - q0), &sn, &co);
+        const float ql[4] = {co, ja3[0] * sn, ja3[1] * sn, ja3[2] * sn};
+        quatmul(lq, lq, ql);
+        quatnorm(lq);
+        quat2mat(R, lq);
+        matvec3(t, R, jp);
+        lp[0] = anc[0] - t[0]; lp[1] = anc[1] - t[1]; lp[2] = anc[2] - t[2];
+      }
+      if (jn > 1) {  // all but the last joint: parent frame -> body frame (L_b^-1)
+        float R[9];
+        quat2mat(R, lq);
+        for (int jj = 0; jj + 1 < jn; jj++) {
+          const int j = ja + jj;
+          float d[3] = {xanchor[3 * j] - lp[0], xanchor[3 * j + 1] - lp[1], xanchor[3 * j + 2] - lp[2]};
+          float ab[3], xb[3];
+          mattvec3(ab, R, d);
+          mattvec3(xb, R, xaxis + 3 * j);
+          for (int k = 0; k < 3; k++) { xanchor[3 * j + k] = ab[k]; xaxis[3 * j + k] = xb[k]; }
+        }
+      }
+    }
+    float* rec = xmat + 9 * b;
+    rec[0] = lp[0]; rec[1] = lp[1]; rec[2] = lp[2];
+    rec[3] = __int_as_float(br.parent);
+    rec[4] = lq[0]; rec[5] = lq[1]; rec[6] = lq[2]; rec[7] = lq[3];
+  }
+  SYNC();
+  float xp[3] = {lp[0], lp[1], lp[2]}, xq[4] = {lq[0], lq[1], lq[2], lq[3]};
+  if (act) {
+    int a = br.parent;
+    while (a > 0) {
+      const float* r = xmat + 9 * a;
+      const float ap[3] = {r[0], r[1], r[2]};
+      const int an = __float_as_int(r[3]);
+      const float aq[4] = {r[4], r[5], r[6], r[7]};
+      // xp <- ap + rot(aq) xp ; xq <- aq xq
+      float t[3];
+      t[0] = 2.f * (aq[2] * xp[2] - aq[3] * xp[1]);
+      t[1] = 2.f * (aq[3] * xp[0] - aq[1] * xp[2]);
+      t[2] = 2.f * (aq[1] * xp[1] - aq[2] * xp[0]);
+      const float v0 = xp[0] + aq[0] * t[0] + (aq[2] * t[2] - aq[3] * t[1]);
+      const float v1 = xp[1] + aq[0] * t[1] + (aq[3] * t[0] - aq[1] * t[2]);
+      const float v2 = xp[2] + aq[0] * t[2] + (aq[1] * t[1] - aq[2] * t[0]);
+      xp[0] = ap[0] + v0; xp[1] = ap[1] + v1; xp[2] = ap[2] + v2;
+      quatmul(xq, aq, xq);
+      a = an;
+    }
+    quatnorm(xq);
+  }
+  SYNC();
   if (LANE == 0) {
     xpos[0] = xpos[1] = xpos[2] = 0;
     xquat[0] = 1; xquat[1] = xquat[2] = xquat[3] = 0;
     for (int k = 0; k < 9; k++) xmat[k] = (k % 4 == 0) ? 1.f : 0.f;
     xipos[0] = xipos[1] = xipos[2] = 0;
   }
-  SYNC();
-  for (int lv = 1; lv <= c.nlevel; lv++) {
-    if (act && br.depth == lv) {
-      const int b = LANE, p = br.parent, ja = br.ja, jn = br.jn;
-      float xp[3], xq[4];
-      if (jn > 0 && br.jtype == DXJ_FREE) {
-        const float* q = qpos + br.qadr;
-        xp[0] = q[0]; xp[1] = q[1]; xp[2] = q[2];
-        xq[0] = q[3]; xq[1] = q[4]; xq[2] = q[5]; xq[3] = q[6];
-        quatnorm(xq);
-        xanchor[3 * ja] = xp[0]; xanchor[3 * ja + 1] = xp[1]; xanchor[3 * ja + 2] = xp[2];
-        xaxis[3 * ja] = 0; xaxis[3 * ja + 1] = 0; xaxis[3 * ja + 2] = 1;
-      } else {
-        float t[3];
-        matvec3(t, xmat + 9 * p, br.pos);
-        xp[0] = xpos[3 * p] + t[0]; xp[1] = xpos[3 * p + 1] + t[1]; xp[2] = xpos[3 * p + 2] + t[2];
-        quatmul(xq, xquat + 4 * p, br.quat);
-        for (int jj = 0; jj < jn; jj++) {
-          const int j = ja + jj;
-          float jp[3], ja3[3], q0;
-          int qa;
+  if (act) {
+    float R[9], t[3];
+    quat2mat(R, xq);
+    for (int e = 0; e < 3; e++) xpos[3 * b + e] = xp[e];
+    for (int e = 0; e < 4; e++) xquat[4 * b + e] = xq[e];
+    for (int e = 0; e < 9; e++) xmat[9 * b + e] = R[e];
+    matvec3(t, R, br.ipos);
+    for (int e = 0; e < 3; e++) xipos[3 * b + e] = xp[e] + t[e];
+    if (fr) {
+      xanchor[3 * ja] = xp[0]; xanchor[3 * ja + 1] = xp[1]; xanchor[3 * ja + 2] = xp[2];
+      xaxis[3 * ja] = 0; xaxis[3 * ja + 1] = 0; xaxis[3 * ja + 2] = 1;
+    } else {
+      for (int jj = 0; jj < jn; jj++) {
+        const int j = ja + jj;
+        float ab[3], xb[3];
+        if (jj + 1 == jn) {  // the last joint's anchor and axis are its own, in the body frame
           if (jj == 0) {
-            for (int k = 0; k < 3; k++) { jp[k] = br.jpos[k]; ja3[k] = br.jaxis[k]; }
-            qa = br.qadr;
-            q0 = br.q0;
+            for (int k = 0; k < 3; k++) { ab[k] = br.jpos[k]; xb[k] = br.jaxis[k]; }
           } else {
-            for (int k = 0; k < 3; k++) { jp[k] = m.jnt_pos[3 * j + k]; ja3[k] = m.jnt_axis[3 * j + k]; }
-            qa = m.jnt_qposadr[j];
-            q0 = m.qpos0[qa];
+            for (int k = 0; k < 3; k++) { ab[k] = m.jnt_pos[3 * j + k]; xb[k] = m.jnt_axis[3 * j + k]; }
           }
-          float R[9];
-          quat2mat(R, xq);
-          matvec3(t, R, jp);
-          float anc[3] = {t[0] + xp[0], t[1] + xp[1], t[2] + xp[2]};
-          float ax[3];
-          matvec3(ax, R, ja3);
-          xanchor[3 * j] = anc[0]; xanchor[3 * j + 1] = anc[1]; xanchor[3 * j + 2] = anc[2];
-          xaxis[3 * j] = ax[0]; xaxis[3 * j + 1] = ax[1]; xaxis[3 * j + 2] = ax[2];
-          float ang = qpos[qa] - q0;
-          float sn, co;
-          sincosf(0.5f * ang, &sn, &co);
-          float ql[4] = {co, ja3[0] * sn, ja3[1] * sn, ja3[2] * sn};
-          quatmul(xq, xq, ql);
-          quatnorm(xq);
-          quat2mat(R, xq);
-          matvec3(t, R, jp);
-          xp[0] = anc[0] - t[0]; xp[1] = anc[1] - t[1]; xp[2] = anc[2] - t[2];
+        } else {
+          for (int k = 0; k < 3; k++) { ab[k] = xanchor[3 * j + k]; xb[k] = xaxis[3 * j + k]; }
         }
+        float aw[3], xw[3];
+        matvec3(aw, R, ab);
+        matvec3(xw, R, xb);
+        for (int k = 0; k < 3; k++) { xanchor[3 * j + k] = xp[k] + aw[k]; xaxis[3 * j + k] = xw[k]; }
       }
-      float R[9];
-      quat2mat(R, xq);
-      for (int e = 0; e < 3; e++) xpos[3 * b + e] = xp[e];
-      for (int e = 0; e < 4; e++) xquat[4 * b + e] = xq[e];
-      for (int e = 0; e < 9; e++) xmat[9 * b + e] = R[e];
-      float t[3];
-      matvec3(t, R, br.ipos);
-      for (int e = 0; e < 3; e++) xipos[3 * b + e] = xp[e] + t[e];
     }
-    SYNC();
   }
+  SYNC();
 }
 
 template <class Ctx>
