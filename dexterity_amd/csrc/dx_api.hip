@@ -271,6 +271,11 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     delete m;
     return nullptr;
   }
+  if (d.nu > 64 || d.njnt > 64) {  // one lane per actuator / joint (velocity stage, Euler)
+    fail(DX_ELIMIT, "nu and njnt must be <= 64");
+    delete m;
+    return nullptr;
+  }
   int nb = d.nbody, nv = d.nv;
   auto& parent = m->hi["body_parent"];
   auto& rootid = m->hi["body_rootid"];

@@ -273,14 +273,15 @@ enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NI
 // LDS.  Joint fields are the body's first joint (Shadow / Adroit bodies have <= 1).
 struct BodyRec {
   int parent, depth, ja, jn, jtype, qadr, dofadr, dofnum, jdof, rootidx;
-  float pos[3], quat[4], ipos[3], jpos[3], jaxis[3], q0, mass;
+  float pos[3], quat[4], ipos[3], jpos[3], jaxis[3], q0, mass, inert[3];
 };
 template <class Ctx>
 __device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
   const int b = LANE;
   const bool act = b >= 1 && b < c.nbody;
   const DXG float4* R = c.mdl().body_rec + 8 * (act ? b : 0);
-  const float4 a = R[0], p = R[1], q = R[2], i = R[3], jp = R[4], jx = R[5], d = R[6];
+  const float4 a = R[0], p = R[1], q = R[2], i = R[3], jp = R[4], jx = R[5], d = R[6], in = R[7];
+  r.inert[0] = in.x; r.inert[1] = in.y; r.inert[2] = in.z;
   r.parent = __float_as_int(a.x);
   r.depth = act ? __float_as_int(a.y) : -1;
   r.ja = __float_as_int(a.z);
@@ -310,7 +311,7 @@ __device__ __forceinline__ bool load_body(const Ctx& c, BodyRec& r) {
 // chain of cheap compositions with no barrier per level.  Phase 3: rotation matrix,
 // inertial frame, joint anchors and axes in the world frame.
 template <class Ctx>
-__device__ __forceinline__ void kinematics(const Ctx& c) {
+__device__ __forceinline__ void kinematics_impl(const Ctx& c, const BodyRec& br, const bool act) {
   const DevModel& m = c.mdl();
   float* qpos = c.f(c.L.qpos);
   float* xpos = c.f(c.L.xpos);
@@ -319,8 +320,6 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
   float* xipos = c.f(c.L.xipos);
   float* xanchor = c.f(c.L.xanchor);
   float* xaxis = c.f(c.L.xaxis);
-  BodyRec br;
-  const bool act = load_body(c, br);
   const int b = LANE, ja = br.ja, jn = br.jn;
   const bool fr = act && jn > 0 && br.jtype == DXJ_FREE;
   float lp[3] = {br.pos[0], br.pos[1], br.pos[2]};
@@ -446,18 +445,41 @@ __device__ __forceinline__ void kinematics(const Ctx& c) {
 }
 
 template <class Ctx>
-__device__ __forceinline__ void com_pos(const Ctx& c) {
+__device__ __forceinline__ void kinematics(const Ctx& c) {
+  BodyRec br;
+  const bool act = load_body(c, br);
+  kinematics_impl(c, br, act);
+}
+
+// Per-lane model data of com_pos beyond the body record: the body's inertia frame
+// (lane = body) and the dof record (lane = dof).  Loaded with the body record before
+// kinematics, so no model-table round trip follows a barrier.
+struct ComPre {
+  float imat[9];
+  float4 dof0;
+};
+template <class Ctx>
+__device__ __forceinline__ void load_com_pre(const Ctx& c, ComPre& p) {
+  const DevModel& m = c.mdl();
+  const int b = min(LANE, c.nbody - 1);
+#pragma unroll
+  for (int k = 0; k < 9; k++) p.imat[k] = m.body_imat[9 * b + k];
+  p.dof0 = m.dof_rec[2 * min(LANE, c.nv - 1)];
+}
+
+template <class Ctx>
+__device__ __forceinline__ void com_pos_impl(const Ctx& c, const BodyRec& br, const bool act, const ComPre& pre) {
   const DevModel& m = c.mdl();
   float* xipos = c.f(c.L.xipos);
   float* xmat = c.f(c.L.xmat);
   float* rcom = c.f(c.L.rcom);
-  // subtree com of every root (only roots are needed as com-frame origins)
+  // subtree com of every root (only roots are needed as com-frame origins); lane = body
   for (int r = 0; r < c.nroot; r++) {
     float s0 = 0, s1 = 0, s2 = 0, sm = 0;
-    for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
-      if (m.body_rootidx[b] != r) continue;
-      float ms = m.body_mass[b];
-      s0 += ms * xipos[3 * b]; s1 += ms * xipos[3 * b + 1]; s2 += ms * xipos[3 * b + 2]; sm += ms;
+    if (act && br.rootidx == r) {
+      const int b = LANE;
+      const float ms = br.mass;
+      s0 = ms * xipos[3 * b]; s1 = ms * xipos[3 * b + 1]; s2 = ms * xipos[3 * b + 2]; sm = ms;
     }
     s0 = wave_sum(s0); s1 = wave_sum(s1); s2 = wave_sum(s2); sm = wave_sum(sm);
     if (LANE == 0) {
@@ -468,12 +490,13 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   }
   SYNC();
   float* cinert = c.f(c.L.cinert);
-  for (int b = 1 + LANE; b < c.nbody; b += DX_WAVE) {
+  if (act) {
+    const int b = LANE;
     float Rb[9];
-    matmul3(Rb, xmat + 9 * b, m.body_imat + 9 * b);
-    const float* I = m.body_inertia + 3 * b;
-    float mass = m.body_mass[b];
-    const float* rc = rcom + 3 * m.body_rootidx[b];
+    matmul3(Rb, xmat + 9 * b, pre.imat);
+    const float* I = br.inert;
+    float mass = br.mass;
+    const float* rc = rcom + 3 * br.rootidx;
     float off[3] = {xipos[3 * b] - rc[0], xipos[3 * b + 1] - rc[1], xipos[3 * b + 2] - rc[2]};
     float Iw[9];
     for (int i = 0; i < 3; i++)
@@ -495,7 +518,7 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
   float* xanchor = c.f(c.L.xanchor);
   float* xaxis = c.f(c.L.xaxis);
   for (int d = LANE; d < c.nv; d += DX_WAVE) {
-    const float4 dr = m.dof_rec[2 * d];
+    const float4 dr = pre.dof0;
     const int b = __float_as_int(dr.x), j = __float_as_int(dr.y), tk = __float_as_int(dr.w);
     const float* rc = rcom + 3 * __float_as_int(dr.z);
     float off[3] = {rc[0] - xanchor[3 * j], rc[1] - xanchor[3 * j + 1], rc[2] - xanchor[3 * j + 2]};
@@ -521,23 +544,68 @@ __device__ __forceinline__ void com_pos(const Ctx& c) {
 }
 
 template <class Ctx>
-__device__ __forceinline__ void tendon_lengths(const Ctx& c) {
+__device__ __forceinline__ void com_pos(const Ctx& c) {
+  BodyRec br;
+  const bool act = load_body(c, br);
+  ComPre pre;
+  load_com_pre(c, pre);
+  com_pos_impl(c, br, act, pre);
+}
+// mj_kinematics + mj_comPos with every model-table load issued up front
+template <class Ctx>
+__device__ __forceinline__ void kin_com(const Ctx& c) {
+  BodyRec br;
+  const bool act = load_body(c, br);
+  ComPre pre;
+  load_com_pre(c, pre);
+  kinematics_impl(c, br, act);
+  com_pos_impl(c, br, act, pre);
+}
+
+// Tendon wrap tables of lane t = LANE (first two wraps), loaded before kinematics.
+struct TenPre {
+  int adr, num, q0, q1, atrn, aidx;
+  float c0, c1, ag;
+};
+template <class Ctx>
+__device__ __forceinline__ void load_ten_pre(const Ctx& c, TenPre& p) {
+  const DevModel& m = c.mdl();
+  const bool ok = LANE < c.ntendon;
+  const int t = ok ? LANE : 0;
+  p.adr = ok ? m.tendon_adr[t] : 0;
+  p.num = ok ? m.tendon_num[t] : 0;
+  p.c0 = p.num > 0 ? m.wrap_coef[p.adr] : 0.f;
+  p.q0 = p.num > 0 ? m.wrap_qadr[p.adr] : 0;
+  p.c1 = p.num > 1 ? m.wrap_coef[p.adr + 1] : 0.f;
+  p.q1 = p.num > 1 ? m.wrap_qadr[p.adr + 1] : 0;
+  // actuator lane: gear, transmission, and its joint's qpos address or its tendon
+  const bool aok = LANE < c.nu;
+  const int a = aok ? LANE : 0;
+  p.ag = aok ? m.actuator_gear[a] : 0.f;
+  p.atrn = aok ? m.actuator_trntype[a] : 1;
+  const int id = aok ? m.actuator_trnid[a] : 0;
+  p.aidx = p.atrn == 0 ? m.jnt_qposadr[id] : id;
+}
+template <class Ctx>
+__device__ __forceinline__ void tendon_lengths(const Ctx& c, const TenPre& p) {
   const DevModel& m = c.mdl();
   float* qpos = c.f(c.L.qpos);
   float* tl = c.f(c.L.ten_len);
   for (int t = LANE; t < c.ntendon; t += DX_WAVE) {
+    const bool own = t == LANE;  // first pass: the preloaded wraps
+    const int adr = own ? p.adr : m.tendon_adr[t], num = own ? p.num : m.tendon_num[t];
     float len = 0;
-    for (int w = m.tendon_adr[t]; w < m.tendon_adr[t] + m.tendon_num[t]; w++)
-      len += m.wrap_coef[w] * qpos[m.wrap_qadr[w]];
+    for (int w = 0; w < num; w++) {
+      const float wc = (own && w == 0) ? p.c0 : ((own && w == 1) ? p.c1 : m.wrap_coef[adr + w]);
+      const int wq = (own && w == 0) ? p.q0 : ((own && w == 1) ? p.q1 : m.wrap_qadr[adr + w]);
+      len += wc * qpos[wq];
+    }
     tl[t] = len;
   }
   SYNC();
+  // actuator lengths (position actuators' bias), lane = actuator (nu <= 64)
   float* al = c.f(c.L.act_len);
-  for (int i = LANE; i < c.nu; i += DX_WAVE) {
-    float g = m.actuator_gear[i];
-    al[i] = m.actuator_trntype[i] == 0 ? g * qpos[m.jnt_qposadr[m.actuator_trnid[i]]]
-                                       : g * tl[m.actuator_trnid[i]];
-  }
+  if (LANE < c.nu) al[LANE] = p.atrn == 0 ? p.ag * qpos[p.aidx] : p.ag * tl[p.aidx];
 }
 
 // Symmetric nv x nv matrices (M, the Newton Hessian, Cholesky factors) are stored
@@ -552,11 +620,15 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
   float* cinert = c.f(c.L.cinert);
   float* M = c.f(c.L.M);
   float* cdof = c.f(c.L.cdof);
+  // model records first: their L2 round trips overlap the level passes below
+  // (a load after a barrier is a full round trip on the wave's critical path)
+  BodyRec br;
+  const bool act = load_body(c, br);
+  const int i0 = min(LANE, nv - 1);  // nv <= 64 (model check): one dof per lane
+  const float4 d0r = m.dof_rec[2 * i0], d1r = m.dof_rec[2 * i0 + 1];
   for (int k = LANE; k < 10 * c.nbody; k += DX_WAVE) crb[k] = cinert[k];
   for (int k = LANE; k < ti(nv); k += DX_WAVE) M[k] = 0;
   SYNC();
-  BodyRec br;
-  const bool act = load_body(c, br);
   for (int lv = c.nlevel; lv >= 2; lv--) {
     if (act && br.depth == lv && br.parent > 0)
       for (int e = 0; e < 10; e++) atomicAdd(crb + 10 * br.parent + e, crb[10 * LANE + e]);
@@ -564,7 +636,7 @@ __device__ __forceinline__ void crb_mass(const Ctx& c) {
   }
   // row i: j over the dof's ancestors (incl. itself), a bit mask from dof_rec
   for (int i = LANE; i < nv; i += DX_WAVE) {
-    const float4 d0 = m.dof_rec[2 * i], d1 = m.dof_rec[2 * i + 1];
+    const float4 d0 = d0r, d1 = d1r;
     float f[6];
     mul_inert(f, crb + 10 * __float_as_int(d0.x), cdof + 6 * i);
     uint64_t anc = (uint64_t)(uint32_t)__float_as_int(d1.z) | ((uint64_t)(uint32_t)__float_as_int(d1.w) << 32);
@@ -648,8 +720,7 @@ __device__ __forceinline__ float half_dup(float v, bool up) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(up ? r[1] : r[0]);
 }
-__device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const DXG float* dadd, float hs,
-                                                  float* x, float* T) {
+__device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, float dj, float* x, float* T) {
   const int l = LANE;
   const int j = l & 31, hi = l >> 5;
   dx_f16v C;
@@ -659,7 +730,7 @@ __device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const D
     const int ra = max(i, j), rb = min(i, j);
     const bool in = i < n && j < n;
     float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
-    if (dadd && i == j && in) e += hs * dadd[i];
+    if (i == j && in) e += dj;
     C[v] = e;
   }
   float b = l < n ? x[l] : 0.f;
@@ -725,8 +796,8 @@ __device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, const D
 // apply the rank-2 update to C11, C12 and C22; columns 32-63 then factor C22 alone.
 // L goes to T (packed rows, ti(n) words, may alias A) as it is produced, and both
 // substitutions run with lane = row (0-63) on readlane / writelane chains.
-__device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const DXG float* dadd, float hs,
-                                                  float* x, float* T) {
+__device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float dj1, float dj2, float* x,
+                                                  float* T) {
   const int l = LANE;
   const int j = l & 31, hi = l >> 5;
   dx_f16v C11, C12, C22;
@@ -736,7 +807,7 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
     {  // C11: A[i][j]
       const int ra = max(i, j), rb = min(i, j);
       float e = A[ti(ra) + rb];  // i, j < 32 < n
-      if (dadd && i == j) e += hs * dadd[i];
+      if (i == j) e += dj1;
       C11[v] = e;
     }
     {  // C12: A[i][32 + j] = A[32 + j][i]
@@ -748,7 +819,7 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
       const bool in = ri < n && rj < n;
       const int ra = max(ri, rj), rb = min(ri, rj);
       float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
-      if (dadd && i == j && in) e += hs * dadd[ri];
+      if (i == j && in) e += dj2;
       C22[v] = e;
     }
   }
@@ -847,10 +918,23 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, const D
   SYNC();
 }
 
-// x <- (A + hs * diag(dadd))^-1 x for a packed lower-triangle A (LDS), n <= 64;
+// Diagonal additions hs * dadd for chol_solve, one pair per lane (columns l % 32 and
+// 32 + l % 32).  Load them early, before the caller's barriers: a model-table load
+// issued after a barrier is a whole L2 round trip on the wave's critical path.
+struct DiagAdd { float d1, d2; };
+__device__ __forceinline__ DiagAdd diag_add(const DXG float* dadd, float hs, int n) {
+  const int j = LANE & 31;
+  DiagAdd d;
+  d.d1 = j < n ? hs * dadd[j] : 0.f;
+  d.d2 = 32 + j < n ? hs * dadd[32 + j] : 0.f;
+  return d;
+}
+// x <- (A + diag(dd))^-1 x for a packed lower-triangle A (LDS), n <= 64;
 // T: ti(max(n, 32)) words of LDS scratch, may alias A.
-__device__ __forceinline__ void chol_solve(const float* A, int n, const DXG float* dadd, float hs, float* x,
-                                           float* T) {
-  if (n <= 32) mfma_chol_solve32(A, n, dadd, hs, x, T);
-  else mfma_chol_solve64(A, n, dadd, hs, x, T);
+__device__ __forceinline__ void chol_solve(const float* A, int n, DiagAdd dd, float* x, float* T) {
+  if (n <= 32) mfma_chol_solve32(A, n, dd.d1, x, T);
+  else mfma_chol_solve64(A, n, dd.d1, dd.d2, x, T);
+}
+__device__ __forceinline__ void chol_solve(const float* A, int n, float* x, float* T) {
+  chol_solve(A, n, DiagAdd{0.f, 0.f}, x, T);
 }

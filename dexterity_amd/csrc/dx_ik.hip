@@ -144,8 +144,7 @@ extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(const DevModel* __
     }
     SYNC();
   }
-  kinematics(c);
-  com_pos(c);
+  kin_com(c);
   float* pt = c.f(K.pt);
   float* J = c.f(K.J);
   sites_to_lds(c, P, pt);
@@ -189,7 +188,7 @@ extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(const DevModel* __
       H[t] = s + (i == j ? P.reg : 0.f);
     }
     SYNC();
-    mfma_chol_solve32(H, n3, nullptr, 0.f, y, H);
+    mfma_chol_solve32(H, n3, 0.f, y, H);
     for (int d = LANE; d < nv; d += DX_WAVE) {
       float s = 0.f;
       for (int r = 0; r < n3; r++) s = fmaf(J[r * nv + d], y[r], s);
@@ -197,8 +196,7 @@ extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(const DevModel* __
     }
     SYNC();
     ik_integrate(c, P, qd, 1.0f);
-    kinematics(c);
-    com_pos(c);
+    kin_com(c);
     sites_to_lds(c, P, pt);
     it++;
     // ik_solver.py:201-233: per-site error and progress, then the break conditions

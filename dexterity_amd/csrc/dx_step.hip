@@ -1109,12 +1109,51 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   float* qvel = c.f(c.L.qvel);
   int* meta = (int*)c.f(c.L.efc_meta);
   int nfric = c.nfric;
+  float* con = c.f(c.L.con);
+  // Model tables of every section's first lane pass (lane = friction row, limited joint,
+  // contact), issued up front in dependency levels: three overlapped L2 round trips
+  // instead of a chain of them per section after each barrier.
+  // level 1
+  const int ncon = I[I_NCON];
+  const bool fok = LANE < nfric, lok = LANE < c.nlimj, cok = LANE < ncon;
+  const int fd = fok ? m.fric_dof[LANE] : 0;
+  const int lj = lok ? m.limj_jnt[LANE] : 0;
+  // (contact tables only for lanes holding a contact: a scene without contact pairs
+  // has empty gpair tables)
+  const int cgp = cok ? __float_as_int(con[DX_CON_STRIDE * LANE + 13]) : 0;
+  const int cg1 = cok ? m.gpair_geom[2 * cgp] : 0, cg2 = cok ? m.gpair_geom[2 * cgp + 1] : 0;
+  const int ccd = cok ? m.gpair_condim[cgp] : 1;
+  const float cfr0 = cok ? m.gpair_friction[5 * cgp] : 0.f, cfr1 = cok ? m.gpair_friction[5 * cgp + 1] : 0.f;
+  const float csr[2] = {cok ? m.gpair_solref[2 * cgp] : 0.f, cok ? m.gpair_solref[2 * cgp + 1] : 0.f};
+  float csi[5];
+  for (int e = 0; e < 5; e++) csi[e] = cok ? m.gpair_solimp[5 * cgp + e] : 0.f;
+  const float cmg = cok ? m.gpair_margin[cgp] : 0.f;
+  // level 2
+  const float ffl = m.dof_frictionloss[fd], fiw = m.dof_invweight0[fd];
+  const float fsr[2] = {m.dof_solref[2 * fd], m.dof_solref[2 * fd + 1]};
+  float fsi[5];
+  for (int e = 0; e < 5; e++) fsi[e] = m.dof_solimp[5 * fd + e];
+  const int lqa = m.jnt_qposadr[lj], ldof = m.jnt_dofadr[lj];
+  const float lr0 = m.jnt_range[2 * lj], lr1 = m.jnt_range[2 * lj + 1], lmg = m.jnt_margin[lj];
+  const float lsr[2] = {m.jnt_solref[2 * lj], m.jnt_solref[2 * lj + 1]};
+  float lsi[5];
+  for (int e = 0; e < 5; e++) lsi[e] = m.jnt_solimp[5 * lj + e];
+  const int cb1 = cok ? m.geom_bodyid[cg1] : 0, cb2 = cok ? m.geom_bodyid[cg2] : 0;
+  // level 3
+  const float liw = m.dof_invweight0[ldof];
+  const uint64_t cc1 = m.body_chain[cb1], cc2 = m.body_chain[cb2];
+  const float ctran = m.body_invweight0[2 * cb1] + m.body_invweight0[2 * cb2];
+  const int cr1 = m.body_rootidx[cb1], cr2 = m.body_rootidx[cb2];
   // 1. dof friction rows: fixed positions [0, nfric)
   for (int k = LANE; k < nfric; k += DX_WAVE) {
-    int d = m.fric_dof[k];
+    const bool own = k == LANE;
+    int d = own ? fd : m.fric_dof[k];
     meta[k] = DXR_FRIC | (d << 8);
-    row_params(c, k, 0, 0, m.dof_frictionloss[d], m.dof_invweight0[d], m.dof_solref + 2 * d,
-               m.dof_solimp + 5 * d, qvel[d], 1.0f, true);
+    if (own)
+      row_params(c, k, 0, 0, ffl, fiw, fsr, fsi, qvel[d], 1.0f, true);
+    else
+      row_params(c, k, 0, 0, m.dof_frictionloss[d], m.dof_invweight0[d], m.dof_solref + 2 * d,
+                 m.dof_solimp + 5 * d, qvel[d], 1.0f, true);
   }
   // 2. joint limits (one side at most unless range < 2 margin): lane per limited joint
   int nrow = nfric;
@@ -1123,26 +1162,32 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     int cnt = 0;
     float dist[2];
     int j = -1;
+    const bool own = base == 0;  // first pass: the preloaded tables
+    float mg = 0.f;
     if (k < c.nlimj) {
-      j = m.limj_jnt[k];
-      float q = qpos[m.jnt_qposadr[j]];
-      dist[0] = q - m.jnt_range[2 * j];
-      dist[1] = m.jnt_range[2 * j + 1] - q;
-      cnt = (dist[0] < m.jnt_margin[j]) + (dist[1] < m.jnt_margin[j]);
+      j = own ? lj : m.limj_jnt[k];
+      float q = qpos[own ? lqa : m.jnt_qposadr[j]];
+      dist[0] = q - (own ? lr0 : m.jnt_range[2 * j]);
+      dist[1] = (own ? lr1 : m.jnt_range[2 * j + 1]) - q;
+      mg = own ? lmg : m.jnt_margin[j];
+      cnt = (dist[0] < mg) + (dist[1] < mg);
     }
     int inc = wave_incl_scan(cnt);
     int off = inc - cnt;
     int tot = __builtin_amdgcn_readlane(inc, 63);
     if (cnt) {
       int r = nrow + off;
-      int d = m.jnt_dofadr[j];
+      int d = own ? ldof : m.jnt_dofadr[j];
       for (int side = 0; side < 2; side++) {
-        if (dist[side] >= m.jnt_margin[j]) continue;
+        if (dist[side] >= mg) continue;
         if (r < c.L.nefc_max) {
           meta[r] = DXR_LIMJ | (side << 4) | (d << 8);  // hinge: the joint's dof
           float v = side == 0 ? qvel[d] : -qvel[d];
-          row_params(c, r, dist[side], m.jnt_margin[j], 0, m.dof_invweight0[d], m.jnt_solref + 2 * j,
-                     m.jnt_solimp + 5 * j, v, 1.0f, false);
+          if (own)
+            row_params(c, r, dist[side], mg, 0, liw, lsr, lsi, v, 1.0f, false);
+          else
+            row_params(c, r, dist[side], mg, 0, m.dof_invweight0[d], m.jnt_solref + 2 * j,
+                       m.jnt_solimp + 5 * j, v, 1.0f, false);
         }
         r++;
       }
@@ -1184,8 +1229,6 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   }
   SYNC();
   // 4. contacts: sparse frame jacobian, then pyramid rows
-  int ncon = I[I_NCON];
-  float* con = c.f(c.L.con);
   float* cdof = c.f(c.L.cdof);
   float* rcom = c.f(c.L.rcom);
   unsigned char* cj_idx = (unsigned char*)c.f(c.L.cj_idx);
@@ -1193,10 +1236,17 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   float* cq = c.f(c.L.cq);
   for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
     float* r = con + DX_CON_STRIDE * ci;
+    const bool own = ci == LANE;
     int gp = __float_as_int(r[13]);
-    int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
-    int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-    uint64_t c1 = m.body_chain[b1], c2 = m.body_chain[b2];
+    uint64_t c1, c2;
+    int r1, r2;  // root trees of the two bodies: a dof of c1 ^ c2 is in c1 (tree r1) or c2 (tree r2)
+    if (own) {
+      c1 = cc1; c2 = cc2; r1 = cr1; r2 = cr2;
+    } else {
+      int b1 = m.geom_bodyid[m.gpair_geom[2 * gp]], b2 = m.geom_bodyid[m.gpair_geom[2 * gp + 1]];
+      c1 = m.body_chain[b1]; c2 = m.body_chain[b2];
+      r1 = m.body_rootidx[b1]; r2 = m.body_rootidx[b2];
+    }
     uint64_t sup = c1 ^ c2;
     int nnz = 0;
     float vel[3] = {0, 0, 0};
@@ -1204,8 +1254,7 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
       int d = __ffsll((long long)sup) - 1;
       sup &= sup - 1;
       float sgn = (c2 >> d) & 1ull ? 1.f : -1.f;
-      int bb = m.dof_bodyid[d];
-      const float* rc = rcom + 3 * m.body_rootidx[bb];
+      const float* rc = rcom + 3 * (((c1 >> d) & 1ull) ? r1 : r2);
       const float* cd = cdof + 6 * d;
       float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
       float t[3];
@@ -1221,10 +1270,10 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     }
     if (sup) I[I_OVF] |= 4;
     for (int k = 0; k < 3; k++) cq[3 * ci + k] = vel[k];  // frame velocities (J qvel)
-    int nr = m.gpair_condim[gp] == 1 ? 1 : 4;
+    int nr = (own ? ccd : m.gpair_condim[gp]) == 1 ? 1 : 4;
     r[14] = __int_as_float(nnz | (nr << 8));
-    r[16] = m.gpair_friction[5 * gp];
-    r[17] = m.gpair_friction[5 * gp + 1];
+    r[16] = own ? cfr0 : m.gpair_friction[5 * gp];
+    r[17] = own ? cfr1 : m.gpair_friction[5 * gp + 1];
     uint64_t sp = c1 ^ c2;
     r[18] = __int_as_float((int)(uint32_t)sp);
     r[19] = __int_as_float((int)(uint32_t)(sp >> 32));
@@ -1244,13 +1293,21 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     int off = inc - nr;
     int tot = __builtin_amdgcn_readlane(inc, 63);
     if (nr) {
-      int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
-      int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-      float tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-      const float* fr = m.gpair_friction + 5 * gp;
-      const float* sr = m.gpair_solref + 2 * gp;
-      const float* si = m.gpair_solimp + 5 * gp;
-      float mg = m.gpair_margin[gp];
+      const bool own = base == 0;  // first pass: the preloaded tables
+      float tran, mg, fr[2], sr[2], si[5];
+      if (own) {
+        tran = ctran; mg = cmg; fr[0] = cfr0; fr[1] = cfr1;
+        sr[0] = csr[0]; sr[1] = csr[1];
+        for (int e = 0; e < 5; e++) si[e] = csi[e];
+      } else {
+        int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
+        int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+        mg = m.gpair_margin[gp];
+        fr[0] = m.gpair_friction[5 * gp]; fr[1] = m.gpair_friction[5 * gp + 1];
+        sr[0] = m.gpair_solref[2 * gp]; sr[1] = m.gpair_solref[2 * gp + 1];
+        for (int e = 0; e < 5; e++) si[e] = m.gpair_solimp[5 * gp + e];
+      }
       r[15] = __int_as_float(nrow + off);
       if (nr == 1) {
         int row = nrow + off;
@@ -1293,6 +1350,24 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
   float* cdd = c.f(c.L.cdof_dot);
   float* cinert = c.f(c.L.cinert);
   float* qs = c.f(c.L.qfrc_smooth);
+  // Actuator tables (lane = actuator, nu <= 64), with the transmission's dof or first
+  // two tendon wraps, loaded now so that their L2 round trips (two of them dependent)
+  // overlap the tree sums instead of following the barriers below.
+  const int ia = min(LANE, max(c.nu - 1, 0));
+  const bool a_ok = LANE < c.nu;
+  const int a_trn = a_ok ? m.actuator_trntype[ia] : 0, a_id = a_ok ? m.actuator_trnid[ia] : 0;
+  const int a_clim = a_ok ? m.actuator_ctrllimited[ia] : 0, a_flim = a_ok ? m.actuator_forcelimited[ia] : 0;
+  const int a_bt = a_ok ? m.actuator_biastype[ia] : 0;
+  const float a_g = a_ok ? m.actuator_gear[ia] : 0.f, a_gain = a_ok ? m.actuator_gainprm[3 * ia] : 0.f;
+  const float a_c0 = a_ok ? m.actuator_ctrlrange[2 * ia] : 0.f, a_c1 = a_ok ? m.actuator_ctrlrange[2 * ia + 1] : 0.f;
+  const float a_f0 = a_ok ? m.actuator_forcerange[2 * ia] : 0.f, a_f1 = a_ok ? m.actuator_forcerange[2 * ia + 1] : 0.f;
+  const float a_b0 = a_ok ? m.actuator_biasprm[3 * ia] : 0.f, a_b1 = a_ok ? m.actuator_biasprm[3 * ia + 1] : 0.f,
+              a_b2 = a_ok ? m.actuator_biasprm[3 * ia + 2] : 0.f;
+  const int a_dof = (a_ok && a_trn == 0) ? m.jnt_dofadr[a_id] : 0;
+  const int a_wa = (a_ok && a_trn != 0) ? m.tendon_adr[a_id] : 0;
+  const int a_wn = (a_ok && a_trn != 0) ? m.tendon_num[a_id] : 0;
+  const float a_wc0 = a_wn > 0 ? m.wrap_coef[a_wa] : 0.f, a_wc1 = a_wn > 1 ? m.wrap_coef[a_wa + 1] : 0.f;
+  const int a_wd0 = a_wn > 0 ? m.wrap_dof[a_wa] : 0, a_wd1 = a_wn > 1 ? m.wrap_dof[a_wa + 1] : 0;
   // The tree recursions of mj_comVel / mj_rne are sums over a body's dof chain (the
   // dofs on its path to the root, dx_api.hip body_chain), so every dof and every body
   // is computed at once instead of one tree level after another:
@@ -1381,30 +1456,33 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
   float* ctrl = c.f(c.L.ctrl);
   float* tl = c.f(c.L.ten_len);
   (void)tl;
-  for (int i = LANE; i < c.nu; i += DX_WAVE) {
+  if (a_ok) {
+    const int i = LANE;
     float cc = ctrl[i];
-    if (m.actuator_ctrllimited[i])
-      cc = fminf(m.actuator_ctrlrange[2 * i + 1], fmaxf(m.actuator_ctrlrange[2 * i], cc));
-    float g = m.actuator_gear[i];
-    int id = m.actuator_trnid[i];
+    if (a_clim) cc = fminf(a_c1, fmaxf(a_c0, cc));
+    const float g = a_g;
     float vel;
-    if (m.actuator_trntype[i] == 0) {
-      vel = g * qvel[m.jnt_dofadr[id]];
+    if (a_trn == 0) {
+      vel = g * qvel[a_dof];
     } else {
       vel = 0;
-      for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++)
-        vel += g * m.wrap_coef[w] * qvel[m.wrap_dof[w]];
+      for (int w = 0; w < a_wn; w++) {
+        const float wc = w == 0 ? a_wc0 : (w == 1 ? a_wc1 : m.wrap_coef[a_wa + w]);
+        const int wd = w == 0 ? a_wd0 : (w == 1 ? a_wd1 : m.wrap_dof[a_wa + w]);
+        vel += g * wc * qvel[wd];
+      }
     }
-    float force = m.actuator_gainprm[3 * i] * cc;
-    if (m.actuator_biastype[i] == 1)
-      force += m.actuator_biasprm[3 * i] + m.actuator_biasprm[3 * i + 1] * al[i] + m.actuator_biasprm[3 * i + 2] * vel;
-    if (m.actuator_forcelimited[i])
-      force = fminf(m.actuator_forcerange[2 * i + 1], fmaxf(m.actuator_forcerange[2 * i], force));
-    if (m.actuator_trntype[i] == 0) {
-      atomicAdd(qs + m.jnt_dofadr[id], g * force);
+    float force = a_gain * cc;
+    if (a_bt == 1) force += a_b0 + a_b1 * al[i] + a_b2 * vel;
+    if (a_flim) force = fminf(a_f1, fmaxf(a_f0, force));
+    if (a_trn == 0) {
+      atomicAdd(qs + a_dof, g * force);
     } else {
-      for (int w = m.tendon_adr[id]; w < m.tendon_adr[id] + m.tendon_num[id]; w++)
-        atomicAdd(qs + m.wrap_dof[w], g * m.wrap_coef[w] * force);
+      for (int w = 0; w < a_wn; w++) {
+        const float wc = w == 0 ? a_wc0 : (w == 1 ? a_wc1 : m.wrap_coef[a_wa + w]);
+        const int wd = w == 0 ? a_wd0 : (w == 1 ? a_wd1 : m.wrap_dof[a_wa + w]);
+        atomicAdd(qs + wd, g * wc * force);
+      }
     }
   }
   SYNC();
@@ -1885,7 +1963,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     float* H = c.f(c.L.H);
     for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
     SYNC();
-    chol_solve(H, nv, nullptr, 0.f, dir, H);
+    chol_solve(H, nv, dir, H);
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float alpha = line_search(c, qacc, Ma, dir, &changed);
@@ -1931,10 +2009,11 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   // rows and contact jacobians overwrite those; the Newton Hessian overwrites the
   // kinematic block.  Collision does not depend on velocities, so this order gives
   // the same result as MuJoCo's mj_fwdPosition -> mj_fwdVelocity.
-  kinematics(c);
-  com_pos(c);
+  TenPre tp;
+  load_ten_pre(c, tp);
+  kin_com(c);
   stage_mark(c, ST_KIN);
-  tendon_lengths(c);
+  tendon_lengths(c, tp);
   crb_mass(c);
   stage_mark(c, ST_CRB);
   velocity_stage(c, xfrc);
@@ -1946,7 +2025,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   const float* qs = c.f(c.L.qfrc_smooth);
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
   SYNC();
-  chol_solve(M, nv, nullptr, 0.f, a0, H);
+  chol_solve(M, nv, a0, H);
   stage_mark(c, ST_SMOOTH);
   collision(c, 0, -1, -1);
   make_constraint(c);
@@ -1972,21 +2051,25 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
   float* qvel = c.f(c.L.qvel);
   float* qpos = c.f(c.L.qpos);
   float* acc = c.f(c.L.v1);
+  // joint tables before the barriers (njnt <= nv <= 64: one joint per lane)
+  const int j0 = min(LANE, c.njnt - 1);
+  const int jqa = m.jnt_qposadr[j0], jda = m.jnt_dofadr[j0], jty = m.jnt_type[j0];
+  const DiagAdd dd = c.any_damping ? diag_add(m.dof_damping, h, nv) : DiagAdd{0.f, 0.f};
   if (c.any_damping) {
     float* H = c.f(c.L.H);
     const float* M = c.f(c.L.M);
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
     SYNC();
-    chol_solve(M, nv, m.dof_damping, h, acc, H);
+    chol_solve(M, nv, dd, acc, H);
   } else {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
     SYNC();
   }
   for (int i = LANE; i < nv; i += DX_WAVE) qvel[i] += h * acc[i];
   SYNC();
-  for (int j = LANE; j < c.njnt; j += DX_WAVE) {
-    int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
-    if (m.jnt_type[j] == DXJ_FREE) {
+  if (LANE < c.njnt) {
+    const int qa = jqa, da = jda;
+    if (jty == DXJ_FREE) {
       for (int k = 0; k < 3; k++) qpos[qa + k] += h * qvel[da + k];
       float* q = qpos + qa + 3;
       const float* w = qvel + da + 3;
@@ -2011,8 +2094,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
 template <class Ctx>
 __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env) {
   const DevModel& m = c.mdl();
-  kinematics(c);
-  com_pos(c);
+  kin_com(c);
   // cvel (no forces)
   float* qvel = c.f(c.L.qvel);
   float* cdof = c.f(c.L.cdof);
