@@ -9,11 +9,13 @@ device uniformly within each actuator's ctrlrange (the random agent of
 manipulation_test.py:44-45).  Inputs are resident in HBM; nothing crosses PCIe in
 the timed region.
 
-N=1: 4096 envs on one MI355X.  N>1 (torchrun, one process per GPU): 4096 envs per
-GPU (weak scaling, 32768 on 8 GPUs = config 4) and an RCCL all-gather of the packed
-[obs | reward | discount | step_type] shards every control step.
+N=1: 4096 envs on one MI355X.  N>1 (torch.distributed.run launches one process per
+GPU; only its RANK / WORLD_SIZE / LOCAL_RANK / MASTER_PORT environment is used):
+4096 envs per GPU (weak scaling, 32768 on 8 GPUs = config 4) and, every control
+step, the RCCL all-gather of the packed [obs | reward | discount | step_type] shards
+(dx_allgather_obs: librccl called from libdx).  No PyTorch.
 
-Prints ONE JSON line (rank 0).  See DESIGN.md §5 for the roofline accounting.
+Prints ONE JSON line (rank 0).  Roofline accounting: DESIGN.md §5.4.
 """
 
 from __future__ import annotations
@@ -34,6 +36,7 @@ sys.path.insert(0, ROOT)
 ALGO_BYTES_PER_ENV_STEP = (20 + 31 + 30 + 30 + 31 + 30 + 30 + 123 + 3) * 4  # 1312 B
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector)
+FLOP_SAMPLE_ENVS = 256
 
 
 def parse():
@@ -42,13 +45,26 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--envs-per-gpu", type=int, default=4096)
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (all threads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
 
-def cpu_baseline(seconds: float, flops_per_env_step_box: list):
-    """The fp64 oracle (oracle/dx_oracle.c) timed on this box's host cores, OpenMP over envs."""
+def host_threads() -> int:
+    """Host cores this process may use: the affinity mask, bounded by the job's CPU
+    share when the launcher states one (OMP_NUM_THREADS; 16 per GPU on the MI355X
+    boxes, whose `nproc` counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS")
+    if share and share.isdigit() and int(share) > 0:
+        n = min(n, int(share))
+    return max(1, n)
+
+
+def oracle_flops_per_env_step(states, nsub: int) -> float:
+    """FLOPs of one control step on the oracle's per-stage counters, averaged over
+    environment states sampled from the GPU batch at the end of the timed region (so
+    the contact mix is the bench workload's)."""
     import numpy as np
 
     from dexterity_amd import blob
@@ -59,38 +75,85 @@ def cpu_baseline(seconds: float, flops_per_env_step_box: list):
     O.build()
     cm = CompiledModel.load(os.path.join(ROOT, "assets", "shadow_reorient.npz"))
     om = O.OracleModel(blob.pack(cm.arrays))
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    nenv = threads * 8
-    rng = np.random.RandomState(12345)
-    qpos = np.tile(cm.qpos0, (nenv, 1))
-    qpos[:, 24:27] += rng.uniform(-0.025, 0.025, size=(nenv, 3)) * [1, 1, 0]
-    qvel = np.zeros((nenv, cm.nv))
-    ws = np.zeros((nenv, cm.nv))
     xfrc = gravity_compensation(cm, "shadow_hand_e/")
+    qpos, qvel, ws, ctrl = (np.asarray(a, dtype=np.float64) for a in states)
+    fl = []
+    O.batch_step(om, qpos, qvel, ctrl, ws, xfrc, nsub=nsub, nthreads=host_threads(), flops=fl)
+    return fl[0] / qpos.shape[0]
+
+
+def cpu_baseline(seconds: float, threads: int, states, nsub: int):
+    """The fp64 oracle (oracle/dx_oracle.c, "port") timed on this box's host cores,
+    OpenMP over environments, on the same scene and the bench's own state mix: the
+    sample starts from environment states taken from the GPU batch, draws random
+    actions within ctrlrange each control step, and restarts an env from its initial
+    state once its cube lies on the ground (the reference would reset it on the
+    prop-ground contact, reorient.py:229-235)."""
+    import numpy as np
+
+    from dexterity_amd import blob
+    from dexterity_amd.mjcf.compiler import CompiledModel
+    from dexterity_amd.physics import gravity_compensation
+    from oracle import oracle as O
+
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "shadow_reorient.npz"))
+    om = O.OracleModel(blob.pack(cm.arrays))
+    xfrc = gravity_compensation(cm, "shadow_hand_e/")
+    q0, v0, w0 = (np.array(a, dtype=np.float64) for a in states[:3])
+    n = q0.shape[0]
+    qpos, qvel, ws = q0.copy(), v0.copy(), w0.copy()
     lo, hi = cm.actuator_ctrlrange.T
-    # per-env-step FLOPs from the instrumented oracle on the same scene (5 substeps)
-    d = O.OracleData(om)
-    d.xfrc_applied[:] = xfrc.ravel()
-    for _ in range(40):  # settle the cube first so the sample includes contacts
-        d.step()
-    d.flops_reset()
-    for _ in range(5):
-        d.step()
-    flops_per_env_step_box.append(float(d.flops().sum()))
+    rng = np.random.RandomState(12345)
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        ctrl = rng.uniform(lo, hi, size=(nenv, cm.nu))
-        rc, qpos, qvel, ws = O.batch_step(om, qpos, qvel, ctrl, ws, xfrc, nsub=5, nthreads=threads)
+        ctrl = rng.uniform(lo, hi, size=(n, cm.nu))
+        rc, qpos, qvel, ws = O.batch_step(om, qpos, qvel, ctrl, ws, xfrc, nsub=nsub, nthreads=threads)
+        down = qpos[:, 26] < 0.025  # cube centre below 2.5 cm: resting on the ground (half-size 2 cm)
+        qpos[down], qvel[down], ws[down] = q0[down], v0[down], w0[down]
         steps += 1
     dt = time.perf_counter() - t0
     return {
-        "value": nenv * steps / dt,
+        "value": n * steps / dt,
         "unit": "env-steps/sec",
         "cores": threads,
         "kind": "port",
-        "sample": f"fp64 C oracle (oracle/dx_oracle.c), same scene, {nenv} envs x {steps} control steps "
-        f"(5 substeps each), random ctrl, OpenMP {threads} threads, {dt:.1f} s",
+        "sample": f"fp64 C oracle (oracle/dx_oracle.c), reorient scene, {n} env states taken from the GPU batch "
+        f"x {steps} control steps (5 substeps each), random ctrl, fallen cubes restarted, OpenMP {threads} "
+        f"threads, {dt:.1f} s",
+    }
+
+
+def cpu_baseline_reach_1env(seconds: float):
+    """BASELINE.json config 1: reach (Adroit hand, the reference task's hand), 1 env,
+    1 thread, dt 0.02 x 1 substep, uniform random actions (manipulation_test.py:44-45)."""
+    import numpy as np
+
+    from dexterity_amd import blob
+    from dexterity_amd.mjcf.compiler import CompiledModel
+    from dexterity_amd.physics import gravity_compensation
+    from oracle import oracle as O
+
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "adroit_reach.npz"))
+    om = O.OracleModel(blob.pack(cm.arrays))
+    d = O.OracleData(om)
+    d.xfrc_applied[:] = gravity_compensation(cm, "adroit_hand/").ravel()
+    lo, hi = cm.actuator_ctrlrange.T
+    rng = np.random.RandomState(12345)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        d.ctrl[:] = rng.uniform(lo, hi)
+        d.step()
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {
+        "value": steps / dt,
+        "unit": "env-steps/sec",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"config 1: fp64 C oracle, reach (Adroit hand), 1 env, 1 thread, {steps} control steps "
+        f"(1 substep each, dt 0.02), random ctrl, {dt:.1f} s (Python call per step included)",
     }
 
 
@@ -99,62 +162,60 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    import torch  # imported before libdx so both share one HIP runtime
-
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     from dexterity_amd import _lib, distributed, manipulation
 
+    L = _lib.load()
+    comm = distributed.Comm.from_env(device=local) if world > 1 else None
     B = args.envs_per_gpu
     env = manipulation.load("reorient", "state_dense", seed=distributed.rank_seed(12345, rank), num_envs=B,
                             device=local)
-    L = _lib.load()
-    obs_w = env.obs_dim + 3
-    if world > 1:
-        collator = distributed.OutputCollator(B, obs_w, device=f"cuda:{local}")
+    collator = distributed.OutputCollator(env, comm) if comm else None
 
     def one_step(i):
         a = env.sample_actions(i)
         env.step(a, device_action=True)
-        if world > 1:
-            _lib.check(L.dx_env_pack_outputs(env.ptr, ctypes.c_void_p(collator.shard.data_ptr())))
-            env.physics.sync()
-            collator.gather()
+        if collator:
+            collator.gather()  # enqueued on the env stream behind the step: no host sync
 
     env.reset()
     for i in range(args.warmup):
         one_step(i)
     env.physics.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if comm:
+        comm.barrier()
     _lib.check(L.dx_timing_enable(env.physics.ptr, 1))
     _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int32())))
     t0 = time.perf_counter()
     for i in range(args.steps):
         one_step(args.warmup + i)
     env.physics.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if comm:
+        comm.barrier()
     elapsed = time.perf_counter() - t0
     kt, kn = ctypes.c_double(), ctypes.c_int32()
     _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(kt), ctypes.byref(kn)))
     _lib.check(L.dx_timing_enable(env.physics.ptr, 0))
-    if world > 1:
-        elapsed = distributed.max_over_ranks(elapsed, f"cuda:{local}")
+    # a substep-queue timeout would mean corrupted hand-offs: no number is reported then
+    qerr = env.physics.debug_get("queue_timeouts")
+    if int(qerr[0]) != 0:
+        raise SystemExit("substep queue timed out during the timed region; refusing to report")
+    if comm:
+        elapsed = comm.max(elapsed)
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
     kernel_ms = kt.value / max(1, kn.value)
-    out = None
+    nsub = env.task.config.n_sub_steps
     if rank == 0:
-        achieved = ALGO_BYTES_PER_ENV_STEP * B / (kernel_ms * 1e-3) / 1e9
+        import numpy as np
+
+        ph = env.physics
+        idx = np.linspace(0, B - 1, min(FLOP_SAMPLE_ENVS, B)).astype(int)
+        sample = [ph.get(f)[idx] for f in (_lib.QPOS, _lib.QVEL, _lib.QACC_WARMSTART, _lib.CTRL)]
+        flops = oracle_flops_per_env_step(sample, nsub)
+        achieved_tf = flops * B / (kernel_ms * 1e-3) / 1e12
+        achieved_gbs = ALGO_BYTES_PER_ENV_STEP * B / (kernel_ms * 1e-3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
         if os.path.exists(pmc):
@@ -162,10 +223,14 @@ def main():
                 p = json.load(f)
             if p.get("envs") == B:
                 traffic = p.get("hbm_bytes_per_launch")
-        flops_box = []
-        cpu = None
+        cpu, extra = None, []
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds, flops_box)
+            gpu_states = [ph.get(f) for f in (_lib.QPOS, _lib.QVEL, _lib.QACC_WARMSTART)]
+            threads = host_threads()
+            cpu = cpu_baseline(args.cpu_seconds, threads, gpu_states, nsub)
+            one = [s[: max(8, B // 256)] for s in gpu_states]
+            extra.append(cpu_baseline(args.cpu_seconds / 3, 1, one, nsub))
+            extra.append(cpu_baseline_reach_1env(args.cpu_seconds / 3))
         out = {
             "metric": "env-steps/sec (whole node), Shadow-hand cube reorient @4096 envs, 1/2/4/8 GPUs",
             "value": round(value, 1),
@@ -183,34 +248,42 @@ def main():
                 "workload": "reorient.state_dense, Shadow hand + cube, full contact + Newton solver",
                 "envs_per_gpu": B,
                 "global_envs": world * B,
-                "substeps_per_env_step": 5,
+                "substeps_per_env_step": nsub,
                 "physics_dt": 0.005,
-                "parallelism": f"env-sharded x{world}" + (", RCCL obs all-gather" if world > 1 else ""),
+                "parallelism": f"env-sharded x{world}" + (", RCCL obs all-gather (libdx)" if world > 1 else ""),
             },
+            # the path is FP32-VALU / latency bound: the headline
+            # roofline is the oracle-counted FLOPs per env-step over the step kernel's
+            # mean launch time against the FP32 vector peak; HBM is the secondary block
             "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 3),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "bound": "valu_fp32",
+                "achieved": round(achieved_tf, 4),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 5),
                 "traffic": traffic,
                 "kernel": "dx_step_kernel",
                 "kernel_ms_avg": round(kernel_ms, 4),
-                "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                "flops_per_env_step": round(flops),
+                "flops_sample": f"oracle stage counters over {len(idx)} env states of the GPU batch, {nsub} substeps",
+                "hbm": {
+                    "achieved": round(achieved_gbs, 3),
+                    "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s",
+                    "frac": round(achieved_gbs / HBM_PEAK_GBS, 6),
+                    "algo_bytes_per_env_step": ALGO_BYTES_PER_ENV_STEP,
+                    "traffic": traffic,
+                },
             },
             "cpu_baseline": cpu,
+            "cpu_baseline_extra": extra,
         }
-        if flops_box:
-            fl = flops_box[0]
-            out["roofline"]["valu_fp32"] = {
-                "flops_per_env_step": round(fl),
-                "achieved_tflops": round(fl * B / (kernel_ms * 1e-3) / 1e12, 4),
-                "peak_tflops": FP32_PEAK_TFLOPS,
-            }
         print(json.dumps(out), flush=True)
+    if collator:
+        collator.close()
     env.close()
-    if world > 1:
-        dist.destroy_process_group()
+    if comm:
+        comm.close()
 
 
 if __name__ == "__main__":

@@ -29,7 +29,10 @@ EXPORTS = (
     "dx_env_pack_outputs", "dx_timing_enable", "dx_timing_read", "dx_stage_timing", "dx_stage_read",
     "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout", "dx_env_goal_dim",
     "dx_jac_site", "dx_ik_solve",
+    "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
+    "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier",
 )
+COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
           "smooth_solve", "newton_eval", "newton_grad", "newton_hessian", "newton_chol", "newton_linesearch",
           "qfrc_constraint", "euler", "observe", "io", "matvec", "np_mpr", "jacvec")
@@ -122,6 +125,15 @@ def load(path: str = LIB_PATH):
     L.dx_debug_poison_lds.argtypes = [i32]
     L.dx_jac_site.argtypes = [vp, vp, i32, vp, vp]
     L.dx_ik_solve.argtypes = [vp, ctypes.POINTER(IkOptions), vp, i32, vp, i32, vp, vp, vp, vp, vp, vp]
+    L.dx_comm_unique_id.argtypes = [vp]
+    L.dx_comm_init.restype = vp
+    L.dx_comm_init.argtypes = [ctypes.c_char_p, i32, i32, i32]
+    L.dx_comm_destroy.argtypes = [vp]
+    L.dx_comm_rank.argtypes = [vp]
+    L.dx_comm_size.argtypes = [vp]
+    L.dx_allgather_obs.argtypes = [vp, vp, vp]
+    L.dx_comm_allreduce_max.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
+    L.dx_comm_barrier.argtypes = [vp]
     _lib = L
     return L
 

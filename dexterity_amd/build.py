@@ -8,8 +8,11 @@ launches the specialization whose layout equals the model's, else the generic ke
 
 from __future__ import annotations
 
+import concurrent.futures
 import glob
+import hashlib
 import os
+import re
 import subprocess
 import sys
 
@@ -35,23 +38,70 @@ def _stale() -> bool:
     return any(os.path.getmtime(p) > t for p in deps)
 
 
+FLAGS = (
+    # fp32 division / sqrt as v_rcp / v_sqrt (<= 1 ulp) instead of the correctly
+    # rounded ~10-instruction sequences: the kernels are latency bound and the
+    # parity tolerances are orders of magnitude above 1 ulp
+    "-O3", f"--offload-arch={ARCH}", "-fPIC", "-std=c++17",
+    "-fno-hip-fp32-correctly-rounded-divide-sqrt",
+    # no SLP packing of scalar fp32 math into v_pk_* (the operand shuffles cost
+    # more than the packing saves here), denormals flushed (no range scaling
+    # around v_sqrt / v_rcp)
+    "-fno-slp-vectorize", "-fgpu-flush-denormals-to-zero",
+)
+OBJ = os.path.join(ROOT, "build", "obj")
+
+
+def _spec_names() -> list:
+    if not os.path.exists(SPECS):
+        return []
+    m = re.search(r"#define DX_SPECS\(X\)(.*)", open(SPECS).read())
+    return re.findall(r"X\((\w+)\)", m.group(1)) if m else []
+
+
+def _units() -> list:
+    """(object name, source, extra flags): every source once, plus dx_step.hip once per
+    scene specialization (-DDX_SPEC_ONLY), so the kernels compile in parallel."""
+    units = [(os.path.splitext(s)[0], s, ()) for s in SOURCES]
+    units += [(f"dx_step_{n}", "dx_step.hip", (f"-DDX_SPEC_ONLY={n}",)) for n in _spec_names()]
+    return units
+
+
 def _compile(out: str, verbose: bool) -> None:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [
-        # fp32 division / sqrt as v_rcp / v_sqrt (<= 1 ulp) instead of the correctly
-        # rounded ~10-instruction sequences: the kernels are latency bound and the
-        # parity tolerances are orders of magnitude above 1 ulp
-        hipcc, "-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
-        "-fno-hip-fp32-correctly-rounded-divide-sqrt",
-        # no SLP packing of scalar fp32 math into v_pk_* (the operand shuffles cost
-        # more than the packing saves here), denormals flushed (no range scaling
-        # around v_sqrt / v_rcp)
-        "-fno-slp-vectorize", "-fgpu-flush-denormals-to-zero",
-        *[os.path.join(CSRC, s) for s in SOURCES], "-o", out,
-    ]
+    os.makedirs(OBJ, exist_ok=True)
+    h = hashlib.sha1()
+    for f in sorted(SOURCES + HEADERS + ("dx_specs.inc",)):
+        path = os.path.join(CSRC, f)
+        if os.path.exists(path):
+            h.update(f.encode() + open(path, "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "dx.h"), "rb").read())
+    h.update(" ".join(FLAGS).encode())
+    key = h.hexdigest()[:16]
+    jobs, objs = [], []
+    for name, src, extra in _units():
+        obj = os.path.join(OBJ, f"{name}.{key}.o")
+        objs.append(obj)
+        if not os.path.exists(obj):
+            jobs.append([hipcc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"])
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(cmd[-1], cmd[-1][: -len(".tmp")])
+
+    nproc = int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))
+    with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(nproc, 8))) as ex:
+        for f in [ex.submit(run, j) for j in jobs]:
+            f.result()
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-fPIC", "-shared", *objs, "-L/opt/rocm/lib", "-lrccl", "-o", out]
     if verbose:
-        print(" ".join(cmd))
+        print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
+    for old in glob.glob(os.path.join(OBJ, "*.o")):  # objects of other source versions
+        if old not in objs:
+            os.remove(old)
 
 
 def spec_text(lib_path: str) -> str:

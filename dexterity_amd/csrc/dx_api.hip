@@ -6,6 +6,7 @@
 // fp32 and uploads one read-only copy per device.  dx_batch owns the per-env
 // state arrays ([nenv][width], fp32) and a HIP stream.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
@@ -951,6 +952,17 @@ static void* field_base(dx_batch* b, int field) {
   return nullptr;
 }
 
+// A substep-queue launch that timed out waiting for a predecessor task aborts
+// (dx_step.hip step_queue); the batch state is then unusable.  Checked at every
+// host synchronisation point.
+static int queue_check(dx_batch* b) {
+  if (!b->db.qerr) return 0;
+  int err = 0;
+  HIPCHK(hipMemcpy(&err, b->db.qerr, 4, hipMemcpyDeviceToHost));
+  if (err) return fail(DX_EHIP, "substep queue timed out waiting for a predecessor task (launch aborted)");
+  return 0;
+}
+
 extern "C" int dx_field_ptr(dx_batch* b, int field, void** devptr) {
   if (!b || !devptr) return fail(DX_EINVAL, "null argument");
   void* p = field_base(b, field);
@@ -982,7 +994,7 @@ extern "C" int dx_get_field(dx_batch* b, int field, void* dst, int32_t env0, int
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipMemcpyAsync(dst, base + (size_t)env0 * w * 4, (size_t)n * w * 4, hipMemcpyDefault, b->stream));
   HIPCHK(hipStreamSynchronize(b->stream));
-  return 0;
+  return queue_check(b);
 }
 
 extern "C" int dx_set_xfrc(dx_batch* b, const float* xfrc, int32_t nbody) {
@@ -1060,9 +1072,10 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   timing_begin(b, &t0);
   hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
-  // every workgroup of a queued launch makes exactly one claim past the last task
-  if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
   HIPCHK(e);
+  // every workgroup of a queued launch makes exactly one claim past the last task
+  // (advanced only for a launch that was enqueued: the device counter moved with it)
+  if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
   // next launch: heaviest environments first (costs just measured)
   if (mode == 0 && b->db.order) HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order));
   return 0;
@@ -1207,7 +1220,7 @@ extern "C" int dx_sync(dx_batch* b) {
   if (!b) return fail(DX_EINVAL, "null batch");
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipStreamSynchronize(b->stream));
-  return 0;
+  return queue_check(b);
 }
 
 extern "C" int dx_debug_enable(dx_batch* b, int enable) {
@@ -1407,11 +1420,7 @@ static int env_run(dx_env* e, const float* action) {
 
 extern "C" int dx_env_reset(dx_env* e) {
   if (!e) return fail(DX_EINVAL, "null env");
-  std::vector<int> neg(e->P.nenv, -1);
-  // episode < 0 forces initialize_episode in the pre-kernel for every env
-  std::vector<int> cur(e->P.nenv);
-  HIPCHK(hipMemcpyAsync(cur.data(), e->S.episode, cur.size() * 4, hipMemcpyDeviceToHost, e->batch->stream));
-  HIPCHK(hipStreamSynchronize(e->batch->stream));
+  // step_type LAST makes the pre-kernel run initialize_episode for every env
   std::vector<int> last(e->P.nenv, 2);
   HIPCHK(hipMemcpyAsync(e->S.step_type, last.data(), last.size() * 4, hipMemcpyHostToDevice, e->batch->stream));
   HIPCHK(hipStreamSynchronize(e->batch->stream));
@@ -1510,7 +1519,7 @@ extern "C" int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count) {
   *total_ms = tot;
   *count = (int32_t)st.ev.size();
   st.ev.clear();
-  return 0;
+  return queue_check(b);
 }
 
 // packs [obs | reward | discount | step_type] per env into dst (device, [nenv][obs_dim+3])
@@ -1526,6 +1535,99 @@ extern "C" int dx_env_pack_outputs(dx_env* e, float* dst_dev) {
                      e->P.obs_dim, e->S.obs, e->S.reward, e->S.discount, e->S.step_type, dst_dev);
   HIPCHK(hipGetLastError());
   return 0;
+}
+
+// ------------------------------------------------------------------------ //
+// multi-GPU observation collation: RCCL (librccl) directly, no framework layer
+// ------------------------------------------------------------------------ //
+// One process per GPU.  Physics has no exchange (environments are independent);
+// the only collective is the per-control-step all-gather of the packed outputs,
+// enqueued on the env's stream right behind the task post kernel, so the host
+// never waits for it.  The gather is in place: this rank packs straight into its
+// own slice of dst.
+struct dx_comm {
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 1, device = 0;
+  hipStream_t stream = nullptr;  // barrier / scalar reductions
+  double* scalar = nullptr;      // device scratch for dx_comm_allreduce_max
+};
+
+#define NCCLCHK(x)                                                                                 \
+  do {                                                                                             \
+    ncclResult_t r_ = (x);                                                                         \
+    if (r_ != ncclSuccess) return fail(DX_EHIP, std::string(#x ": ") + ncclGetErrorString(r_));    \
+  } while (0)
+
+extern "C" int dx_comm_unique_id(void* id) {
+  if (!id) return fail(DX_EINVAL, "null id buffer");
+  static_assert(sizeof(ncclUniqueId) == DX_COMM_ID_BYTES, "RCCL unique id size");
+  ncclUniqueId u;
+  NCCLCHK(ncclGetUniqueId(&u));
+  memcpy(id, &u, sizeof(u));
+  return 0;
+}
+
+extern "C" dx_comm* dx_comm_init(const void* id, int32_t nranks, int32_t rank, int32_t device) {
+  if (!id || nranks < 1 || rank < 0 || rank >= nranks) { fail(DX_EINVAL, "bad comm arguments"); return nullptr; }
+  if (hipSetDevice(device) != hipSuccess) { fail(DX_EHIP, "hipSetDevice failed"); return nullptr; }
+  dx_comm* c = new dx_comm();
+  c->rank = rank;
+  c->nranks = nranks;
+  c->device = device;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, u, rank);
+  if (r != ncclSuccess) {
+    fail(DX_EHIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    delete c;
+    return nullptr;
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&c->scalar, sizeof(double)) != hipSuccess) {
+    fail(DX_EHIP, "comm stream / scratch allocation failed");
+    dx_comm_destroy(c);
+    return nullptr;
+  }
+  return c;
+}
+
+extern "C" void dx_comm_destroy(dx_comm* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) (void)ncclCommDestroy(c->comm);
+  if (c->scalar) (void)hipFree(c->scalar);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+extern "C" int dx_comm_rank(const dx_comm* c) { return c ? c->rank : fail(DX_EINVAL, "null comm"); }
+extern "C" int dx_comm_size(const dx_comm* c) { return c ? c->nranks : fail(DX_EINVAL, "null comm"); }
+
+extern "C" int dx_allgather_obs(dx_env* e, dx_comm* c, float* dst_dev) {
+  if (!e || !c || !dst_dev) return fail(DX_EINVAL, "null argument");
+  dx_batch* b = e->batch;
+  if (b->device != c->device) return fail(DX_EINVAL, "env and comm are on different devices");
+  const size_t count = (size_t)e->P.nenv * (e->P.obs_dim + 3);
+  float* mine = dst_dev + (size_t)c->rank * count;
+  if (int rc = dx_env_pack_outputs(e, mine)) return rc;
+  NCCLCHK(ncclAllGather(mine, dst_dev, count, ncclFloat32, c->comm, b->stream));
+  return 0;
+}
+
+extern "C" int dx_comm_allreduce_max(dx_comm* c, double* value) {
+  if (!c || !value) return fail(DX_EINVAL, "null argument");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpyAsync(c->scalar, value, sizeof(double), hipMemcpyHostToDevice, c->stream));
+  NCCLCHK(ncclAllReduce(c->scalar, c->scalar, 1, ncclFloat64, ncclMax, c->comm, c->stream));
+  HIPCHK(hipMemcpyAsync(value, c->scalar, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+extern "C" int dx_comm_barrier(dx_comm* c) {
+  double x = 0;
+  return dx_comm_allreduce_max(c, &x);
 }
 
 // Fills every CU's LDS with NaN bit patterns (test hook: the step kernel must not

@@ -2431,16 +2431,26 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     const int k = (int)(t - (unsigned)s * (unsigned)B.nenv);
     const int env = B.order ? B.order[k] : k;
     if (s > 0) {
+      int abort = 0;
       if (LANE == 0) {
         unsigned n = 0;
         while (__hip_atomic_load(B.progress + env, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != qtag(B.epoch, s)) {
           __builtin_amdgcn_s_sleep(2);
-          if (++n > (1u << 25)) {  // ~seconds: never expected; leave a mark and go on
+          // ~seconds without progress (never expected), or another task gave up: the
+          // launch is aborted -- no task computes on a state whose predecessor has
+          // not been published, and the next dx_sync reports the error
+          if (++n > (1u << 25)) {
             __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            abort = 1;
+            break;
+          }
+          if ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            abort = 1;
             break;
           }
         }
       }
+      if (__builtin_amdgcn_readfirstlane(abort)) continue;  // drain: later claims end the loop
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -2462,18 +2472,13 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   }
 }
 
-// The model struct is read through a device pointer (dx_api.hip device_model) in
-// the constant address space rather than passed by value in the kernarg segment.
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
-dx_step_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
-  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
-  if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
-  else step_body<SpecRT>(m, B, L, nsub, mode);
-}
-
 // ------------------------------------------------------------------------ //
 // model specializations (build.py writes dx_specs.inc from the shipped scenes)
 // ------------------------------------------------------------------------ //
+// build.py compiles this file once per specialization with -DDX_SPEC_ONLY=<spec>
+// (that translation unit holds only that scene's kernel and its launcher), and once
+// without it (generic kernel, dispatch, helper kernels), so the kernels compile in
+// parallel.
 #if __has_include("dx_specs.inc")
 #include "dx_specs.inc"
 #endif
@@ -2498,10 +2503,37 @@ static bool spec_matches(const DevModel& d, const Lds& L) {
   return true;
 }
 
+#define DX_SPEC_FNS(SP)                                                                               \
+  bool dx_match_##SP(const DevModel& d, const Lds& L);                                                \
+  hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
+                            const Lds& L, int nsub, int mode);
+
+#ifdef DX_SPEC_ONLY
+#define DX_SPEC_DEFINE(SP)                                                                            \
+  bool dx_match_##SP(const DevModel& d, const Lds& L) { return spec_matches<SP>(d, L); }             \
+  hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
+                            const Lds& L, int nsub, int mode) {                                       \
+    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
+    return hipGetLastError();                                                                         \
+  }
+#define DX_SPEC_DEFINE1(SP) DX_SPEC_DEFINE(SP)
+DX_SPEC_DEFINE1(DX_SPEC_ONLY)
+#else
+DX_SPECS(DX_SPEC_FNS)
+
+// The model struct is read through a device pointer (dx_api.hip device_model) in
+// the constant address space rather than passed by value in the kernarg segment.
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_step_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
+  else step_body<SpecRT>(m, B, L, nsub, mode);
+}
+
 // Index of the specialization whose layout and dimensions equal the model's, or -1.
 int dx_spec_find(const DevModel& d, const Lds& L) {
   int k = 0;
-#define DX_TRY(SP) if (spec_matches<SP>(d, L)) return k; k++;
+#define DX_TRY(SP) if (dx_match_##SP(d, L)) return k; k++;
   DX_SPECS(DX_TRY)
 #undef DX_TRY
   (void)k;
@@ -2536,11 +2568,8 @@ hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, i
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B,
                           const Lds& L, int nsub, int mode) {
   int k = 0;
-#define DX_LAUNCH(SP)                                                                                   \
-  if (spec == k) {                                                                                      \
-    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
-    return hipGetLastError();                                                                           \
-  }                                                                                                     \
+#define DX_LAUNCH(SP)                                                         \
+  if (spec == k) return dx_launch_##SP(grid, lds, stream, m, B, L, nsub, mode); \
   k++;
   DX_SPECS(DX_LAUNCH)
 #undef DX_LAUNCH
@@ -2562,3 +2591,4 @@ extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int
   for (int i = LANE; i < m.nu; i += blockDim.x) B.ctrl[(size_t)env * m.nu + i] = 0;
   if (LANE == 0) B.time[env] = 0;
 }
+#endif  // DX_SPEC_ONLY

@@ -65,8 +65,7 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
       B.qvel[(size_t)env * P.nv + i] = 0;
       B.qacc_ws[(size_t)env * P.nv + i] = 0;
     }
-    if (action)
-      for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = 0;
+    for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = 0;  // mj_resetData
     B.time[env] = 0;
     if (P.kind == DX_KIND_REORIENT) {
       // reorient.py:182-188: goal first (GoalTask.initialize_episode), then the prop

@@ -1,16 +1,28 @@
-"""Multi-GPU sharding and observation collation.
+"""Multi-GPU sharding and observation collation, torch-free.
 
-Environments are independent: rank r of W owns the contiguous env range
-`env_shard(B_global, r, W)` on its own GPU and steps it with no data-path
-collective.  The only exchange is one all-gather per control step of each rank's
-packed `[obs | reward | discount | step_type]` rows (dx_env_pack_outputs), which
-over RCCL/xGMI is ~2 MB per rank at 4096 envs.  The same code runs on gloo for the
-CPU tests.
+Environments are independent. Rank r of W owns the contiguous env range
+`env_shard(B_global, r, W)` on its own GPU and steps it with no data-path collective.
+The only exchange is one all-gather per control step of each rank's packed
+`[obs | reward | discount | step_type]` rows. That gather is `dx_allgather_obs` in
+libdx, which calls RCCL (librccl) directly over xGMI: about 2 MB per rank at 4096 envs.
+
+Bootstrap: rank 0 creates the RCCL unique id (`dx_comm_unique_id`) and publishes it
+in a file named by the job key. Every rank reads it before `dx_comm_init`. A job
+launched by `torch.distributed.run` (the bench contract's launcher) gives every rank
+the same MASTER_PORT and the same parent process (the launcher's agent), so
+`job_key()` is unique per job without any extra rendezvous. The launcher is the only
+torch component involved, and nothing here imports torch.
 """
 
 from __future__ import annotations
 
-from typing import Tuple
+import ctypes
+import os
+import tempfile
+import time
+from typing import Callable, Optional, Tuple
+
+from dexterity_amd import _lib
 
 
 def env_shard(global_envs: int, rank: int, world: int) -> Tuple[int, int]:
@@ -29,38 +41,149 @@ def rank_seed(seed: int, rank: int) -> int:
     return int(seed) + int(rank)
 
 
+def gathered_rows(rank: int, n_per_rank: int) -> slice:
+    """Rows of the gathered [W * n, width] buffer that hold rank `rank`'s envs (the
+    in-place all-gather of dx_allgather_obs packs each rank into its own slice)."""
+    return slice(rank * n_per_rank, (rank + 1) * n_per_rank)
+
+
+def job_key() -> str:
+    """Same string on every rank of one launcher job, different across jobs."""
+    return f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+
+
+def exchange_id(rank: int, key: str, make_id: Callable[[], bytes], timeout: float = 120.0,
+                directory: Optional[str] = None) -> bytes:
+    """Rank 0 calls make_id() and publishes the bytes; every rank returns them.
+
+    The file is written to a temporary name and renamed, so a reader never sees a
+    partial id. Rank 0 removes the file once the id is consumed (on the next call with
+    the same key, or at exit of the job through `cleanup_id`)."""
+    directory = directory or tempfile.gettempdir()
+    path = os.path.join(directory, f"dx_comm_{key}.id")
+    if rank == 0:
+        data = bytes(make_id())
+        tmp = f"{path}.{os.getpid()}.tmp"
+        with open(tmp, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+        return data
+    t0 = time.monotonic()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                data = f.read()
+            if data:
+                return data
+        except FileNotFoundError:
+            pass
+        if time.monotonic() - t0 > timeout:
+            raise TimeoutError(f"rank {rank}: no communicator id at {path} after {timeout:.0f} s")
+        time.sleep(0.01)
+
+
+def cleanup_id(key: str, directory: Optional[str] = None) -> None:
+    path = os.path.join(directory or tempfile.gettempdir(), f"dx_comm_{key}.id")
+    try:
+        os.remove(path)
+    except FileNotFoundError:
+        pass
+
+
+class Comm:
+    """An RCCL communicator owned by libdx (dx_comm_* in include/dx.h)."""
+
+    def __init__(self, rank: int, world: int, device: int, key: Optional[str] = None):
+        L = _lib.load()
+        self.rank, self.world, self.device = int(rank), int(world), int(device)
+        self.key = key or job_key()
+
+        def make_id() -> bytes:
+            buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+            _lib.check(L.dx_comm_unique_id(buf))
+            return buf.raw
+
+        uid = exchange_id(self.rank, self.key, make_id)
+        self.ptr = L.dx_comm_init(uid, self.world, self.rank, self.device)
+        if not self.ptr:
+            raise _lib.DxError(f"dx_comm_init failed: {L.dx_last_error().decode()}")
+        self.barrier()  # every rank holds the id now
+        if self.rank == 0:
+            cleanup_id(self.key)
+
+    @classmethod
+    def from_env(cls, device: Optional[int] = None) -> "Comm":
+        rank = int(os.environ.get("RANK", "0"))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        return cls(rank, world, local if device is None else device)
+
+    def barrier(self) -> None:
+        _lib.check(_lib.load().dx_comm_barrier(self.ptr))
+
+    def max(self, value: float) -> float:
+        """Max over ranks of a host scalar (blocking)."""
+        v = ctypes.c_double(float(value))
+        _lib.check(_lib.load().dx_comm_allreduce_max(self.ptr, ctypes.byref(v)))
+        return v.value
+
+    def close(self) -> None:
+        if getattr(self, "ptr", None) and _lib._lib is not None:
+            _lib._lib.dx_comm_destroy(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        self.close()
+
+
 class OutputCollator:
-    """All-gathers equally sized per-rank [n, width] float32 shards into [W*n, width]."""
+    """The gathered [W * n, obs_dim + 3] float32 buffer of a sharded job, in device
+    memory on this rank's GPU; `gather()` enqueues dx_allgather_obs on the env's
+    stream (no host synchronisation)."""
 
-    def __init__(self, n_per_rank: int, width: int, device):
-        import torch
-        import torch.distributed as dist
+    def __init__(self, env, comm: Comm):
+        self.env, self.comm = env, comm
+        self.width = env.obs_dim + 3
+        self.rows = comm.world * env.num_envs
+        self.nbytes = self.rows * self.width * 4
+        self.ptr = _device_alloc(self.nbytes)
 
-        self.dist = dist
-        self.world = dist.get_world_size()
-        self.shard = torch.empty((n_per_rank, width), dtype=torch.float32, device=device)
-        self.gathered = torch.empty((self.world * n_per_rank, width), dtype=torch.float32, device=device)
-        self._use_tensor_api = dist.get_backend() != "gloo"
-        if not self._use_tensor_api:
-            self._parts = list(self.gathered.chunk(self.world, dim=0))
+    def gather(self) -> int:
+        _lib.check(_lib.load().dx_allgather_obs(self.env.ptr, self.comm.ptr, ctypes.c_void_p(self.ptr)))
+        return self.ptr
 
-    def gather(self):
-        """Collective over the current contents of `self.shard`; returns `self.gathered`."""
-        if self._use_tensor_api:
-            self.dist.all_gather_into_tensor(self.gathered, self.shard)
-        else:
-            parts = [p.clone() for p in self._parts]
-            self.dist.all_gather(parts, self.shard)
-            for dst, src in zip(self._parts, parts):
-                dst.copy_(src)
-        return self.gathered
+    def read(self):
+        """Host copy of the gathered buffer (synchronises the env's stream)."""
+        import numpy as np
+
+        from dexterity_amd.manipulation import _copy_d2h
+
+        self.env.physics.sync()
+        out = np.empty((self.rows, self.width), dtype=np.float32)
+        _copy_d2h(out, self.ptr)
+        return out
+
+    def close(self) -> None:
+        if getattr(self, "ptr", None):
+            _device_free(self.ptr)
+        self.ptr = None
+
+    def __del__(self):
+        self.close()
 
 
-def max_over_ranks(seconds: float, device) -> float:
-    """The bench contract's job time: the slowest rank's elapsed seconds."""
-    import torch
-    import torch.distributed as dist
+def _device_alloc(nbytes: int) -> int:
+    from dexterity_amd.manipulation import _hip_runtime
 
-    t = torch.tensor([seconds], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    hip = _hip_runtime()
+    p = ctypes.c_void_p()
+    rc = hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes))
+    if rc != 0 or not p.value:
+        raise _lib.DxError(f"hipMalloc({nbytes}) failed ({rc})")
+    return p.value
+
+
+def _device_free(ptr: int) -> None:
+    from dexterity_amd.manipulation import _hip_runtime
+
+    _hip_runtime().hipFree(ctypes.c_void_p(ptr))

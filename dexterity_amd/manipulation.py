@@ -296,11 +296,13 @@ class GoalEnvironment:
             _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(int(action))))
             return None
         a = np.ascontiguousarray(action, dtype=np.float32).reshape(self.num_envs, -1)
-        _lib.check(_lib.load().dx_set_field(self.physics.ptr, _lib.CTRL, a.ctypes.data, 0, self.num_envs))
-        # copy host actions into the device action buffer via the ctrl field
-        ctrl_ptr = self.physics.field_ptr(_lib.CTRL)
+        if a.shape[1] != self.model.nu:
+            raise ValueError(f"action must be [{self.num_envs}, {self.model.nu}], got {a.shape}")
+        # host actions go into the library's device action buffer (the pre-kernel
+        # reads it and writes ctrl: mujoco_actuation.py:33)
         self.physics.sync()
-        _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(ctrl_ptr)))
+        _copy_h2d(self._dev_action, a)
+        _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(self._dev_action)))
         return self.timestep()
 
     def sample_actions(self, step: int) -> int:
@@ -338,8 +340,8 @@ class GoalEnvironment:
         return self._read(_lib.OUT_SUCCESSES, np.int32, 1)[:, 0]
 
 
-def _copy_d2h(out: np.ndarray, devptr: int) -> None:
-    """Device -> host copy through the HIP runtime libdx is linked against."""
+def _hip_runtime():
+    """The HIP runtime libdx is linked against (for plain host<->device copies)."""
     global _hip
     if _hip is None:
         try:
@@ -347,7 +349,19 @@ def _copy_d2h(out: np.ndarray, devptr: int) -> None:
         except OSError:
             _hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so")
         _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    rc = _hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(devptr), out.nbytes, 2)  # DeviceToHost
+        _hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+        _hip.hipFree.argtypes = [ctypes.c_void_p]
+    return _hip
+
+
+def _copy_d2h(out: np.ndarray, devptr: int) -> None:
+    rc = _hip_runtime().hipMemcpy(out.ctypes.data, ctypes.c_void_p(devptr), out.nbytes, 2)  # DeviceToHost
+    if rc != 0:
+        raise _lib.DxError(f"hipMemcpy failed ({rc})")
+
+
+def _copy_h2d(devptr: int, src: np.ndarray) -> None:
+    rc = _hip_runtime().hipMemcpy(ctypes.c_void_p(devptr), src.ctypes.data, src.nbytes, 1)  # HostToDevice
     if rc != 0:
         raise _lib.DxError(f"hipMemcpy failed ({rc})")
 

@@ -189,6 +189,30 @@ int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
  * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */
 int dx_env_pack_outputs(dx_env* e, float* dst_dev);
 
+/* Multi-GPU observation collation over RCCL -------- */
+/* The reference runs one environment per process and has no collective; here each
+ * process (one per GPU) owns a dx_env shard of the job's environments and the only
+ * exchange is one all-gather of the packed outputs per control step, over xGMI.
+ * Bootstrap: rank 0 calls dx_comm_unique_id and hands the DX_COMM_ID_BYTES bytes to
+ * every rank (file, env var, socket: the caller's choice) before dx_comm_init. */
+typedef struct dx_comm dx_comm;
+#define DX_COMM_ID_BYTES 128
+int dx_comm_unique_id(void* id /* DX_COMM_ID_BYTES */);
+/* Collective over nranks processes (ncclCommInitRank); device = this rank's GPU. */
+dx_comm* dx_comm_init(const void* id, int32_t nranks, int32_t rank, int32_t device);
+void dx_comm_destroy(dx_comm* c);
+int dx_comm_rank(const dx_comm* c);
+int dx_comm_size(const dx_comm* c);
+/* All-gather of every rank's packed [obs | reward | discount | step_type] rows into
+ * dst ([nranks * nenv][obs_dim + 3] f32, device memory on this rank's GPU): rank r's
+ * environments land at rows [r * nenv, (r + 1) * nenv).  Enqueued on the env's stream
+ * after its step (no host synchronisation); every rank must pass an env with the same
+ * nenv and obs_dim. */
+int dx_allgather_obs(dx_env* e, dx_comm* c, float* dst_dev);
+/* Blocking max over ranks of a host scalar (also a barrier): the bench's job time. */
+int dx_comm_allreduce_max(dx_comm* c, double* value);
+int dx_comm_barrier(dx_comm* c);
+
 /* Kinematic queries and batched inverse kinematics ---------------------- */
 /* mj_jacSite (utils/mujoco_utils.py:67-73, compute_object_6d_jacobian) for every env
  * at its current qpos (kinematics + com positions are recomputed first; the batch's

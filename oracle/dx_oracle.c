@@ -1760,10 +1760,17 @@ void dxo_flops_reset(dxo_data* d) { memset(d->flops, 0, sizeof(d->flops)); }
 
 int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                    const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads) {
+  return dxo_batch_step_counted(m, nenv, nsub, qpos, qvel, ctrl, qacc_warmstart, xfrc, nthreads, NULL);
+}
+
+int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
+                           const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads,
+                           double* flops) {
   int err = 0;
+  double fsum = 0;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel reduction(| : err)
+#pragma omp parallel reduction(| : err) reduction(+ : fsum)
 #endif
   {
     dxo_data* d = dxo_data_create(m);
@@ -1781,7 +1788,9 @@ int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double*
       memcpy(qvel + (size_t)e * m->nv, d->qvel, 8 * m->nv);
       memcpy(qacc_warmstart + (size_t)e * m->nv, d->qacc_warmstart, 8 * m->nv);
     }
+    for (int k = 0; k < DXO_NSTAGE; k++) fsum += d->flops[k];
     dxo_data_free(d);
   }
+  if (flops) *flops = fsum;
   return err ? -1 : 0;
 }

@@ -83,6 +83,10 @@ void dxo_flops_reset(dxo_data* d);
 int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                    const double* ctrl, double* qacc_warmstart, const double* xfrc,
                    int nthreads);
+/* Same, also returning the summed FLOP counters of all envs and substeps. */
+int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
+                           const double* ctrl, double* qacc_warmstart, const double* xfrc,
+                           int nthreads, double* flops);
 
 #ifdef __cplusplus
 }

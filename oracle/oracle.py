@@ -56,6 +56,8 @@ def lib():
         L.dxo_flops_reset.argtypes = [vp]
         L.dxo_batch_step.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip]
         L.dxo_batch_step.restype = ip
+        L.dxo_batch_step_counted.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip, dp]
+        L.dxo_batch_step_counted.restype = ip
         L.dxo_fk.argtypes = [vp, vp]
         L.dxo_fk.restype = ip
         L.dxo_jac_site.argtypes = [vp, vp, ip, dp, dp]
@@ -170,12 +172,16 @@ class OracleData:
         lib().dxo_flops_reset(self.ptr)
 
 
-def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub: int, nthreads: int = 0):
-    """Steps nenv independent envs nsub times (OpenMP over envs). Arrays are updated in place."""
+def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub: int, nthreads: int = 0,
+               flops: list = None):
+    """Steps nenv independent envs nsub times (OpenMP over envs). Arrays are updated in
+    place (when already contiguous float64). With `flops` (a list), appends the summed
+    FLOP count of every env and substep."""
     dp = ctypes.POINTER(ctypes.c_double)
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (qpos, qvel, ctrl, qacc_warmstart)]
     x = None if xfrc is None else np.ascontiguousarray(xfrc, dtype=np.float64)
-    rc = lib().dxo_batch_step(
+    fl = ctypes.c_double(0.0)
+    rc = lib().dxo_batch_step_counted(
         model.ptr,
         arrs[0].shape[0],
         nsub,
@@ -185,5 +191,8 @@ def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub:
         arrs[3].ctypes.data_as(dp),
         None if x is None else x.ctypes.data_as(dp),
         nthreads,
+        ctypes.byref(fl),
     )
+    if flops is not None:
+        flops.append(fl.value)
     return rc, arrs[0], arrs[1], arrs[3]

@@ -1,8 +1,10 @@
-"""N>1 path on CPU: env sharding, rank seeds, and the packed-output all-gather over
-gloo with world_size 2 (the same collator bench.py drives over RCCL)."""
+"""N>1 path on CPU (no GPU, no torch): env sharding, rank seeds, the gathered-buffer
+layout, and the communicator-id bootstrap between two processes (the file exchange
+every rank of a torch.distributed.run job performs before dx_comm_init).  The RCCL
+all-gather itself runs on the GPU (tests/test_gpu_parity.py::test_allgather_world1)."""
 
+import multiprocessing as mp
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -26,57 +28,46 @@ def test_env_shard_partitions():
         distributed.env_shard(10, 2, 2)
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
+def test_gathered_rows_cover_the_job():
+    world, n = 8, 4096
+    seen = np.zeros(world * n, dtype=int)
+    for r in range(world):
+        sl = distributed.gathered_rows(r, n)
+        assert sl.start == distributed.env_shard(world * n, r, world)[0]
+        seen[sl] += 1
+    assert np.all(seen == 1)
+    assert distributed.rank_seed(12345, 3) == 12348
 
 
-def _worker(rank, world, port, n, width, q):
-    import torch
-    import torch.distributed as dist
+def _exchange_worker(rank, key, directory, q):
+    def make_id():
+        return bytes(range(128))[::-1] if rank == 0 else b"wrong"
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        col = distributed.OutputCollator(n, width, device="cpu")
-        for step in range(3):
-            # rows of rank r at step s: value = 1000*r + 10*s + column, row index in last col
-            rows = torch.arange(width, dtype=torch.float32).repeat(n, 1) + 1000 * rank + 10 * step
-            rows[:, -1] = torch.arange(n, dtype=torch.float32)
-            col.shard.copy_(rows)
-            g = col.gather().clone()
-            if rank == 0:
-                q.put(("gather", step, g.numpy()))
-        t = distributed.max_over_ranks(0.5 + rank, "cpu")
-        if rank == 0:
-            q.put(("max", 0, t))
-    finally:
-        dist.destroy_process_group()
+    q.put((rank, distributed.exchange_id(rank, key, make_id, timeout=60, directory=directory)))
 
 
-def test_collator_gloo_world2():
-    import torch.multiprocessing as mp
-
+def test_id_exchange_world2(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    world, n, width = 2, 5, 7
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, width, q)) for r in range(world)]
+    key = f"test_{os.getpid()}"
+    # rank 1 starts first: it must wait for rank 0's file, never read a partial one
+    procs = [ctx.Process(target=_exchange_worker, args=(r, key, str(tmp_path), q)) for r in (1, 0)]
     for p in procs:
         p.start()
-    got = [q.get(timeout=120) for _ in range(4)]
+    got = dict(q.get(timeout=120) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    gathers = {s: g for kind, s, g in got if kind == "gather"}
-    for step, g in gathers.items():
-        assert g.shape == (world * n, width)
-        for r in range(world):
-            blk = g[r * n:(r + 1) * n]
-            np.testing.assert_array_equal(blk[:, 0], 1000 * r + 10 * step)
-            np.testing.assert_array_equal(blk[:, -1], np.arange(n))
-    assert [v for kind, _, v in got if kind == "max"] == [1.5]
+    assert got[0] == got[1] == bytes(range(128))[::-1]
+    distributed.cleanup_id(key, str(tmp_path))
+    assert not list(tmp_path.iterdir())
+
+
+def test_id_exchange_times_out(tmp_path):
+    with pytest.raises(TimeoutError):
+        distributed.exchange_id(1, "nobody", lambda: b"", timeout=0.2, directory=str(tmp_path))
+
+
+def test_job_key_is_shared_by_launcher_children(monkeypatch):
+    monkeypatch.setenv("MASTER_PORT", "29511")
+    assert distributed.job_key() == f"29511_{os.getppid()}"
