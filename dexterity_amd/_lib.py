@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("DX_LIB") or os.path.join(_HERE, "libdx.so")  # DX_LIB
 # dx_field
 QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
 SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST = 6, 7, 8, 9, 10, 11, 12, 13, 14
+SENSOR_TORQUE = 15
 INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST)
 
 EXPORTS = (
@@ -30,7 +31,7 @@ EXPORTS = (
     "dx_debug_poison_lds", "dx_hull_support", "dx_model_layout", "dx_env_goal_dim",
     "dx_jac_site", "dx_ik_solve",
     "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
-    "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier",
+    "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -102,6 +103,7 @@ def load(path: str = LIB_PATH):
     L.dx_stream.argtypes = [vp]
     L.dx_sync.argtypes = [vp]
     L.dx_debug_enable.argtypes = [vp, ctypes.c_int]
+    L.dx_sensor_enable.argtypes = [vp, ctypes.c_int]
     L.dx_debug_get.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.dx_last_error.restype = ctypes.c_char_p
     L.dx_abi_version.restype = ctypes.c_int

@@ -21,7 +21,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdx.so")
 SPECS = os.path.join(CSRC, "dx_specs.inc")
-SOURCES = ("dx_step.hip", "dx_ik.hip", "dx_task.hip", "dx_api.hip")
+SOURCES = ("dx_step.hip", "dx_ik.hip", "dx_task.hip", "dx_sensor.hip", "dx_api.hip")
 HEADERS = ("dx_internal.h", "dx_device.h")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 DIMS = ("nq", "nv", "nbody", "njnt", "nu", "ntendon", "nsite", "nlevel", "nroot", "nfric", "nlimj", "nlimt",

@@ -737,6 +737,7 @@ extern "C" int dx_field_width(const dx_model* m, int field) {
     case DX_SITE_VEL: return 6 * d.nsite;
     case DX_XPOS: return 3 * d.nbody;
     case DX_XQUAT: return 4 * d.nbody;
+    case DX_SENSOR_TORQUE: return 3 * d.nbody;
   }
   return fail(DX_EINVAL, "unknown field");
 }
@@ -825,6 +826,8 @@ struct dx_batch {
   float* xfrc;
   std::vector<void*> allocs;
   bool debug;
+  float* sensor = nullptr;  // DX_SENSOR_TORQUE [nenv][nbody][3] (allocated by dx_sensor_enable)
+  float* sen_stash = nullptr;
 };
 
 static int balloc(dx_batch* b, void** p, size_t bytes) {
@@ -948,6 +951,7 @@ static void* field_base(dx_batch* b, int field) {
     case DX_NITER: return B.niter;
     case DX_NCAND: return B.ncand;
     case DX_STEP_COST: return B.cost;
+    case DX_SENSOR_TORQUE: return b->sensor;
   }
   return nullptr;
 }
@@ -1076,6 +1080,10 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   // every workgroup of a queued launch makes exactly one claim past the last task
   // (advanced only for a launch that was enqueued: the device counter moved with it)
   if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
+  // torque sensors from the last substep's stash (mode 0 step, mode 1 forward)
+  if (b->db.sen_stash && mode != 2)
+    HIPCHK(dx_launch_sensor(b->nenv, ((size_t)b->model->lds.total + 6 * DX_MAX_NV) * 4, b->stream, b->dm_dev, b->db,
+                            b->model->lds, b->sensor));
   // next launch: heaviest environments first (costs just measured)
   if (mode == 0 && b->db.order) HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order));
   return 0;
@@ -1221,6 +1229,22 @@ extern "C" int dx_sync(dx_batch* b) {
   HIPCHK(hipSetDevice(b->device));
   HIPCHK(hipStreamSynchronize(b->stream));
   return queue_check(b);
+}
+
+extern "C" int dx_sensor_enable(dx_batch* b, int enable) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  DevBatch& B = b->db;
+  if (enable) {
+    if (!b->sen_stash) {
+      const size_t E = b->nenv, words = (size_t)b->dm.nq + 2 * b->dm.nv + 1 + 8 * DX_NCON_MAX;
+      if (int rc = balloc(b, (void**)&b->sen_stash, E * words * 4)) return rc;
+      if (int rc = balloc(b, (void**)&b->sensor, E * 3 * b->dm.nbody * 4)) return rc;
+    }
+    B.sen_stash = b->sen_stash;
+  } else {
+    B.sen_stash = nullptr;  // buffers stay allocated (and the field readable) until destroy
+  }
+  return 0;
 }
 
 extern "C" int dx_debug_enable(dx_batch* b, int enable) {

@@ -113,6 +113,9 @@ struct DevBatch {
   unsigned* progress;
   unsigned epoch, qbase;
   int* qerr;
+  // torque sensors (dx_sensor.hip): the last substep's pre-integration state, solved
+  // qacc and contact forces, [nenv][dx_sensor_stash_words]; null when the field is off
+  float* sen_stash;
 };
 #define DX_NSTAGE 40
 
@@ -177,6 +180,10 @@ int dx_spec_find(const DevModel& d, const Lds& L);
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);
+
+// dx_sensor.hip: joint torque sensors from the step kernel's stash (host side)
+hipError_t dx_launch_sensor(int nenv, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
+                            const Lds& L, float* out);
 
 // dx_ik.hip: site Jacobians and batched damped-least-squares IK (host side).
 struct IkDev {

@@ -2317,10 +2317,41 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
   if (LANE == 0) B.time[env] = time;
 }
 
+// Torque sensors (dx_sensor.hip), when enabled: the state the sensors of mj_step2
+// read -- pre-integration qpos / qvel, the solved qacc -- and every contact's bodies,
+// point and world-frame force on body 2 (the contact-frame forces jac_t_force left in
+// cw, decoded from the pyramid rows, rotated by the contact frame).
+template <class Ctx>
+__device__ __forceinline__ void sensor_stash(const Ctx& c, const DevBatch& B, int env) {
+  const DevModel& m = c.mdl();
+  const int nq = c.nq, nv = c.nv;
+  float* o = B.sen_stash + (size_t)env * (nq + 2 * nv + 1 + 8 * DX_NCON_MAX);
+  for (int i = LANE; i < nq; i += DX_WAVE) o[i] = c.f(c.L.qpos)[i];
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    o[nq + i] = c.f(c.L.qvel)[i];
+    o[nq + nv + i] = c.f(c.L.qacc)[i];
+  }
+  const int n = c.I[I_NEFC] > 0 ? c.I[I_NCON] : 0;
+  if (LANE == 0) o[nq + 2 * nv] = __int_as_float(n);
+  const float* con = c.f(c.L.con);
+  const float* cw = c.f(c.L.cw);
+  for (int ci = LANE; ci < n; ci += DX_WAVE) {
+    const float* r = con + DX_CON_STRIDE * ci;
+    const int gp = __float_as_int(r[13]);
+    float* q = o + nq + 2 * nv + 1 + 8 * ci;
+    q[0] = __int_as_float(m.geom_bodyid[m.gpair_geom[2 * gp]]);
+    q[1] = __int_as_float(m.geom_bodyid[m.gpair_geom[2 * gp + 1]]);
+    q[2] = r[0]; q[3] = r[1]; q[4] = r[2];
+    const float f0 = cw[3 * ci], f1 = cw[3 * ci + 1], f2 = cw[3 * ci + 2];
+    for (int k = 0; k < 3; k++) q[5 + k] = r[3 + k] * f0 + r[6 + k] * f1 + r[9 + k] * f2;
+  }
+}
+
 // One physics step (mj_step): forward, warm start <- solved qacc, Euler.
 template <class Ctx>
-__device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time) {
+__device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time, int env = -1) {
   forward(c, B.xfrc);
+  if (env >= 0 && B.sen_stash) sensor_stash(c, B, env);
   float* ws = c.f(c.L.v5);
   for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
   SYNC();
@@ -2394,8 +2425,12 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   int steps = mode == 0 ? nsub : 1;
   if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
   for (int s = 0; s < steps; s++) {
-    if (mode == 0) env_substep(c, B, time);
-    else forward(c, B.xfrc);
+    if (mode == 0) {
+      env_substep(c, B, time, s == steps - 1 ? env : -1);
+    } else {
+      forward(c, B.xfrc);
+      if (B.sen_stash) sensor_stash(c, B, env);
+    }
   }
   env_finish(c, B, env, time);
   if (LANE == 0 && B.cost && mode == 0)
@@ -2458,7 +2493,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     c.stage_acc = B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr;
     c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
     float time = env_begin(c, B, env);
-    if (!(B.skip && B.skip[env])) env_substep(c, B, time);  // a freshly reset env is only observed
+    if (!(B.skip && B.skip[env])) env_substep(c, B, time, s == nsub - 1 ? env : -1);  // a freshly reset env is only observed
     if (s == nsub - 1) env_finish(c, B, env, time);
     else env_store_state(c, B, env, time);
     if (LANE == 0 && B.cost) {

@@ -559,6 +559,25 @@ class CompiledModel:
     def name2id(self, kind: str, name: str) -> int:
         return self.names[kind].index(name)
 
+    def disabled(self, *flags: str) -> "CompiledModel":
+        """A copy with MuJoCo subsystems switched off, as
+        `physics.model.disable("contact", "gravity", "actuation")` does in the reference
+        (hands_test.py:171; [3P] mjDSBL_CONTACT / mjDSBL_GRAVITY / mjDSBL_ACTUATION):
+        no collision, zero gravity (the bias force and rnePostConstraint's base
+        acceleration), zero actuator forces."""
+        arrays = {k: np.array(v, copy=True) for k, v in self.arrays.items()}
+        for f in flags:
+            if f == "contact":
+                arrays["disable_contact"] = np.array([1], np.int32)
+            elif f == "gravity":
+                arrays["gravity"] = np.zeros_like(arrays["gravity"])
+            elif f == "actuation":
+                arrays["actuator_gainprm"] = np.zeros_like(arrays["actuator_gainprm"])
+                arrays["actuator_biasprm"] = np.zeros_like(arrays["actuator_biasprm"])
+            else:
+                raise ValueError(f"unknown disable flag {f!r}")
+        return CompiledModel(arrays, {k: list(v) for k, v in self.names.items()})
+
 
 _SCALAR_INT = {
     "nq", "nv", "nbody", "njnt", "ngeom", "nsite", "nu", "ntendon", "nwrap", "nmesh",

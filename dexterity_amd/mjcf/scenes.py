@@ -14,6 +14,8 @@ compiled blobs under `assets/` are what the runtime (and the GPU box) loads.
   collisions disabled (`reach.py:131-132`), dt 0.02.
 * `shadow_reach`     -- BASELINE.json config 2 naming (reach with the Shadow hand,
   contact-free smooth dynamics), dt 0.02.
+* `adroit_hand`      -- the Adroit hand alone (the reference's hands_test.py physics
+  known-answer tests), dt 0.002, iterations 20.
 * `bimanual_handover` -- BASELINE.json config 5 (synthetic; the reference has no
   bimanual task): two Shadow hands welded to the world palm-up side by side at the
   Juggle task's x offsets (`juggle.py:22-26`, +-0.1 m, here +-0.12 m so the palms do not
@@ -80,6 +82,18 @@ def adroit_reach():
     return scene.compile()
 
 
+def adroit_hand():
+    """The Adroit hand alone, as `mjcf.Physics.from_mjcf_model(AdroitHand().mjcf_model)`
+    builds it in the reference's hand tests (hands_test.py:167-169, 211-212): the
+    vendor MJCF is the root model, so its own `<option iterations="20">`
+    (adroit_hand.xml:12) applies and the timestep is MuJoCo's default 0.002 s; no
+    arena, no ground, the hand at its MJCF pose."""
+    scene = Scene(timestep=0.002)
+    scene.iterations = 20
+    scene.attach_mjcf(ADROIT_XML, "adroit_hand/")
+    return scene.compile()
+
+
 BIMANUAL_OFFSET = 0.12
 
 
@@ -102,5 +116,6 @@ SCENES = {
     "shadow_reorient": shadow_reorient,
     "shadow_reach": shadow_reach,
     "adroit_reach": adroit_reach,
+    "adroit_hand": adroit_hand,
     "bimanual_handover": bimanual_handover,
 }

@@ -136,6 +136,18 @@ class BatchedPhysics:
                                            None if jr is None else jr.ctypes.data))
         return jp, jr
 
+    def enable_sensors(self, enable: bool = True) -> None:
+        """Joint torque sensors (DX_SENSOR_TORQUE) computed by every step / forward."""
+        _lib.check(_lib.load().dx_sensor_enable(self.ptr, int(enable)))
+
+    def joint_torques(self, joints, axes) -> np.ndarray:
+        """`DexterousHandObservables.joint_torques` (dexterous_hand.py:266-275): each
+        joint's 3-axis torque sensor (a site at its body origin) projected on the
+        joint axis; joints are (body id) per joint, axes [njoint, 3] in the body frame."""
+        s = self.get(_lib.SENSOR_TORQUE).reshape(self.nenv, -1, 3)
+        bodies = np.asarray(joints, dtype=int)
+        return np.einsum("ejk,jk->ej", s[:, bodies, :], np.asarray(axes, dtype=np.float64))
+
     def debug(self, enable: bool = True) -> None:
         _lib.check(_lib.load().dx_debug_enable(self.ptr, int(enable)))
 

@@ -72,6 +72,11 @@ enum dx_field {
   DX_NCAND = 13,        /* 1  (int32 bits) narrowphase candidates of the last collision pass */
   DX_STEP_COST = 14,    /* 1  (uint32 bits) shader cycles / 1024 the env's last dx_step took
                            (feeds the longest-first dispatch order; 0 if disabled) */
+  DX_SENSOR_TORQUE = 15,/* 3*nbody  r  (after dx_sensor_enable): 3-axis `torque` sensor of a
+                           site at each body's origin, in the body frame -- the joint torque
+                           sensors of shadow_hand_e.py:176-196 / adroit_hand.py:153-172
+                           (mj_rnePostConstraint + mj_sensorAcc of the last substep, before
+                           its integration, as after dm_control's physics.step()) */
   DX_NFIELD
 };
 
@@ -125,6 +130,11 @@ int dx_forward(dx_batch* b);
 /* Stream the batch's kernels are enqueued on (hipStream_t) and a blocking sync. */
 void* dx_stream(dx_batch* b);
 int dx_sync(dx_batch* b);
+
+/* Sensors ---------------------------------------------------------------- */
+/* Enables DX_SENSOR_TORQUE: dx_step / dx_forward then also compute every body's torque
+ * sensor (one extra small kernel per call; nothing when disabled). */
+int dx_sensor_enable(dx_batch* b, int enable);
 
 /* Debug / parity -------------------------------------------------------- */
 /* When enabled, dx_forward/dx_step record per-env intermediates of the LAST

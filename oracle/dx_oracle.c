@@ -180,6 +180,7 @@ struct dxo_data {
   double *xpos, *xquat, *xmat, *xipos, *ximat, *xanchor, *xaxis;
   double *geom_xpos, *geom_xmat, *site_xpos, *site_xmat;
   double *subtree_com, *cinert, *cdof, *cvel, *cdof_dot, *crb, *cacc, *cfrc;
+  double *cfrc_ext, *cfrc_int, *cacc_post, *sensor_torque;
   double *ten_length, *ten_J, *actuator_length, *actuator_moment, *actuator_force;
   double *M, *L, *H;
   double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_applied, *qfrc_smooth, *qfrc_constraint;
@@ -210,6 +211,8 @@ dxo_data* dxo_data_create(const dxo_model* m) {
   d->subtree_com = calloc(3 * nb, 8); d->cinert = calloc(10 * nb, 8); d->cdof = calloc(6 * nv, 8);
   d->cvel = calloc(6 * nb, 8); d->cdof_dot = calloc(6 * nv, 8); d->crb = calloc(10 * nb, 8);
   d->cacc = calloc(6 * nb, 8); d->cfrc = calloc(6 * nb, 8);
+  d->cfrc_ext = calloc(6 * nb, 8); d->cfrc_int = calloc(6 * nb, 8); d->cacc_post = calloc(6 * nb, 8);
+  d->sensor_torque = calloc(3 * nb, 8);
   d->ten_length = calloc(m->ntendon + 1, 8); d->ten_J = calloc((m->ntendon + 1) * nv, 8);
   d->actuator_length = calloc(m->nu + 1, 8); d->actuator_moment = calloc((m->nu + 1) * nv, 8);
   d->actuator_force = calloc(m->nu + 1, 8);
@@ -1523,6 +1526,107 @@ static void finish_constraint(const dxo_model* m, dxo_data* d) {
 }
 
 /* ------------------------------------------------------------------------ */
+/* mj_rnePostConstraint + torque sensors (mj_sensorAcc) [3P]                 */
+/* ------------------------------------------------------------------------ */
+/* The reference puts a 3-axis `torque` sensor on a site at the origin of every
+ * joint's body (shadow_hand_e.py:176-196, adroit_hand.py:153-172); the sensor reads
+ * the internal force of the body on its parent, cfrc_int, at the site, in the site
+ * frame.  cfrc_int needs the full acceleration (qacc after the constraint solve) and
+ * the external forces: xfrc_applied and the contact forces decoded from the pyramid
+ * rows (mju_decodePyramid).  Computed after the solve of every forward pass, before
+ * integration (mj_step2 -> mj_sensorAcc); not part of the FLOP counters (the GPU
+ * computes it only when the sensor field is enabled). */
+static void shift_force(double* res, const double* f, const double* newpos, const double* oldpos) {
+  /* mju_transformSpatial, force: torque_new = torque - (newpos - oldpos) x force */
+  double dif[3], cr[3];
+  sub3(dif, newpos, oldpos);
+  cross3(cr, dif, f + 3);
+  res[0] = f[0] - cr[0]; res[1] = f[1] - cr[1]; res[2] = f[2] - cr[2];
+  res[3] = f[3]; res[4] = f[4]; res[5] = f[5];
+}
+
+static void rne_post_constraint(const dxo_model* m, dxo_data* d) {
+  int nb = m->nbody;
+  memset(d->cfrc_ext, 0, 48 * nb);
+  for (int b = 1; b < nb; b++) {
+    const double* x = d->xfrc_applied + 6 * b;
+    if (x[0] == 0 && x[1] == 0 && x[2] == 0 && x[3] == 0 && x[4] == 0 && x[5] == 0) continue;
+    double f[6] = {x[3], x[4], x[5], x[0], x[1], x[2]}, fc[6];
+    shift_force(fc, f, d->subtree_com + 3 * m->body_rootid[b], d->xipos + 3 * b);
+    for (int e = 0; e < 6; e++) d->cfrc_ext[6 * b + e] += fc[e];
+  }
+  for (int r = 0; r < d->nefc;) {
+    int type = d->efc_type[r];
+    if (type != EFC_CON_PYR && type != EFC_CON_FL) { r++; continue; }
+    const OContact* con = d->contact + d->efc_id[r];
+    double lf[3] = {0, 0, 0};
+    if (type == EFC_CON_FL) {
+      lf[0] = d->efc_force[r];
+      r += 1;
+    } else {
+      for (int e = 0; e < 4; e++) lf[0] += d->efc_force[r + e];
+      lf[1] = (d->efc_force[r] - d->efc_force[r + 1]) * con->friction[0];
+      lf[2] = (d->efc_force[r + 2] - d->efc_force[r + 3]) * con->friction[1];
+      r += 4;
+    }
+    /* world force = frame^T lf (frame rows: normal, tangent1, tangent2) */
+    double f[6] = {0, 0, 0, 0, 0, 0}, fc[6];
+    for (int k = 0; k < 3; k++) f[3 + k] = con->frame[k] * lf[0] + con->frame[3 + k] * lf[1] + con->frame[6 + k] * lf[2];
+    int b1 = m->geom_bodyid[con->geom1], b2 = m->geom_bodyid[con->geom2];
+    if (b1) {
+      shift_force(fc, f, d->subtree_com + 3 * m->body_rootid[b1], con->pos);
+      for (int e = 0; e < 6; e++) d->cfrc_ext[6 * b1 + e] -= fc[e];
+    }
+    if (b2) {
+      shift_force(fc, f, d->subtree_com + 3 * m->body_rootid[b2], con->pos);
+      for (int e = 0; e < 6; e++) d->cfrc_ext[6 * b2 + e] += fc[e];
+    }
+  }
+  double* ca = d->cacc_post;
+  memset(ca, 0, 48);
+  ca[3] = -m->gravity[0]; ca[4] = -m->gravity[1]; ca[5] = -m->gravity[2];
+  memset(d->cfrc_int, 0, 48);
+  for (int b = 1; b < nb; b++) {
+    double* a = ca + 6 * b;
+    memcpy(a, ca + 6 * m->body_parent[b], 48);
+    for (int j = m->body_dofadr[b]; j >= 0 && j < m->body_dofadr[b] + m->body_dofnum[b]; j++)
+      for (int e = 0; e < 6; e++) a[e] += d->cdof_dot[6 * j + e] * d->qvel[j] + d->cdof[6 * j + e] * d->qacc[j];
+    double t1[6], t2[6], t3[6];
+    mul_inert(t1, d->cinert + 10 * b, a);
+    mul_inert(t2, d->cinert + 10 * b, d->cvel + 6 * b);
+    cross_force(t3, d->cvel + 6 * b, t2);
+    for (int e = 0; e < 6; e++) d->cfrc_int[6 * b + e] = t1[e] + t3[e] - d->cfrc_ext[6 * b + e];
+  }
+  for (int b = nb - 1; b > 0; b--) {
+    int p = m->body_parent[b];
+    if (p > 0)
+      for (int e = 0; e < 6; e++) d->cfrc_int[6 * p + e] += d->cfrc_int[6 * b + e];
+  }
+  /* torque sensor on a site at body b's origin (site frame = body frame) */
+  memset(d->sensor_torque, 0, 24);
+  for (int b = 1; b < nb; b++) {
+    double t[6];
+    shift_force(t, d->cfrc_int + 6 * b, d->xpos + 3 * b, d->subtree_com + 3 * m->body_rootid[b]);
+    mattvec3(d->sensor_torque + 3 * b, d->xmat + 9 * b, t);
+  }
+}
+
+/* mj_objectVelocity (utils/mujoco_utils.py:27-34), world orientation: the com-based
+ * cvel of the object's body moved to the object position; res = [lin(3), ang(3)]
+ * (the order get_site_velocity returns).  objtype 0: body inertial frame (xipos,
+ * what frame*vel sensors of objtype "body" read), 1: site, 2: body frame (xpos). */
+void dxo_object_velocity(const dxo_model* m, const dxo_data* d, int objtype, int id, double res[6]) {
+  int b = objtype == 1 ? m->site_bodyid[id] : id;
+  const double* pos = objtype == 1 ? d->site_xpos + 3 * id : objtype == 0 ? d->xipos + 3 * b : d->xpos + 3 * b;
+  const double* cv = d->cvel + 6 * b;
+  double off[3], w[3];
+  sub3(off, pos, d->subtree_com + 3 * m->body_rootid[b]);
+  cross3(w, cv, off);
+  res[0] = cv[3] + w[0]; res[1] = cv[4] + w[1]; res[2] = cv[5] + w[2];
+  res[3] = cv[0]; res[4] = cv[1]; res[5] = cv[2];
+}
+
+/* ------------------------------------------------------------------------ */
 /* Euler with implicit joint damping                                         */
 /* ------------------------------------------------------------------------ */
 static void euler(const dxo_model* m, dxo_data* d) {
@@ -1584,6 +1688,16 @@ int dxo_forward(const dxo_model* m, dxo_data* d) {
   /* constraint velocities were computed in make_constraint with current qvel */
   solve_newton(m, d);
   finish_constraint(m, d);
+  rne_post_constraint(m, d);
+  return 0;
+}
+
+/* Observation-time pass at the current state (no forces): kinematics, com, site
+ * poses and cvel -- what the observables read after dm_control's step1. */
+int dxo_observe(const dxo_model* m, dxo_data* d) {
+  kinematics(m, d);
+  com_pos(m, d);
+  com_vel(m, d);
   return 0;
 }
 
@@ -1725,6 +1839,9 @@ double* dxo_field(dxo_data* d, const char* name, int* len) {
   F("cinert", d->cinert, 10 * nb);
   F("cdof", d->cdof, 6 * nv);
   F("cvel", d->cvel, 6 * nb);
+  F("cfrc_int", d->cfrc_int, 6 * nb);
+  F("cfrc_ext", d->cfrc_ext, 6 * nb);
+  F("sensor_torque", d->sensor_torque, 3 * nb);
   F("geom_xpos", d->geom_xpos, 3 * m->ngeom);
   F("geom_xmat", d->geom_xmat, 9 * m->ngeom);
   F("site_xpos", d->site_xpos, 3 * m->nsite);

@@ -53,6 +53,12 @@ int dxo_step(const dxo_model* m, dxo_data* d);
 /* Position-only pass (kinematics + collision), as used for observations. */
 int dxo_kinematics(const dxo_model* m, dxo_data* d);
 
+/* Observation pass: mj_kinematics + mj_comPos + mj_comVel at the current state. */
+int dxo_observe(const dxo_model* m, dxo_data* d);
+/* mj_objectVelocity, world orientation, res = [lin(3), ang(3)] at the object:
+ * objtype 0 body inertial frame (xipos), 1 site, 2 body frame (xpos). */
+void dxo_object_velocity(const dxo_model* m, const dxo_data* d, int objtype, int id, double res[6]);
+
 /* mj_kinematics + mj_comPos (no collision). */
 int dxo_fk(const dxo_model* m, dxo_data* d);
 /* mj_jacSite after dxo_fk: jacp / jacr [3][nv] (either may be NULL). */
@@ -67,7 +73,9 @@ int dxo_ik_attempt(const dxo_model* m, dxo_data* d, int nsite, const int* sites,
  * Names: qpos qvel ctrl qacc qacc_warmstart qacc_smooth qfrc_bias qfrc_passive
  * qfrc_actuator qfrc_applied qfrc_smooth qfrc_constraint xfrc_applied xpos xquat
  * xmat xipos site_xpos M actuator_force actuator_length ten_length cvel
- * efc_force efc_aref efc_R efc_pos efc_J time.  */
+ * efc_force efc_aref efc_R efc_pos efc_J time cfrc_int cfrc_ext sensor_torque
+ * (sensor_torque [nbody][3]: the `torque` sensor of a site at each body's origin,
+ * site frame, from the last forward pass: mj_rnePostConstraint + mj_sensorAcc).  */
 double* dxo_field(dxo_data* d, const char* name, int* len);
 
 int dxo_ncon(const dxo_data* d);

@@ -58,6 +58,9 @@ def lib():
         L.dxo_batch_step.restype = ip
         L.dxo_batch_step_counted.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip, dp]
         L.dxo_batch_step_counted.restype = ip
+        L.dxo_observe.argtypes = [vp, vp]
+        L.dxo_observe.restype = ip
+        L.dxo_object_velocity.argtypes = [vp, vp, ip, ip, dp]
         L.dxo_fk.argtypes = [vp, vp]
         L.dxo_fk.restype = ip
         L.dxo_jac_site.argtypes = [vp, vp, ip, dp, dp]
@@ -140,6 +143,19 @@ class OracleData:
 
     def fk(self):
         return lib().dxo_fk(self.model.ptr, self.ptr)
+
+    def observe(self):
+        """Kinematics + com + cvel at the current state (dm_control's step1 outputs)."""
+        return lib().dxo_observe(self.model.ptr, self.ptr)
+
+    def object_velocity(self, objtype: str, idx: int) -> np.ndarray:
+        """mj_objectVelocity in the world frame, [lin, ang] (mujoco_utils.py:10-35);
+        objtype "body" (inertial frame), "site" or "xbody"."""
+        res = np.zeros(6)
+        code = {"body": 0, "site": 1, "xbody": 2}[objtype]
+        lib().dxo_object_velocity(self.model.ptr, self.ptr, code, int(idx),
+                                  res.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        return res
 
     def jac_site(self, site: int):
         """mj_jacSite after fk(): (jacp [3, nv], jacr [3, nv])."""

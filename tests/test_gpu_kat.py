@@ -1,0 +1,134 @@
+"""The reference's own physics known-answer tests, run through the C ABI on the GPU
+(and, as the checker, on the fp64 oracle):
+
+  * hands_test.py:159-193  joint torque sensors at static equilibrium: Adroit hand
+    alone, contact / gravity / actuation disabled, a torque tau in {0, -6, 5} applied
+    on the body of joint {0, 2, 4} about the joint axis; step until the joint stops
+    (|qvel| <= 1e-2); the joint torque observable must read -tau within 1e-2;
+  * hands_test.py:195-228  five golden Adroit fingertip positions reached by the IK
+    solver (linear_tol 1e-3, early stop, first successful attempt) and confirmed by
+    forward kinematics within atol 1e-3.
+"""
+
+import os
+
+import numpy as np
+import pytest
+
+from dexterity_amd import _lib, blob
+from dexterity_amd.mjcf.compiler import CompiledModel
+from tests.conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+# hands_test.py:196-205
+FINGERTIP_GOLDEN = np.array([
+    [-0.003572, -0.020904, 0.371999],
+    [-0.028277, -0.036063, 0.391271],
+    [-0.052305, -0.006066, 0.393481],
+    [-0.089808, -0.042816, 0.423813],
+    [0.026246, -0.017261, 0.416314],
+])
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    from dexterity_amd import build, physics
+
+    build.build()
+    return physics
+
+
+@pytest.fixture(scope="module")
+def adroit_hand():
+    return CompiledModel.load(os.path.join(ROOT, "assets", "adroit_hand.npz"))
+
+
+def _applied_torque(cm, xmat, joint, tau):
+    """physics.bind(joint.parent).xfrc_applied[3:] = tau * physics.bind(joint).xaxis."""
+    b = int(cm.jnt_bodyid[joint])
+    xaxis = xmat.reshape(-1, 3, 3)[b] @ np.asarray(cm.jnt_axis[joint], dtype=np.float64)
+    x = np.zeros((cm.nbody, 6))
+    x[b, 3:] = tau * xaxis
+    return x
+
+
+@pytest.mark.parametrize("joint,tau", [(j, t) for j in (0, 2, 4) for t in (0.0, -6.0, 5.0)])
+def test_joint_torque_sensor_equilibrium_kat(gpu, oracle_mod, adroit_hand, joint, tau):
+    cm = adroit_hand.disabled("contact", "gravity", "actuation")
+    b = int(cm.jnt_bodyid[joint])
+    da = int(cm.jnt_dofadr[joint])
+    axis = np.asarray(cm.jnt_axis[joint], dtype=np.float64)
+    # oracle (fp64)
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    d = oracle_mod.OracleData(om)
+    d.fk()
+    xfrc = _applied_torque(cm, d.xmat, joint, tau)
+    d.xfrc_applied[:] = xfrc.ravel()
+    d.step()
+    n_or = 1
+    while abs(d.qvel[da]) > 1e-2 and n_or < 5000:
+        d.step()
+        n_or += 1
+    torque_or = -(d.sensor_torque.reshape(-1, 3)[b] @ axis)
+    assert abs(torque_or - tau) <= 1e-2
+    # GPU (fp32), same procedure through the C ABI
+    model = gpu.Model(cm)
+    ph = gpu.BatchedPhysics(model, 1)
+    ph.set_xfrc(xfrc)
+    ph.enable_sensors(True)
+    ph.step(1)
+    n = 1
+    while abs(ph.qvel[0, da]) > 1e-2 and n < 5000:
+        ph.step(1)
+        n += 1
+    torque = -ph.joint_torques([b], axis[None, :])[0, 0]
+    ph.close()
+    assert abs(torque - tau) <= 1e-2, (torque, tau, n)
+    assert abs(n - n_or) <= max(2, 0.05 * n_or)
+    assert abs(torque - torque_or) <= 2e-3
+
+
+def test_torque_sensors_match_oracle_with_contacts(gpu, oracle_mod):
+    """Every body's torque sensor after a forward pass at contact-rich reorient states
+    (contact forces, gravity compensation and actuation all enter cfrc_int), GPU fp32
+    vs oracle fp64, within 2e-3 of the largest sensor reading of the state."""
+    from tests.test_gpu_parity import _load_states, _oracle_forward, _oracle_states
+
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "shadow_reorient.npz"))
+    xfrc = gpu.gravity_compensation(cm, "shadow_hand_e/")
+    om, states = _oracle_states(oracle_mod, cm, xfrc)
+    model = gpu.Model(cm)
+    ph = _load_states(gpu, model, xfrc, states)
+    ph.enable_sensors(True)
+    ph.forward()
+    s = ph.get(_lib.SENSOR_TORQUE).reshape(len(states), cm.nbody, 3)
+    with_contacts = 0
+    for e, st in enumerate(states):
+        d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        so = d.sensor_torque.reshape(cm.nbody, 3)
+        scale = max(np.abs(so).max(), 1e-3)
+        assert np.abs(s[e] - so).max() <= 2e-3 * scale, (e, np.abs(s[e] - so).max(), scale)
+        with_contacts += d.ncon > 0
+    assert with_contacts >= 6
+    ph.close()
+
+
+def test_adroit_fingertip_golden_ik(gpu, oracle_mod, adroit_hand):
+    from dexterity_amd.inverse_kinematics import IKSolver
+
+    model = gpu.Model(adroit_hand)
+    solver = IKSolver(model, hand="adroit")
+    qpos = solver.solve(target_positions=FINGERTIP_GOLDEN, linear_tol=1e-3, early_stop=True,
+                        stop_on_first_successful_attempt=True)
+    assert qpos is not None
+    lo, hi = adroit_hand.jnt_range[solver.joints].T
+    assert np.all(qpos >= lo - 1e-6) and np.all(qpos <= hi + 1e-6)
+    # hand.set_joint_angles + fingertip_positions observable, in fp64
+    om = oracle_mod.OracleModel(blob.pack(adroit_hand.arrays))
+    d = oracle_mod.OracleData(om)
+    d.qpos[adroit_hand.jnt_qposadr[solver.joints]] = qpos
+    d.fk()
+    tips = d.site_xpos.reshape(-1, 3)[solver.sites]
+    np.testing.assert_allclose(tips, FINGERTIP_GOLDEN, atol=1e-3)
+    solver.close()

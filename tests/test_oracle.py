@@ -12,13 +12,15 @@ The oracle's dynamics cannot be compared with real MuJoCo here (absent, SURVEY.m
     (hands_test.py:52-57).
 """
 
+import os
+
 import numpy as np
 import pytest
 
 from dexterity_amd import blob
 from dexterity_amd.mjcf import setconst
 from dexterity_amd.physics import gravity_compensation
-from tests.conftest import random_hand_state
+from tests.conftest import ROOT, random_hand_state
 
 
 def _data(oracle_mod, compiled):
@@ -178,3 +180,58 @@ def test_flop_counters_populated(oracle_mod, reorient_compiled):
     d.step()
     fl = d.flops()
     assert fl.shape == (7,) and np.all(fl[[0, 1, 4, 6]] > 0)
+
+
+# --------------------------------------------------------------------------- #
+# the reference's physics known-answer tests, on the fp64 oracle (CPU)
+# --------------------------------------------------------------------------- #
+@pytest.mark.parametrize("joint,tau", [(j, t) for j in (0, 2, 4) for t in (0.0, -6.0, 5.0)])
+def test_oracle_joint_torque_sensor_kat(oracle_mod, joint, tau):
+    """hands_test.py:159-193 on the standalone Adroit hand: contact, gravity and
+    actuation disabled, tau about joint `joint`'s axis on its body, step until the
+    joint stops; the torque sensor projected on the axis reads -tau within 1e-2."""
+    from dexterity_amd import blob
+    from dexterity_amd.mjcf.compiler import CompiledModel
+
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "adroit_hand.npz")).disabled("contact", "gravity", "actuation")
+    d = oracle_mod.OracleData(oracle_mod.OracleModel(blob.pack(cm.arrays)))
+    d.fk()
+    b, da = int(cm.jnt_bodyid[joint]), int(cm.jnt_dofadr[joint])
+    axis = np.asarray(cm.jnt_axis[joint], dtype=np.float64)
+    x = np.zeros((cm.nbody, 6))
+    x[b, 3:] = tau * (d.xmat.reshape(-1, 3, 3)[b] @ axis)
+    d.xfrc_applied[:] = x.ravel()
+    d.step()
+    n = 1
+    while abs(d.qvel[da]) > 1e-2 and n < 5000:
+        d.step()
+        n += 1
+    assert n < 5000
+    assert abs(-(d.sensor_torque.reshape(-1, 3)[b] @ axis) - tau) <= 1e-2
+
+
+def test_oracle_adroit_fingertip_golden_ik(oracle_mod):
+    """hands_test.py:195-228: the five golden fingertip positions are reachable by the
+    IK attempt loop (ik_solver.py:155-228) within 1e-3; starts at the joint midrange,
+    then uniform random starts (the reference's attempts) until one succeeds."""
+    from dexterity_amd import blob, hands
+    from dexterity_amd.mjcf.compiler import CompiledModel
+
+    golden = np.array([[-0.003572, -0.020904, 0.371999], [-0.028277, -0.036063, 0.391271],
+                       [-0.052305, -0.006066, 0.393481], [-0.089808, -0.042816, 0.423813],
+                       [0.026246, -0.017261, 0.416314]])
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "adroit_hand.npz"))
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    sites = [cm.names["site"].index("adroit_hand/" + s) for s in hands.ADROIT_FINGERTIP_SITES]
+    joints = [cm.names["joint"].index("adroit_hand/" + j) for j in hands.SHADOW_JOINTS]
+    lo, hi = np.asarray(cm.jnt_range)[joints].T
+    rng = np.random.RandomState(0)
+    for attempt in range(30):
+        d = oracle_mod.OracleData(om)
+        d.qpos[cm.jnt_qposadr[joints]] = (lo + hi) / 2 if attempt == 0 else rng.uniform(lo, hi)
+        steps, err = d.ik_attempt(sites, joints, golden, early_stop=True)
+        if np.all(err <= 1e-3):
+            break
+    assert np.all(err <= 1e-3)
+    d.fk()
+    np.testing.assert_allclose(d.site_xpos.reshape(-1, 3)[sites], golden, atol=1e-3)
