@@ -32,6 +32,7 @@ EXPORTS = (
     "dx_jac_site", "dx_ik_solve",
     "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
+    "dx_env_set_time_limit",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -41,7 +42,7 @@ COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "
             26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc",
             31: "np_trips", 32: "broad_keep", 33: "mid_pairs", 34: "mid_keep"}
 NSTAGE = 40
-OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES = range(7)
+OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES, OUT_GOAL_QPOS = range(8)
 TASK_REORIENT, TASK_REACH = 0, 1
 REACH_NPARAMS_HEAD = 26
 
@@ -116,6 +117,7 @@ def load(path: str = LIB_PATH):
     L.dx_env_goal_dim.argtypes = [vp]
     L.dx_env_reset.argtypes = [vp]
     L.dx_env_step.argtypes = [vp, vp]
+    L.dx_env_set_time_limit.argtypes = [vp, ctypes.c_float]
     L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
     L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]

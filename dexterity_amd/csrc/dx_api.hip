@@ -1390,6 +1390,8 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   rc |= al((void**)&S.step_type, E * 4); rc |= al((void**)&S.episode, E * 4);
   rc |= al((void**)&S.skip, E * 4); rc |= al((void**)&S.failure, E * 4);
   rc |= al((void**)&S.need, E * 4); rc |= al((void**)&S.goalnum, E * 4); rc |= al((void**)&S.goalfail, E * 4);
+  if (task == DX_TASK_REACH) rc |= al((void**)&S.goal_qpos, E * nq * 4);
+  P.time_limit = INFINITY;
   float* tdata = nullptr;
   TaskParams* dP = nullptr;
   TaskState* dS = nullptr;
@@ -1451,6 +1453,15 @@ extern "C" int dx_env_reset(dx_env* e) {
   return env_run(e, nullptr);
 }
 
+extern "C" int dx_env_set_time_limit(dx_env* e, float seconds) {
+  if (!e || !(seconds > 0)) return fail(DX_EINVAL, "null env or non-positive time limit");
+  e->P.time_limit = seconds;
+  HIPCHK(hipSetDevice(e->batch->device));
+  HIPCHK(hipStreamSynchronize(e->batch->stream));  // the device copy is read by the sampling pass
+  HIPCHK(hipMemcpy((void*)e->batch->db.tp, &e->P, sizeof(TaskParams), hipMemcpyHostToDevice));
+  return 0;
+}
+
 extern "C" int dx_env_step(dx_env* e, const float* action) {
   if (!e || !action) return fail(DX_EINVAL, "null env or action");
   return env_run(e, action);
@@ -1466,6 +1477,10 @@ extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
     case DX_OUT_GOAL: *devptr = e->S.goal; return 0;
     case DX_OUT_SUCCESSES: *devptr = e->S.successes; return 0;
     case DX_OUT_GOAL_FAILURES: *devptr = e->S.goalfail; return 0;
+    case DX_OUT_GOAL_QPOS:
+      if (!e->S.goal_qpos) return fail(DX_EINVAL, "goal joints exist for the reach task only");
+      *devptr = e->S.goal_qpos;
+      return 0;
   }
   return fail(DX_EINVAL, "unknown output");
 }

@@ -147,6 +147,7 @@ struct TaskParams {
   int obs_dim, goal_dim;
   int successes_needed, steps_before_change, fall_termination;
   float threshold, eps, w_orient, w_success, w_action, max_time, timestep_ctrl;
+  float time_limit;         // composer Environment time_limit (s); +inf: none
   float bbox_lo[3], bbox_hi[3];
   // reach (fingertip_position.py / dexterous_hand.py samplers)
   int dense, max_reject, ncoupled;
@@ -160,6 +161,7 @@ struct TaskState {
   float *goal, *solve_start, *reward, *discount, *obs;
   int *successes, *counter, *registered, *exceeded, *step_type, *episode, *skip, *failure;
   int *need, *goalnum, *goalfail;  // reach: bit0 next_goal, bit1 joint init; goals drawn; rejected-out goals
+  float* goal_qpos;                // reach: [nenv][nq] joints that placed the goal (FingertipCartesianPosition.qpos)
 };
 
 // Counter-based RNG: splitmix64 over (seed, env, episode, draw).

@@ -2233,6 +2233,9 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       }
       kinematics(c);
       gc = tip_coord(c, P);
+      // fingertip_position.py:99-103: the accepted goal's joints are the state after
+      // the two steps (kept as FingertipCartesianPosition.qpos; the last draw if none)
+      if (T.goal_qpos && LANE < nq) T.goal_qpos[(size_t)env * nq + LANE] = qpos[LANE];
       if (!contact_now(c)) { ok = true; break; }
       time = t0;
     }

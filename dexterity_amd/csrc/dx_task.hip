@@ -166,7 +166,9 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
       int failure = !reach && P.fall_termination && B.watch && B.watch[env];
       S.failure[env] = failure;
       bool success_done = S.successes[env] >= P.successes_needed;
-      bool terminate = success_done || S.exceeded[env] || failure;
+      // composer.Environment.step: should_terminate_episode or time >= time_limit
+      // (a time-limit truncation keeps the task's discount)
+      bool terminate = success_done || S.exceeded[env] || failure || time >= P.time_limit;
       float r;
       if (reach) {
         r = rsum / (float)P.ntips;

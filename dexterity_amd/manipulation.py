@@ -235,9 +235,14 @@ class GoalEnvironment:
     through `timestep()` / `observation()`.
     """
 
-    def __init__(self, task: ReOrient, num_envs: int, seed: Optional[int] = None, device: int = 0):
+    def __init__(self, task: ReOrient, num_envs: int, seed: Optional[int] = None, device: int = 0,
+                 time_limit: Optional[float] = None, strip_singleton_obs_buffer_dim: bool = True):
         self.task = task
         self.num_envs = int(num_envs)
+        # composer.Environment(time_limit=..., strip_singleton_obs_buffer_dim=...)
+        # (manipulation/__init__.py:81-86); the tasks' own time_limit is inf
+        self.time_limit = float("inf") if time_limit is None else float(time_limit)
+        self.strip_singleton_obs_buffer_dim = bool(strip_singleton_obs_buffer_dim)
         self.model = physics_lib.Model(task.compiled)
         L = _lib.load()
         p = task.params()
@@ -256,6 +261,8 @@ class GoalEnvironment:
         self._action_spec = task.hand_effector.action_spec(self.physics)
         self._host_action = np.zeros((self.num_envs, self.model.nu), dtype=np.float32)
         self._dev_action = self._out(-1)
+        if np.isfinite(self.time_limit):
+            _lib.check(L.dx_env_set_time_limit(self.ptr, self.time_limit))
 
     def close(self):
         if getattr(self, "physics", None) is not None:
@@ -281,8 +288,9 @@ class GoalEnvironment:
         return self._action_spec
 
     def observation_spec(self) -> "collections.OrderedDict[str, Array]":
+        lead = () if self.strip_singleton_obs_buffer_dim else (1,)
         return collections.OrderedDict(
-            (k, Array((s.stop - s.start,), np.float64, name=k)) for k, s in self._layout.items()
+            (k, Array(lead + (s.stop - s.start,), np.float64, name=k)) for k, s in self._layout.items()
         )
 
     # ---------------------------------------------------------------- stepping
@@ -325,13 +333,21 @@ class GoalEnvironment:
         st = self._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0]
         rew = self._read(_lib.OUT_REWARD, np.float32, 1)[:, 0].astype(np.float64)
         disc = self._read(_lib.OUT_DISCOUNT, np.float32, 1)[:, 0].astype(np.float64)
+        # an observation buffer of size 1 per observable (dm_control observation
+        # updater); kept as [B, 1, n] unless strip_singleton_obs_buffer_dim
         observation = collections.OrderedDict(
-            (k, obs[:, s].astype(np.float64)) for k, s in self._layout.items()
+            (k, obs[:, s].astype(np.float64) if self.strip_singleton_obs_buffer_dim
+             else obs[:, None, s].astype(np.float64)) for k, s in self._layout.items()
         )
         return TimeStep(st.astype(np.int32), rew, disc, observation)
 
     def goals(self) -> np.ndarray:
         return self._read(_lib.OUT_GOAL, np.float32, self.goal_dim)
+
+    def goal_qpos(self) -> np.ndarray:
+        """Reach: the joints that placed each env's goal (FingertipCartesianPosition.qpos,
+        fingertip_position.py:136-139)."""
+        return self._read(_lib.OUT_GOAL_QPOS, np.float32, self.model.nq)
 
     def goal_failures(self) -> np.ndarray:
         return self._read(_lib.OUT_GOAL_FAILURES, np.int32, 1)[:, 0]
@@ -378,15 +394,19 @@ ALL_TASKS = tuple(sorted(SUITE))
 ALL_NAMES = [".".join(t) for t in ALL_TASKS]
 
 
-def load(domain_name: str, task_name: str, seed: Optional[int] = None, num_envs: int = 1,
-         device: int = 0) -> GoalEnvironment:
-    """manipulation/__init__.py:56-86 (batched)."""
+def load(domain_name: str, task_name: str, seed: Optional[int] = None,
+         strip_singleton_obs_buffer_dim: bool = True, time_limit: Optional[float] = None,
+         num_envs: int = 1, device: int = 0) -> GoalEnvironment:
+    """manipulation/__init__.py:56-86, batched: the reference's arguments in its order,
+    then the batch size and the GPU.  `time_limit=None` keeps the task's own limit
+    (inf for every suite task)."""
     key = (domain_name, task_name)
     if domain_name not in {d for d, _ in SUITE}:
         raise ValueError(f"Unknown domain: {domain_name}")
     if key not in SUITE:
         raise ValueError(f"Unknown task: {task_name}")
-    return GoalEnvironment(SUITE[key](), num_envs=num_envs, seed=seed, device=device)
+    return GoalEnvironment(SUITE[key](), num_envs=num_envs, seed=seed, device=device, time_limit=time_limit,
+                           strip_singleton_obs_buffer_dim=strip_singleton_obs_buffer_dim)
 
 
 __all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "Reach", "ReachConfig", "ALL_TASKS",

@@ -172,7 +172,9 @@ enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
  *  26..  joint midrange [nq], lower [nq], upper [nq], position->control [nu][nq] */
 #define DX_REACH_NPARAMS_HEAD 26
 enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT_STEP_TYPE = 3,
-                  DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5, DX_OUT_GOAL_FAILURES = 6 };
+                  DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5, DX_OUT_GOAL_FAILURES = 6,
+                  DX_OUT_GOAL_QPOS = 7 /* reach: [nenv][nq] f32, FingertipCartesianPosition.qpos
+                                          (fingertip_position.py:136-139) */ };
 dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task, uint64_t seed,
                       const float* params, int32_t nparams);
 void dx_env_destroy(dx_env* e);
@@ -184,6 +186,10 @@ int dx_env_goal_dim(const dx_env* e);
 int dx_env_reset(dx_env* e);
 /* One control step for every env; action is [nenv][nu] float32, device memory. */
 int dx_env_step(dx_env* e, const float* action);
+/* composer.Environment's time_limit (manipulation/__init__.py:61,83): an episode also
+ * ends (LAST, with the task's discount) once its physics time reaches `seconds`.
+ * Default: none (task.time_limit = inf). */
+int dx_env_set_time_limit(dx_env* e, float seconds);
 /* Device pointers of the outputs: obs [nenv][obs_dim] f32, reward/discount [nenv] f32,
  * step_type [nenv] i32 (0 FIRST, 1 MID, 2 LAST), goal [nenv][goal_dim] f32, successes i32,
  * goal failures i32 (reach goals that exhausted the rejection samples: the reference

@@ -99,3 +99,51 @@ def reach_reward(goal, tips, dense: bool = True, threshold: float = 0.01) -> flo
     if dense:
         return float(np.mean(np.where(d <= threshold, 0.0, [-tanh_squared(x, margin=0.1) for x in d])))
     return float(np.mean(np.where(d <= threshold, 0.0, -1.0)))
+
+
+# --------------------------------------------------------------------------- #
+# STATE_ONLY observations (fp64), from the oracle's state after `observe()`
+# --------------------------------------------------------------------------- #
+def _hand_observation(d, hand_nq: int, hand_nv: int, tip_sites) -> dict:
+    """DexterousHandObservables (dexterous_hand.py:250-310) enabled by
+    observations.HAND_OBSERVABLES for STATE_ONLY (observations.py:77-103)."""
+    q = np.asarray(d.qpos[:hand_nq], dtype=np.float64)
+    site_xpos = d.site_xpos.reshape(-1, 3)
+    return {
+        # np.vstack([sin, cos]).T.ravel(): sin/cos interleaved per joint (:256-260)
+        "joint_positions_sin_cos": np.vstack([np.sin(q), np.cos(q)]).T.ravel(),
+        "joint_velocities": np.asarray(d.qvel[:hand_nv], dtype=np.float64),
+        "fingertip_positions": site_xpos[list(tip_sites)].ravel(),
+        # get_site_velocity(world_frame=True)[:3] = mj_objectVelocity lin part (:297-310,
+        # utils/mujoco_utils.py:10-35)
+        "fingertip_linear_velocities": np.concatenate([d.object_velocity("site", s)[:3] for s in tip_sites]),
+    }
+
+
+def reorient_observation(d, compiled, hand: str, hand_nq: int, hand_nv: int, tip_sites, prop_body: int,
+                         goal) -> "dict[str, np.ndarray]":
+    """ReOrient's observation (reorient.py:81-86 + the hand's, the prop's framepos /
+    framequat / framelinvel / frameangvel sensors of objtype body -- the inertial frame
+    -- [3P] dm_control Primitive, the hint prop's orientation = the goal, and goal_state,
+    task.py:207-216), keyed as the batched env's layout."""
+    out = {f"{hand}/{k}": v for k, v in _hand_observation(d, hand_nq, hand_nv, tip_sites).items()}
+    xq = d.xquat.reshape(-1, 4)[prop_body]
+    iq = np.asarray(compiled.body_iquat, dtype=np.float64).reshape(-1, 4)[prop_body]
+    quat = quat_mul(xq, iq)
+    vel = d.object_velocity("body", prop_body)
+    g = np.asarray(goal, dtype=np.float64)
+    out["prop/position"] = d.xipos.reshape(-1, 3)[prop_body].copy()
+    out["prop/orientation"] = quat / np.linalg.norm(quat)
+    out["prop/linear_velocity"] = vel[:3]
+    out["prop/angular_velocity"] = vel[3:]
+    out["target_prop/orientation"] = g / np.linalg.norm(g)
+    out["goal_state"] = g
+    return out
+
+
+def reach_observation(d, hand: str, hand_nq: int, hand_nv: int, tip_sites, goal) -> "dict[str, np.ndarray]":
+    """Reach's observation: the hand's STATE_ONLY observables and the 15-float
+    fingertip goal (reach.py:119-139, fingertip_position.py:39-44, task.py:207-216)."""
+    out = {f"{hand}/{k}": v for k, v in _hand_observation(d, hand_nq, hand_nv, tip_sites).items()}
+    out["goal_state"] = np.asarray(goal, dtype=np.float64)
+    return out

@@ -45,3 +45,235 @@ def test_allgather_world1(built):
     col.close()
     comm.close()
     env.close()
+
+
+def _oracle_for(env, oracle_mod):
+    return oracle_mod.OracleModel(env.model.blob)
+
+
+def _check_observation(env, oracle_mod, builder):
+    """Every float of the env's observation vs the fp64 restatement on the env's own
+    post-step state (qpos / qvel / goal read back from the device)."""
+    from dexterity_amd import _lib
+
+    ts = env.timestep()
+    ph = env.physics
+    qpos, qvel = ph.get(_lib.QPOS), ph.get(_lib.QVEL)
+    goals = env.goals()
+    om = _oracle_for(env, oracle_mod)
+    worst = {}
+    for e in range(env.num_envs):
+        d = oracle_mod.OracleData(om)
+        d.qpos[:], d.qvel[:] = qpos[e], qvel[e]
+        d.observe()
+        ref = builder(d, goals[e])
+        assert list(ref) == list(ts.observation), (list(ref), list(ts.observation))
+        for k, r in ref.items():
+            g = ts.observation[k][e]
+            assert g.shape == r.shape, k
+            err = np.abs(g - r).max() / max(1.0, np.abs(r).max())
+            worst[k] = max(worst.get(k, 0.0), err)
+    for k, err in worst.items():
+        assert err <= 1e-5, (k, err, worst)
+    return worst
+
+
+def test_observation_matches_oracle_reorient(built, oracle_mod):
+    """All 123 floats of reorient.state_dense (dexterous_hand.py:250-310, reorient.py:
+    81-86, task.py:207-216) within 1e-5 of each field's scale, over 256 envs after 12
+    random-action control steps (episodes in every phase, freshly reset ones included)."""
+    from dexterity_amd import manipulation
+    from oracle import task_ref
+
+    env = manipulation.load("reorient", "state_dense", seed=21, num_envs=256)
+    t = env.task
+    env.reset()
+    for i in range(12):
+        env.step(env.sample_actions(i), device_action=True)
+    assert env.obs_dim == 123
+    sites = list(range(t.tip_site0, t.tip_site0 + t.ntips))
+    worst = _check_observation(
+        env, oracle_mod,
+        lambda d, g: task_ref.reorient_observation(d, t.compiled, t.hand_name, t.hand_nq, t.hand_nv, sites,
+                                                   t.prop_body, g))
+    assert set(worst) >= {"prop/angular_velocity", "shadow_hand_e/fingertip_linear_velocities"}
+    env.close()
+
+
+@pytest.mark.parametrize("domain", ["reach", "reach_shadow"])
+def test_observation_matches_oracle_reach(built, oracle_mod, domain):
+    """All 117 floats of reach.state_dense (Adroit) and of the Shadow variant."""
+    from dexterity_amd import manipulation
+    from oracle import task_ref
+
+    env = manipulation.load(domain, "state_dense", seed=5, num_envs=128)
+    t = env.task
+    env.reset()
+    for i in range(6):
+        env.step(env.sample_actions(i), device_action=True)
+    assert env.obs_dim == 117
+    _check_observation(env, oracle_mod,
+                       lambda d, g: task_ref.reach_observation(d, t.hand_name, t.hand_nq, t.hand_nv, t.tip_sites, g))
+    env.close()
+
+
+def _run(env, steps, actions=None):
+    from dexterity_amd import _lib
+
+    out = []
+    for i in range(steps):
+        if actions is None:
+            env.step(env.sample_actions(i), device_action=True)
+        else:
+            env.step(actions)
+        ts = env.timestep()
+        out.append(dict(st=ts.step_type.copy(), disc=ts.discount.copy(), rew=ts.reward.copy(),
+                        succ=env.successes().copy(), goal=env.goals().copy(),
+                        watch=env.physics.get(_lib.GROUND_CONTACT)[:, 0].copy(),
+                        time=env.physics.get(_lib.TIME)[:, 0].copy()))
+    return out
+
+
+def test_fall_terminates_with_discount_one(built):
+    """ReOrient.after_step / get_discount (reorient.py:201-213, 222-225): a prop-ground
+    contact ends the episode (LAST) with discount 1.0; the next step returns FIRST."""
+    from dexterity_amd import manipulation
+
+    env = manipulation.load("reorient", "state_dense", seed=9, num_envs=512)
+    env.reset()
+    rec = _run(env, 60)
+    falls = 0
+    for k in range(1, len(rec)):
+        r, prev = rec[k], rec[k - 1]
+        mid = prev["st"] != 2  # this step was not an auto-reset
+        fell = mid & (r["watch"] == 1)
+        assert np.all(r["st"][fell] == 2)
+        assert np.all(r["disc"][fell & (r["succ"] == 0)] == 1.0)
+        last = mid & (r["st"] == 2)
+        # every LAST is a fall, a success or a per-goal timeout (300 steps: not reached here)
+        assert np.all(fell[last] | (r["succ"][last] >= 1))
+        assert np.all(r["disc"][last & (r["succ"] == 0)] == 1.0)
+        assert np.all(r["disc"][last & (r["succ"] >= 1)] == 0.0)
+        assert np.all(r["st"][prev["st"] == 2] == 0)  # auto-reset returns FIRST
+        falls += int(fell.sum())
+    assert falls >= 50
+    env.close()
+
+
+def test_per_goal_timeout(built):
+    """GoalTask.after_step / should_terminate_episode (task.py:180-193): time since the
+    goal was set > max_time_per_goal without success ends the episode, discount 1.0."""
+    from dexterity_amd import manipulation
+
+    cfg = manipulation.ReOrientConfig(max_steps_single_solve=4.5, fall_termination=False,
+                                      orientation_threshold=0.0)  # 0.1125 s, never a success
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(cfg), num_envs=64, seed=2)
+    env.reset()
+    rec = _run(env, 7)
+    st = np.stack([r["st"] for r in rec])
+    for k in range(4):
+        assert np.all(st[k] == 1), k
+    assert np.all(st[4] == 2)  # t = 0.125 > 0.1125
+    assert np.all(rec[4]["disc"] == 1.0)
+    assert np.all(st[5] == 0)  # auto-reset
+    env.close()
+
+
+def test_time_limit(built):
+    """composer.Environment(time_limit=...) (manipulation/__init__.py:61,83): LAST once
+    the physics time reaches the limit, with the task's discount (1.0 here)."""
+    from dexterity_amd import manipulation
+
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(manipulation.ReOrientConfig(fall_termination=False)),
+                                       num_envs=64, seed=4, time_limit=0.11)
+    env.reset()
+    rec = _run(env, 6)
+    assert all(np.all(rec[k]["st"] == 1) for k in range(4))
+    assert np.all(rec[4]["st"] == 2) and np.all(rec[4]["disc"] == 1.0)
+    assert np.all(rec[5]["st"] == 0)
+    env.close()
+
+
+def test_goal_change_after_successes(built):
+    """GoalTask.before_step / after_step (task.py:154-185): with every step a success
+    (threshold above any orientation distance), the success counter passes
+    steps_before_changing_goal = 5, the next before_step draws a new goal, and the
+    success is registered again once per goal -- compared step by step with a host
+    restatement of the bookkeeping."""
+    from dexterity_amd import manipulation
+
+    cfg = manipulation.ReOrientConfig(orientation_threshold=4.0, successes_needed=1000, fall_termination=False)
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(cfg), num_envs=32, seed=8)
+    env.reset()
+    g0 = env.goals().copy()
+    rec = _run(env, 20)
+    counter, successes, registered = 0, 0, False
+    prev_goal = g0
+    for k, r in enumerate(rec):
+        changed = counter > cfg.steps_before_moving_target
+        if changed:
+            counter, registered = 0, False
+        counter += 1
+        if not registered:
+            successes += 1
+            registered = True
+        assert np.all(r["succ"] == successes), (k, r["succ"][:4], successes)
+        moved = np.any(r["goal"] != prev_goal, axis=1)
+        assert np.all(moved == changed), k
+        np.testing.assert_allclose(np.linalg.norm(r["goal"], axis=1), 1.0, atol=1e-6)
+        assert np.all(r["st"] == 1)
+        prev_goal = r["goal"]
+    env.close()
+
+
+def test_reach_sparse_closed_loop_kat(built):
+    """reach_test.py:12-35: sparse reward -1 after a zero action; then the control that
+    holds the goal's joint configuration (hand.joint_positions_to_control(goal qpos))
+    drives every fingertip within the threshold, and the step that registers the first
+    success has reward exactly 0."""
+    from dexterity_amd import manipulation
+
+    n = 32
+    env = manipulation.load("reach", "state_sparse", seed=12345, num_envs=n)
+    env.reset()
+    ts = env.step(np.zeros((n, env.model.nu), np.float32))
+    assert np.all(ts.reward == -1.0)
+    qsol = env.goal_qpos().astype(np.float64)
+    ctrl = (qsol @ np.asarray(env.task.position_to_control, dtype=np.float64).T).astype(np.float32)
+    first = np.full(n, -1)
+    reward_at = np.zeros(n)
+    for k in range(150):
+        ts = env.step(ctrl)
+        succ = env.successes()
+        new = (first < 0) & (succ > 0)
+        first[new] = k
+        reward_at[new] = ts.reward[new]
+        assert np.all(ts.step_type[first < 0] == 1)  # no episode ends before its first success
+        if np.all(first >= 0):
+            break
+    assert np.all(first >= 0), first
+    np.testing.assert_array_equal(reward_at, 0.0)
+    env.close()
+
+
+def test_reset_zeroes_ctrl(built):
+    """dx_env_reset = mj_resetData + initialize_episode: ctrl is zero afterwards."""
+    from dexterity_amd import _lib, manipulation
+
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=16)
+    env.reset()
+    env.step(env.sample_actions(0), device_action=True)
+    assert np.abs(env.physics.get(_lib.CTRL)).max() > 0
+    env.reset()
+    np.testing.assert_array_equal(env.physics.get(_lib.CTRL), 0.0)
+    env.close()
+
+
+def test_unstripped_observation_buffer_dim(built):
+    from dexterity_amd import manipulation
+
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=4, strip_singleton_obs_buffer_dim=False)
+    ts = env.reset()
+    for k, spec in env.observation_spec().items():
+        assert ts.observation[k].shape == (4,) + spec.shape and spec.shape[0] == 1
+    env.close()
