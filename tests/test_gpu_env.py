@@ -237,7 +237,13 @@ def test_reach_sparse_closed_loop_kat(built):
     env = manipulation.load("reach", "state_sparse", seed=12345, num_envs=n)
     env.reset()
     ts = env.step(np.zeros((n, env.model.nu), np.float32))
-    assert np.all(ts.reward == -1.0)
+    # -1 per fingertip farther than 1 cm from its goal, averaged (reach.py:196-210); the
+    # reference's single seed starts with every fingertip far (reward -1); here each
+    # env has its own draw, so a fingertip may start within reach
+    tips = ts.observation["adroit_hand/fingertip_positions"].reshape(n, 5, 3)
+    far = np.linalg.norm(tips - env.goals().reshape(n, 5, 3), axis=2) > 0.01
+    np.testing.assert_allclose(ts.reward, -far.mean(axis=1), atol=1e-6)  # fp32 mean
+    assert np.mean(ts.reward == -1.0) >= 0.75
     qsol = env.goal_qpos().astype(np.float64)
     ctrl = (qsol @ np.asarray(env.task.position_to_control, dtype=np.float64).T).astype(np.float32)
     first = np.full(n, -1)
