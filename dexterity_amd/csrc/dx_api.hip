@@ -1306,6 +1306,7 @@ extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nf
 extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatch B, const float* qpos0,
                                               const float* action);
 extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B);
+extern "C" __global__ void dx_mt_seed_kernel(int nenv, uint64_t seed, uint32_t* mt_env, uint32_t* mt_goal);
 
 struct dx_env {
   dx_batch* batch;
@@ -1348,7 +1349,16 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
     P.fall_termination = (int)params[9];
     P.threshold = params[10]; P.eps = params[11]; P.w_orient = params[12]; P.w_success = params[13];
     P.w_action = params[14]; P.max_time = params[15];
-    for (int k = 0; k < 3; k++) { P.bbox_lo[k] = params[16 + k]; P.bbox_hi[k] = params[19 + k]; }
+    for (int k = 0; k < 3; k++) {
+      P.bbox_lo[k] = params[16 + k]; P.bbox_hi[k] = params[19 + k];
+      // fp64 box: the raw bits of six doubles in params 26-37, when given
+      P.bbox_lo_d[k] = params[16 + k];
+      P.bbox_hi_d[k] = params[19 + k];
+      if (nparams >= 38) {
+        memcpy(&P.bbox_lo_d[k], params + 26 + 2 * k, 8);
+        memcpy(&P.bbox_hi_d[k], params + 32 + 2 * k, 8);
+      }
+    }
     watch_geom = (int)params[22]; watch_body = (int)params[23];
     P.goal_dim = 4;
     P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + (P.prop_qadr >= 0 ? 17 : 0) + 4;
@@ -1391,6 +1401,15 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   rc |= al((void**)&S.skip, E * 4); rc |= al((void**)&S.failure, E * 4);
   rc |= al((void**)&S.need, E * 4); rc |= al((void**)&S.goalnum, E * 4); rc |= al((void**)&S.goalfail, E * 4);
   if (task == DX_TASK_REACH) rc |= al((void**)&S.goal_qpos, E * nq * 4);
+  if (task == DX_TASK_REORIENT) {
+    rc |= al((void**)&S.mt_env, E * DX_MT_WORDS * 4);
+    rc |= al((void**)&S.mt_goal, E * DX_MT_WORDS * 4);
+    if (!rc) {
+      hipLaunchKernelGGL(dx_mt_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv, seed, S.mt_env,
+                         S.mt_goal);
+      if (hipGetLastError() != hipSuccess) rc = fail(DX_EHIP, "MT19937 seeding kernel launch failed");
+    }
+  }
   P.time_limit = INFINITY;
   float* tdata = nullptr;
   TaskParams* dP = nullptr;

@@ -149,6 +149,7 @@ struct TaskParams {
   float threshold, eps, w_orient, w_success, w_action, max_time, timestep_ctrl;
   float time_limit;         // composer Environment time_limit (s); +inf: none
   float bbox_lo[3], bbox_hi[3];
+  double bbox_lo_d[3], bbox_hi_d[3];  // the same box in fp64 (the reference's values)
   // reach (fingertip_position.py / dexterous_hand.py samplers)
   int dense, max_reject, ncoupled;
   int coupled[8][2];        // qpos[c[0]] = qpos[c[1]] after uniform joint sampling
@@ -162,7 +163,63 @@ struct TaskState {
   int *successes, *counter, *registered, *exceeded, *step_type, *episode, *skip, *failure;
   int *need, *goalnum, *goalfail;  // reach: bit0 next_goal, bit1 joint init; goals drawn; rejected-out goals
   float* goal_qpos;                // reach: [nenv][nq] joints that placed the goal (FingertipCartesianPosition.qpos)
+  // reorient: numpy-compatible MT19937 streams per env (dx_mt_*): the env's RandomState
+  // (PropPlacer draws) and numpy's global stream (the goal draws), [625][nenv] each
+  uint32_t *mt_env, *mt_goal;
 };
+
+// numpy.random.RandomState-compatible MT19937 ([3P] numpy legacy seeding and
+// random_sample: mt19937_seed, mt19937_gen, legacy_double), one stream per env kept in
+// HBM interleaved over the envs -- word k of env e at k * nenv + e (k < 624), the read
+// position at 624 * nenv + e -- so the rare twist (every 624 words) is a coalesced
+// sweep across a wave's envs.  Pinned against numpy in tests/test_host_logic.py and
+// tests/test_gpu_env.py.
+#define DX_MT_WORDS 625
+__device__ __forceinline__ void dx_mt_seed(uint32_t* s, int nenv, int env, uint32_t seed) {
+  for (int k = 0; k < 624; k++) {
+    s[(size_t)k * nenv + env] = seed;
+    seed = 1812433253u * (seed ^ (seed >> 30)) + (uint32_t)(k + 1);
+  }
+  s[(size_t)624 * nenv + env] = 624;
+}
+__device__ __forceinline__ uint32_t dx_mt_next(uint32_t* s, int nenv, int env) {
+  uint32_t pos = s[(size_t)624 * nenv + env];
+  if (pos >= 624) {
+    for (int k = 0; k < 624; k++) {
+      const uint32_t a = s[(size_t)k * nenv + env], b = s[(size_t)((k + 1) % 624) * nenv + env];
+      const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+      s[(size_t)k * nenv + env] = s[(size_t)((k + 397) % 624) * nenv + env] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    pos = 0;
+  }
+  uint32_t y = s[(size_t)pos * nenv + env];
+  s[(size_t)624 * nenv + env] = pos + 1;
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+// RandomState.random_sample: 53-bit double from two outputs
+__device__ __forceinline__ double dx_mt_double(uint32_t* s, int nenv, int env) {
+  const uint32_t a = dx_mt_next(s, nenv, env) >> 5, b = dx_mt_next(s, nenv, env) >> 6;
+  return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+}
+// [3P] dm_control composer.variation.rotations.UniformQuaternion:
+// u1, u2, u3 = random_state.uniform([0, 0, 0], [1, 2 pi, 2 pi]);
+// q = [sqrt(1-u1) sin u2, sqrt(1-u1) cos u2, sqrt(u1) sin u3, sqrt(u1) cos u3]
+// (computed in double, then rounded to the fp32 state)
+__device__ __forceinline__ void dx_mt_uniform_quat(uint32_t* s, int nenv, int env, float* q) {
+  const double twopi = 6.283185307179586;
+  const double u1 = dx_mt_double(s, nenv, env);
+  const double u2 = twopi * dx_mt_double(s, nenv, env);
+  const double u3 = twopi * dx_mt_double(s, nenv, env);
+  const double a = sqrt(1.0 - u1), b = sqrt(u1);
+  q[0] = (float)(a * sin(u2));
+  q[1] = (float)(a * cos(u2));
+  q[2] = (float)(b * sin(u3));
+  q[3] = (float)(b * cos(u3));
+}
 
 // Counter-based RNG: splitmix64 over (seed, env, episode, draw).
 __device__ __forceinline__ uint64_t dx_mix64(uint64_t z) {

@@ -28,15 +28,14 @@ enum { ST_FIRST = 0, ST_MID = 1, ST_LAST = 2 };
 __device__ __forceinline__ float urand(uint64_t seed, int env, int episode, int draw) {
   return dx_urand(seed, env, episode, draw);
 }
-// uniform unit quaternion (Shoemake), as dm_control rotations.UniformQuaternion
-__device__ void uniform_quat(uint64_t seed, int env, int episode, int draw0, float* q) {
-  float u1 = urand(seed, env, episode, draw0), u2 = urand(seed, env, episode, draw0 + 1),
-        u3 = urand(seed, env, episode, draw0 + 2);
-  float a = sqrtf(1 - u1), b = sqrtf(u1);
-  float s2, c2, s3, c3;
-  sincosf(6.283185307179586f * u2, &s2, &c2);
-  sincosf(6.283185307179586f * u3, &s3, &c3);
-  q[0] = b * c3; q[1] = a * s2; q[2] = a * c2; q[3] = b * s3;
+// Seeds every env's two MT19937 streams with seed + env (numpy RandomState(seed + env)
+// and np.random.seed(seed + env) of the env's process in the reference).
+extern "C" __global__ void dx_mt_seed_kernel(int nenv, uint64_t seed, uint32_t* mt_env, uint32_t* mt_goal) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= nenv) return;
+  const uint32_t s = (uint32_t)(seed + (uint64_t)env);
+  dx_mt_seed(mt_env, nenv, env, s);
+  dx_mt_seed(mt_goal, nenv, env, s);
 }
 
 // orientation distance || axisangle(quat_diff_active(cur, goal)) || = 2 acos(|<goal, cur>|)
@@ -68,14 +67,20 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
     for (int i = 0; i < P.nu; i++) B.ctrl[(size_t)env * P.nu + i] = 0;  // mj_resetData
     B.time[env] = 0;
     if (P.kind == DX_KIND_REORIENT) {
-      // reorient.py:182-188: goal first (GoalTask.initialize_episode), then the prop
-      // placed uniformly in the bbox with a uniform orientation
+      // reorient.py:182-188 in the reference's draw order: the goal first
+      // (GoalTask.initialize_episode, task.py:137-152 -> PropOrientation.next_goal,
+      // prop_orientation.py:34-38, whose sampler gets the RandomState positionally
+      // and so draws from numpy's global stream), then PropPlacer (reorient.py:143-151)
+      // on the env's RandomState: position uniform in the bbox (3 draws), then a
+      // uniform quaternion (3 draws).  A spawn never touches the hand (the box is above
+      // it, tests/test_host_logic.py), so PropPlacer's first attempt is always kept.
       float* g = S.goal + P.goal_dim * env;
-      uniform_quat(P.seed, env, ep, 0, g);
+      dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);
       if (P.prop_qadr >= 0) {
         for (int k = 0; k < 3; k++)
-          q[P.prop_qadr + k] = P.bbox_lo[k] + (P.bbox_hi[k] - P.bbox_lo[k]) * urand(P.seed, env, ep, 3 + k);
-        uniform_quat(P.seed, env, ep, 6, q + P.prop_qadr + 3);
+          q[P.prop_qadr + k] = (float)(P.bbox_lo_d[k] + (P.bbox_hi_d[k] - P.bbox_lo_d[k]) *
+                                                            dx_mt_double(S.mt_env, P.nenv, env));
+        dx_mt_uniform_quat(S.mt_env, P.nenv, env, q + P.prop_qadr + 3);
       }
     } else {
       // reach.py:155-168: fingertip goal (physics rollouts) and collision-free joint
@@ -96,8 +101,7 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
   // GoalTask.before_step (task.py:154-165)
   if (S.counter[env] > P.steps_before_change) {
     if (P.kind == DX_KIND_REORIENT) {
-      int draw = 16 + 3 * S.successes[env];
-      uniform_quat(P.seed, env, S.episode[env], draw, S.goal + P.goal_dim * env);
+      dx_mt_uniform_quat(S.mt_goal, P.nenv, env, S.goal + P.goal_dim * env);  // numpy's global stream
       S.counter[env] = 0;
       S.exceeded[env] = 0;
       S.solve_start[env] = B.time[env];

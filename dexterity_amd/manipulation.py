@@ -119,7 +119,7 @@ class ReOrient:
 
     def params(self) -> np.ndarray:
         c = self.config
-        p = np.zeros(26, dtype=np.float32)
+        p = np.zeros(38, dtype=np.float32)
         p[0] = c.n_sub_steps
         p[1], p[2] = self.hand_nq, self.hand_nv
         p[3], p[4] = self.prop_qadr, self.prop_dadr
@@ -131,6 +131,9 @@ class ReOrient:
         p[16:19] = c.prop_bbox_lower
         p[19:22] = c.prop_bbox_upper
         p[22], p[23] = self.ground_geom, self.prop_body
+        # the box in fp64 for the numpy-compatible spawn draws: raw bits in 26-37
+        box = np.array(c.prop_bbox_lower + c.prop_bbox_upper, dtype=np.float64)
+        p[26:38] = box.view(np.float32)
         return p
 
     def observation_layout(self):

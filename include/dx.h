@@ -154,13 +154,17 @@ int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
  * LAST is re-initialised by its next step and returns FIRST). */
 typedef struct dx_env dx_env;
 enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
-/* Reorient params (float[26]), reorient.py:40-78 / task.py:120-135:
+/* Reorient params (float[26], or float[32]), reorient.py:40-78 / task.py:120-135:
  *  0 n_sub_steps  1 hand_nq  2 hand_nv  3 prop_qposadr  4 prop_dofadr
  *  5 first fingertip site  6 n fingertips  7 successes_needed
  *  8 steps_before_changing_goal  9 fall_termination  10 success_threshold
  *  11 orientation_eps  12 w_orientation  13 w_success  14 w_action
  *  15 max_time_per_goal  16-18 prop bbox lower  19-21 prop bbox upper
- *  22 ground geom  23 prop body  24-25 reserved */
+ *  22 ground geom  23 prop body  24-25 reserved
+ *  26-37 (optional) the bbox in fp64: raw bits of lower[3], upper[3] (two words each)
+ * Randomness: env e draws from numpy-compatible MT19937 streams seeded with
+ * seed + e -- its RandomState (PropPlacer) and numpy's global stream (goals, which
+ * the reference's PropOrientation draws from np.random: prop_orientation.py:38). */
 #define DX_REORIENT_NPARAMS 26
 /* Reach params (float[26 + 3*nq + nu*nq]), reach.py:43-70, task.py:120-135,
  * fingertip_position.py:21-35, dexterous_hand.py:120-168:

@@ -283,3 +283,57 @@ def test_unstripped_observation_buffer_dim(built):
     for k, spec in env.observation_spec().items():
         assert ts.observation[k].shape == (4,) + spec.shape and spec.shape[0] == 1
     env.close()
+
+
+def _uniform_quaternion(rs):
+    """[3P] dm_control rotations.UniformQuaternion.__call__ with a RandomState."""
+    u1, u2, u3 = rs.uniform([0.0] * 3, [1.0, 2 * np.pi, 2 * np.pi])
+    return np.array([np.sqrt(1 - u1) * np.sin(u2), np.sqrt(1 - u1) * np.cos(u2), np.sqrt(u1) * np.sin(u3),
+                     np.sqrt(u1) * np.cos(u3)])
+
+
+def test_reorient_resets_replay_numpy_random_state(built):
+    """Seed-level reset parity: env e of a batch seeded s is the
+    reference env `load("reorient", "state_dense", seed=s + e)` with numpy's global
+    stream seeded s + e.  Replaying numpy in the reference's order -- the goal from the
+    global stream (task.py:137-152, prop_orientation.py:34-38), then PropPlacer's
+    position (3 uniform draws in the bbox) and quaternion from the env's RandomState
+    (reorient.py:143-151, 182-188) -- gives the device's initial goal and prop pose bit
+    for bit after the fp32 cast, for the first episode and for every auto-reset
+    episode that follows."""
+    from dexterity_amd import _lib, manipulation
+
+    seed, n = 777, 128
+    env = manipulation.load("reorient", "state_dense", seed=seed, num_envs=n)
+    cfg = env.task.config
+    lo, hi = np.array(cfg.prop_bbox_lower), np.array(cfg.prop_bbox_upper)
+    env_rs = [np.random.RandomState(seed + e) for e in range(n)]
+    glob_rs = [np.random.RandomState(seed + e) for e in range(n)]
+    qa = env.task.prop_qadr
+
+    def expect(e):
+        g = _uniform_quaternion(glob_rs[e])
+        pos = env_rs[e].uniform(lo, hi)
+        q = _uniform_quaternion(env_rs[e])
+        return g.astype(np.float32), pos.astype(np.float32), q.astype(np.float32)
+
+    def check(envs):
+        qpos = env.physics.get(_lib.QPOS)
+        goals = env.goals()
+        for e in envs:
+            g, pos, q = expect(e)
+            np.testing.assert_array_equal(goals[e], g)
+            np.testing.assert_array_equal(qpos[e, qa:qa + 3], pos)
+            np.testing.assert_array_equal(qpos[e, qa + 3:qa + 7], q)
+
+    ts = env.reset()
+    assert np.all(ts.step_type == 0)
+    check(range(n))
+    resets = 0
+    for i in range(80):
+        env.step(env.sample_actions(i), device_action=True)
+        first = np.nonzero(env.timestep().step_type == 0)[0]
+        check(first)
+        resets += len(first)
+    assert resets >= 40
+    env.close()
