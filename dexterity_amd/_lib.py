@@ -32,7 +32,7 @@ EXPORTS = (
     "dx_jac_site", "dx_ik_solve",
     "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
-    "dx_env_set_time_limit",
+    "dx_env_set_time_limit", "dx_set_outputs",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -105,6 +105,7 @@ def load(path: str = LIB_PATH):
     L.dx_sync.argtypes = [vp]
     L.dx_debug_enable.argtypes = [vp, ctypes.c_int]
     L.dx_sensor_enable.argtypes = [vp, ctypes.c_int]
+    L.dx_set_outputs.argtypes = [vp, ctypes.c_int]
     L.dx_debug_get.argtypes = [vp, ctypes.c_char_p, vp, sz]
     L.dx_last_error.restype = ctypes.c_char_p
     L.dx_abi_version.restype = ctypes.c_int

@@ -909,6 +909,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   }
   B.watch_geom = -1;
   B.watch_body = -1;
+  B.out_bodies = 1;
   if (dx_reset(b, 0, nenv) != 0) { dx_batch_destroy(b); return nullptr; }
   return b;
 }
@@ -1231,6 +1232,12 @@ extern "C" int dx_sync(dx_batch* b) {
   return queue_check(b);
 }
 
+extern "C" int dx_set_outputs(dx_batch* b, int bodies) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  b->db.out_bodies = bodies != 0;
+  return 0;
+}
+
 extern "C" int dx_sensor_enable(dx_batch* b, int enable) {
   if (!b) return fail(DX_EINVAL, "null batch");
   DevBatch& B = b->db;
@@ -1430,6 +1437,7 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
     rc = fail(DX_EHIP, "hipMemcpy failed");
   if (rc) { dx_batch_destroy(b); delete e; return nullptr; }
   b->db.skip = S.skip;
+  b->db.out_bodies = 0;  // the tasks read sites and qpos only (dx_set_outputs turns body poses back on)
   b->db.tp = dP;
   b->db.ts = dS;
   return e;

@@ -93,6 +93,7 @@ struct DevBatch {
   float *site_xpos, *site_vel, *xpos, *xquat;
   int *ncon, *watch, *niter, *ncand;
   const float* xfrc;  // [nbody*6], shared by all envs (may be null)
+  int out_bodies;     // write DX_XPOS / DX_XQUAT after each step (dx_set_outputs)
   const int* skip;    // [nenv] nonzero: env was just reset, observe only (may be null)
   int watch_geom, watch_body;
   const int* watch_pairs;  // body pairs that can hold a watched contact (dx_set_watch), or null

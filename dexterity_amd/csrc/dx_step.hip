@@ -2133,10 +2133,12 @@ __device__ __forceinline__ void observe(const Ctx& c, const DevBatch& B, int env
     vo[0] = cv[3] + wx[0]; vo[1] = cv[4] + wx[1]; vo[2] = cv[5] + wx[2];
     vo[3] = cv[0]; vo[4] = cv[1]; vo[5] = cv[2];
   }
-  // body poses out before the watch pass reuses the com-temporary LDS block
-  const float* xq = c.f(c.L.xquat);
-  for (int k = LANE; k < 3 * c.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * c.nbody + k] = xpos[k];
-  for (int k = LANE; k < 4 * c.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * c.nbody + k] = xq[k];
+  // body poses out (when requested) before the watch pass reuses the com-temporary LDS block
+  if (B.out_bodies) {
+    const float* xq = c.f(c.L.xquat);
+    for (int k = LANE; k < 3 * c.nbody; k += DX_WAVE) B.xpos[(size_t)env * 3 * c.nbody + k] = xpos[k];
+    for (int k = LANE; k < 4 * c.nbody; k += DX_WAVE) B.xquat[(size_t)env * 4 * c.nbody + k] = xq[k];
+  }
   SYNC();
   if (B.watch_geom >= 0 && B.watch) {
     collision(c, 1, B.watch_geom, B.watch_body, B.watch_pairs, B.watch_npairs);

@@ -131,6 +131,11 @@ int dx_forward(dx_batch* b);
 void* dx_stream(dx_batch* b);
 int dx_sync(dx_batch* b);
 
+/* Whether dx_step / dx_forward write the body poses DX_XPOS / DX_XQUAT (default 1 for
+ * a dx_batch, 0 for the batch of a dx_env, whose tasks never read them: 28 B per body
+ * and env-step of HBM writes saved). */
+int dx_set_outputs(dx_batch* b, int bodies);
+
 /* Sensors ---------------------------------------------------------------- */
 /* Enables DX_SENSOR_TORQUE: dx_step / dx_forward then also compute every body's torque
  * sensor (one extra small kernel per call; nothing when disabled). */
