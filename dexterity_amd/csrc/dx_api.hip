@@ -264,6 +264,13 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   d.ntendon = geti(m, "ntendon"); d.nwrap = geti(m, "nwrap"); d.nbpair = geti(m, "nbpair");
   d.ngpair = geti(m, "ngpair"); d.iterations = geti(m, "iterations");
   d.disable_contact = geti(m, "disable_contact");
+  d.solver = geti(m, "solver", 2);  // absent in every reference scene: MuJoCo's default, Newton
+  if (d.solver != 1 && d.solver != 2) {
+    fail(DX_EMODEL, d.solver == 0 ? "solver PGS (the dual solver) is not supported: use CG or Newton"
+                                  : "unknown solver");
+    delete m;
+    return nullptr;
+  }
   d.timestep = (float)getd(m, "timestep"); d.tolerance = (float)getd(m, "tolerance");
   d.impratio = (float)getd(m, "impratio"); d.meaninertia = (float)getd(m, "meaninertia");
   for (int k = 0; k < 3; k++) d.gravity[k] = m->hf["gravity"][k];
@@ -622,6 +629,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.cj_val = take(DX_NCON_MAX * 3 * DX_DOFMAX);
   L.cq = take(3 * DX_NCON_MAX);
   L.cw = take(3 * DX_NCON_MAX);
+  // CG's M^-1 grad: the dead kinematic block past the Newton Hessian when it has room
+  if (U0 + r4(ntri) + r4(nv) <= B0) L.cgv = U0 + r4(ntri);
+  else L.cgv = take(nv);
   end = std::max(end, off);
   L.H = U0;
   L.total = (end + 3) & ~3;  // the kernels zero it with 16-byte stores

@@ -36,6 +36,7 @@ enum { DXR_FRIC = 0, DXR_LIMJ = 1, DXR_LIMT = 2, DXR_CON = 3, DXR_CONFL = 4 };
 struct DevModel {
   int nq, nv, nbody, njnt, ngeom, nsite, nu, ntendon, nwrap, nbpair, ngpair;
   int iterations, disable_contact, any_damping, nlevel, nroot, nfric, nlimj, nlimt;
+  int solver;  // [3P] mjtSolver: 1 CG, 2 Newton (default)
   float timestep, tolerance, impratio, meaninertia;
   float gravity[3];
   // bodies
@@ -132,6 +133,7 @@ struct Lds {
   int ints;  // misc int scalars
   int tsm;   // smooth-solve Cholesky transpose
   int cand;  // collision candidate lists
+  int cgv;   // CG solver: M^-1 grad (nv words, free space during the solve)
   int nefc_max, cand_max;
   int total;
 };

@@ -1836,7 +1836,8 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // -- lane-owned rows r = LANE + 64 k -- so the iterations touch no LDS.
 #define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
 template <class Ctx>
-__device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed) {
+__device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed,
+                                             float* slope0 = nullptr) {
   const DevModel& m = c.mdl();
   int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
@@ -1895,6 +1896,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
     if (fabsf(next - alpha) <= 1e-7f * fabsf(alpha)) break;
     alpha = next;
   }
+  if (slope0) *slope0 = g0;
   // rows whose cost zone differs between the current point and the new one
   int ch = 0;
 #pragma unroll
@@ -1902,6 +1904,98 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
     if (k < ns) ch += jj[k] != 0.f && row_zone(ty[k], Rf[k], ja[k]) != row_zone(ty[k], Rf[k], ja[k] + alpha * jj[k]);
   *changed = wave_sum_i(ch);
   return alpha;
+}
+
+// [3P] MuJoCo's primal CG (mj_solCG), <option solver="CG">: the Newton solver's cost,
+// warm start and exact line search with Polak-Ribiere directions preconditioned by M
+// (Mgrad = M^-1 grad through the matrix-core Cholesky of M), and the same convergence
+// tests -- with the improvement taken from the line search (-alpha g0 / 2) rather than
+// as a difference of fp32 costs.  A non-descent direction restarts along -Mgrad.  Not
+// the default (the reference's scenes run Newton); oracle: dx_oracle.c solve_cg.
+template <class Ctx>
+__device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
+  const int nv = c.nv;
+  float* qacc = c.f(c.L.qacc);
+  float* Ma = c.f(c.L.v1);
+  float* grad = c.f(c.L.v2);
+  float* dir = c.f(c.L.v3);
+  float* Mg_old = c.f(c.L.v5);  // the warm start copy is dead now
+  float* Mg = c.f(c.L.cgv);
+  float* jar = c.f(c.L.efc_jar);
+  const float* M = c.f(c.L.M);
+  const float* qs = c.f(c.L.qfrc_smooth);
+  float* T = c.f(c.L.H);
+  int it = 0;
+  jac_t_force(c, grad);  // grad <- J^T f
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    grad[i] = Ma[i] - qs[i] - grad[i];
+    Mg[i] = grad[i];
+  }
+  SYNC();
+  chol_solve(M, nv, Mg, T);
+  float gmg = 0;
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    dir[i] = -Mg[i];
+    gmg += grad[i] * Mg[i];
+  }
+  float gmg_old = wave_sum(gmg);
+  for (; it < c.iterations; it++) {
+    stage_count(c, CNT_NEWTON_IT);
+    int changed = 0;
+    float g0 = 0.f;
+    const float alpha = line_search(c, qacc, Ma, dir, &changed, &g0);
+    stage_mark(c, ST_NEWTON_LS);
+    if (alpha == 0.f) break;
+    const float* Mdir = c.f(c.L.v4);
+    const float* jvd = c.f(c.L.efc_jv);
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      qacc[i] += alpha * dir[i];
+      Ma[i] += alpha * Mdir[i];
+      Mg_old[i] = Mg[i];
+    }
+    for (int r = LANE; r < c.I[I_NEFC]; r += DX_WAVE) jar[r] += alpha * jvd[r];
+    SYNC();
+    // the decrease along the line, -alpha g0 / 2 (exact for a quadratic segment): the
+    // difference of two fp32 costs drowns in rounding long before CG's slow tail ends
+    const float impr = -0.5f * scale * alpha * g0;
+    jac_t_force(c, grad);
+    float gn = 0;
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      grad[i] = Ma[i] - qs[i] - grad[i];
+      Mg[i] = grad[i];
+      gn += grad[i] * grad[i];
+    }
+    gn = sqrtf(wave_sum(gn)) * scale;
+    SYNC();
+    chol_solve(M, nv, Mg, T);
+    stage_mark(c, ST_NEWTON_GRAD);
+    if (impr < tol || gn < tol) {
+      it++;
+      break;
+    }
+    float num = 0;
+    gmg = 0;
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      num += grad[i] * (Mg[i] - Mg_old[i]);
+      gmg += grad[i] * Mg[i];
+    }
+    num = wave_sum(num);
+    gmg = wave_sum(gmg);
+    const float beta = fmaxf(0.f, num / fmaxf(1e-15f, gmg_old));
+    gmg_old = gmg;
+    float slope = 0;
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      const float di = -Mg[i] + beta * dir[i];
+      slope += grad[i] * di;
+      dir[i] = di;
+    }
+    // not a descent direction (fp32 line searches are exact to 1e-6): restart along -Mgrad
+    if (!(wave_sum(slope) < 0.f))
+      for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -Mg[i];
+    SYNC();
+  }
+  if (LANE == 0) c.I[I_NITER] = it;
+  SYNC();
 }
 
 template <class Ctx>
@@ -1947,6 +2041,10 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   stage_mark(c, ST_NEWTON_EVAL);
   stage_count(c, CNT_SOLVE);
   stage_count(c, CNT_NEFC, nefc);
+  if (m.solver == 1) {
+    solve_cg(c, scale, tol);
+    return;
+  }
   for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
     jac_t_force(c, grad);  // grad <- J^T f

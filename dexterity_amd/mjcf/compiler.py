@@ -559,6 +559,24 @@ class CompiledModel:
     def name2id(self, kind: str, name: str) -> int:
         return self.names[kind].index(name)
 
+    SOLVERS = {"PGS": 0, "CG": 1, "Newton": 2}  # [3P] mjtSolver
+
+    def with_solver(self, solver: str, iterations: Optional[int] = None,
+                    tolerance: Optional[float] = None) -> "CompiledModel":
+        """A copy with MuJoCo's `<option solver=... iterations=... tolerance=...>` set
+        ([3P] mjOption; the reference sets none, so its scenes run Newton, 100
+        iterations, 1e-8).  "CG" and "Newton" run on the device; "PGS" (the dual
+        solver) is rejected by dx_model_load."""
+        if solver not in self.SOLVERS:
+            raise ValueError(f"unknown solver {solver!r}")
+        arrays = dict(self.arrays)
+        arrays["solver"] = np.array([self.SOLVERS[solver]], np.int32)
+        if iterations is not None:
+            arrays["iterations"] = np.array([int(iterations)], np.int32)
+        if tolerance is not None:
+            arrays["tolerance"] = np.array([float(tolerance)])
+        return CompiledModel(arrays, {k: list(v) for k, v in self.names.items()})
+
     def disabled(self, *flags: str) -> "CompiledModel":
         """A copy with MuJoCo subsystems switched off, as
         `physics.model.disable("contact", "gravity", "actuation")` does in the reference
@@ -581,7 +599,7 @@ class CompiledModel:
 
 _SCALAR_INT = {
     "nq", "nv", "nbody", "njnt", "ngeom", "nsite", "nu", "ntendon", "nwrap", "nmesh",
-    "nmeshvert", "nmeshadj", "nbpair", "ngpair", "iterations", "disable_contact",
+    "nmeshvert", "nmeshadj", "nbpair", "ngpair", "iterations", "disable_contact", "solver",
     "ncon_max", "nefc_max",
 }
 _SCALAR_FLT = {"timestep", "tolerance", "impratio", "meaninertia"}

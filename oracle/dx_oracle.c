@@ -43,7 +43,7 @@ struct dxo_model {
   unsigned char* blob;
   size_t nbytes;
   int nq, nv, nbody, njnt, ngeom, nsite, nu, ntendon, nwrap, nmesh, nbpair, ngpair;
-  int iterations, disable_contact, any_damping;
+  int iterations, disable_contact, any_damping, solver;
   double timestep, tolerance, impratio, meaninertia;
   const double* gravity;
   const int *body_parent, *body_rootid, *body_weldid, *body_jntnum, *body_jntadr, *body_dofnum,
@@ -151,6 +151,15 @@ dxo_model* dxo_model_load(const void* blob, size_t nbytes) {
   GETI(gpair_geom); GETI(gpair_condim);
   GETD(gpair_friction); GETD(gpair_solref); GETD(gpair_solimp); GETD(gpair_margin);
   if (!ok) {
+    dxo_model_free(m);
+    return NULL;
+  }
+  /* optional <option solver>: 1 CG, 2 Newton (MuJoCo's default; absent in every
+     reference scene).  PGS (0, dual) is not restated. */
+  s = (const int*)blob_find(m->blob, nbytes, "solver", 0, &cnt);
+  m->solver = s ? s[0] : 2;
+  if (m->solver != 1 && m->solver != 2) {
+    fprintf(stderr, "dxo: solver %d not supported (CG = 1, Newton = 2)\n", m->solver);
     dxo_model_free(m);
     return NULL;
   }
@@ -1516,6 +1525,81 @@ static void solve_newton(const dxo_model* m, dxo_data* d) {
   }
 }
 
+/* [3P] MuJoCo's primal CG (mj_solCG): the same cost, warm start and exact line search
+ * as the Newton solver, with the search direction from Polak-Ribiere nonlinear
+ * conjugate gradients preconditioned by M (Mgrad = M^-1 grad through M's factor), and
+ * the same convergence tests (scaled improvement or scaled gradient < tolerance).  A
+ * direction that is not a descent direction restarts along -Mgrad. */
+static void solve_cg(const dxo_model* m, dxo_data* d) {
+  int nv = m->nv;
+  double* Ma = d->tmp1;
+  double* grad = d->tmp2;
+  double* dir = d->tmp3;
+  double* Mg = d->tmp4;
+  double* Mg_old = d->H;  /* nv doubles of scratch (H is unused by CG) */
+  double* qacc = d->qacc;
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  memcpy(qacc, d->qacc_warmstart, 8 * nv);
+  double cost = eval_cost(m, d, qacc, Ma);
+  double cost_smooth = eval_cost(m, d, d->qacc_smooth, Ma);
+  if (cost_smooth < cost) {
+    memcpy(qacc, d->qacc_smooth, 8 * nv);
+    cost = cost_smooth;
+  } else {
+    cost = eval_cost(m, d, qacc, Ma);
+  }
+  d->niter = 0;
+  if (d->nefc == 0) {
+    memcpy(qacc, d->qacc_smooth, 8 * nv);
+    return;
+  }
+  /* gradient = M qacc - qfrc_smooth - J^T force; Mgrad = M^-1 gradient */
+#define CG_GRAD()                                                                   \
+  do {                                                                              \
+    for (int i = 0; i < nv; i++) grad[i] = Ma[i] - d->qfrc_smooth[i];               \
+    for (int r = 0; r < d->nefc; r++) {                                             \
+      const double* J = d->efc_J + (size_t)r * nv;                                  \
+      for (int k = 0; k < nv; k++) grad[k] -= J[k] * d->efc_force[r];               \
+    }                                                                               \
+    chol_solve(d->L, Mg, grad, nv, &d->flops[DXO_ST_SOLVE]);                        \
+    d->flops[DXO_ST_SOLVE] += 2.0 * nv * d->nefc;                                   \
+  } while (0)
+  CG_GRAD();
+  double gMg_old = 0;
+  for (int i = 0; i < nv; i++) { dir[i] = -Mg[i]; gMg_old += grad[i] * Mg[i]; }
+  for (int it = 0; it < m->iterations; it++) {
+    double alpha = line_search(m, d, qacc, Ma, dir);
+    if (alpha == 0) break;
+    for (int i = 0; i < nv; i++) qacc[i] += alpha * dir[i];
+    double newcost = eval_cost(m, d, qacc, Ma);
+    d->niter++;
+    double improvement = scale * (cost - newcost);
+    cost = newcost;
+    memcpy(Mg_old, Mg, 8 * nv);
+    CG_GRAD();
+    double gnorm = 0;
+    for (int i = 0; i < nv; i++) gnorm += grad[i] * grad[i];
+    gnorm = sqrt(gnorm) * scale;
+    if (improvement < m->tolerance || gnorm < m->tolerance) break;
+    double num = 0, gMg = 0;
+    for (int i = 0; i < nv; i++) { num += grad[i] * (Mg[i] - Mg_old[i]); gMg += grad[i] * Mg[i]; }
+    double beta = num / fmax(MINVAL, gMg_old);
+    if (beta < 0) beta = 0;
+    gMg_old = gMg;
+    double slope = 0;
+    for (int i = 0; i < nv; i++) {
+      dir[i] = -Mg[i] + beta * dir[i];
+      slope += grad[i] * dir[i];
+    }
+    /* not a descent direction (the line search is exact only to its tolerance): restart
+       along -M^-1 grad */
+    if (!(slope < 0))
+      for (int i = 0; i < nv; i++) dir[i] = -Mg[i];
+    d->flops[DXO_ST_SOLVE] += 8.0 * nv;
+  }
+#undef CG_GRAD
+}
+
 static void finish_constraint(const dxo_model* m, dxo_data* d) {
   int nv = m->nv;
   memset(d->qfrc_constraint, 0, 8 * nv);
@@ -1686,7 +1770,10 @@ int dxo_forward(const dxo_model* m, dxo_data* d) {
   rne(m, d);
   smooth_forces(m, d);
   /* constraint velocities were computed in make_constraint with current qvel */
-  solve_newton(m, d);
+  if (m->solver == 1)
+    solve_cg(m, d);
+  else
+    solve_newton(m, d);
   finish_constraint(m, d);
   rne_post_constraint(m, d);
   return 0;

@@ -337,3 +337,35 @@ def test_reorient_resets_replay_numpy_random_state(built):
         resets += len(first)
     assert resets >= 40
     env.close()
+
+
+def test_collision_free_joint_sampling_kat(built, oracle_mod):
+    """hands_test.py:100-110: joint angles drawn by sample_collision_free_joint_angles
+    (dexterous_hand.py:144-168, here over the full joint range) put the Adroit hand in
+    no self-contact -- checked by the fp64 oracle's collision pass at every env's
+    sampled configuration (has_self_collision: any hand-hand contact with dist <= 1e-8,
+    utils/mujoco_collisions.py:95-127)."""
+    from dexterity_amd import _lib, manipulation
+
+    cfg = manipulation.ReachConfig(init_joint_range_fraction=1.0)
+    env = manipulation.GoalEnvironment(manipulation.Reach(cfg, hand="adroit"), num_envs=64, seed=12345)
+    ts = env.reset()
+    assert np.all(ts.step_type == 0)
+    qpos = env.physics.get(_lib.QPOS).astype(np.float64)
+    cm = env.task.compiled
+    lo, hi = np.asarray(cm.jnt_range, dtype=np.float64)[: cm.nq].T
+    assert np.all(qpos >= lo - 1e-6) and np.all(qpos <= hi + 1e-6)
+    om = oracle_mod.OracleModel(env.model.blob)
+    spread = qpos.std(axis=0)
+    assert np.all(spread[hi > lo] > 0.05 * (hi - lo)[hi > lo])  # really spread over the range
+    touching = 0
+    for e in range(env.num_envs):
+        d = oracle_mod.OracleData(om)
+        d.qpos[:] = qpos[e]
+        d.kinematics()
+        c = d.contacts()
+        dist = c[:, 12] if len(c) else np.zeros(0)
+        assert np.all(dist > -1e-6), (e, dist.min())  # fp32 sampling vs fp64 check
+        touching += int(np.any(dist <= 1e-8))
+    assert touching == 0
+    env.close()

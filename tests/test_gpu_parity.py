@@ -556,3 +556,30 @@ def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
         big.step(5)
     assert np.all(np.isfinite(big.qpos)) and np.all(np.isfinite(big.qvel))
     assert (big.get(_lib.NCON)[:, 0] > 0).mean() > 0.5
+
+
+def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):
+    """<option solver="CG"> ([3P] MuJoCo's primal CG): the kernel's CG (dx_step.hip
+    solve_cg) against the oracle's (dx_oracle.c solve_cg) on the contact-rich states,
+    and both against the Newton optimum; then a few CG substeps stay finite."""
+    cm, xfrc, om, states, _ = reorient_setup
+    # CG converges linearly, and fp32 and fp64 CG take different paths: both run to
+    # the optimum (tight tolerance, ample iterations) and are compared there
+    cg = cm.with_solver("CG", iterations=1000, tolerance=1e-10)
+    model = gpu.Model(cg)
+    om_cg = oracle_mod.OracleModel(blob.pack(cg.arrays))
+    phys = _load_states(gpu, model, xfrc, states)
+    phys.forward()
+    qacc = phys.qacc
+    for e, st in enumerate(states):
+        d_cg = _oracle_forward(oracle_mod, om_cg, cg, xfrc, st)
+        d_nt = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        scale = max(1.0, np.abs(d_nt.qacc_smooth).max())
+        assert np.abs(qacc[e] - d_cg.qacc).max() <= 5e-4 * scale, (e, np.abs(qacc[e] - d_cg.qacc).max(), scale)
+        assert np.abs(qacc[e] - d_nt.qacc).max() <= 5e-4 * scale
+    phys.close()
+    # MuJoCo's defaults (100 iterations, 1e-8) with CG: the reorient batch steps
+    phys = _load_states(gpu, gpu.Model(cm.with_solver("CG")), xfrc, states)
+    phys.step(10)
+    assert np.all(np.isfinite(phys.qpos))
+    phys.close()

@@ -235,3 +235,38 @@ def test_oracle_adroit_fingertip_golden_ik(oracle_mod):
     assert np.all(err <= 1e-3)
     d.fk()
     np.testing.assert_allclose(d.site_xpos.reshape(-1, 3)[sites], golden, atol=1e-3)
+
+
+def test_oracle_cg_reaches_the_newton_optimum(oracle_mod, reorient_compiled):
+    """`<option solver="CG">` ([3P] MuJoCo's primal Polak-Ribiere CG) minimises the same
+    convex constraint cost as Newton: on contact-rich states both reach the same
+    acceleration (to the solvers' tolerance) and cost."""
+    from dexterity_amd import blob
+
+    cm = reorient_compiled
+    xfrc = gravity_compensation(cm, "shadow_hand_e/")
+    newton = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    cg = oracle_mod.OracleModel(blob.pack(cm.with_solver("CG", iterations=1000, tolerance=1e-10).arrays))
+    rng = np.random.RandomState(3)
+    d = oracle_mod.OracleData(newton)
+    d.xfrc_applied[:] = xfrc.ravel()
+    d.qpos[24:27] += [0.01, -0.01, 0]
+    lo, hi = cm.actuator_ctrlrange.T
+    checked = 0
+    for s in range(120):
+        d.ctrl[:] = 0.3 * rng.uniform(lo, hi)
+        d.step()
+        if s % 20 != 19:
+            continue
+        a = oracle_mod.OracleData(newton)
+        b = oracle_mod.OracleData(cg)
+        for x in (a, b):
+            x.xfrc_applied[:] = xfrc.ravel()
+            x.qpos[:], x.qvel[:], x.ctrl[:], x.qacc_warmstart[:] = d.qpos, d.qvel, d.ctrl, d.qacc_warmstart
+            x.forward()
+        assert a.nefc == b.nefc and a.nefc > 24
+        scale = max(1.0, np.abs(a.qacc_smooth).max())
+        assert np.abs(a.qacc - b.qacc).max() <= 1e-4 * scale, np.abs(a.qacc - b.qacc).max()
+        assert b.niter >= 1
+        checked += a.ncon > 0
+    assert checked >= 3
