@@ -1324,6 +1324,7 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
                                               const float* action);
 extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBatch B);
 extern "C" __global__ void dx_mt_seed_kernel(int nenv, uint64_t seed, uint32_t* mt_env, uint32_t* mt_goal);
+extern "C" __global__ void dx_mtw_seed_kernel(int nenv, uint64_t seed, uint32_t* mt);
 
 struct dx_env {
   dx_batch* batch;
@@ -1433,6 +1434,17 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   TaskState* dS = nullptr;
   if (!rc && task == DX_TASK_REACH) {
     size_t nt = 3 * (size_t)nq + (size_t)nu * nq;
+    // optional fp64 block (raw bits of 6 x nq doubles) for numpy-compatible draws
+    if (nparams >= DX_REACH_NPARAMS_HEAD + (int)nt + 12 * nq) {
+      nt += 12 * (size_t)nq;
+      P.tdata_f64 = 1;
+      rc |= al((void**)&S.mt_reach, E * DX_MTW_WORDS * 4);
+      if (!rc) {
+        hipLaunchKernelGGL(dx_mtw_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv, seed,
+                           S.mt_reach);
+        if (hipGetLastError() != hipSuccess) rc = fail(DX_EHIP, "MT19937 seeding kernel launch failed");
+      }
+    }
     rc |= al((void**)&tdata, nt * 4);
     if (!rc && hipMemcpy(tdata, params + DX_REACH_NPARAMS_HEAD, nt * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = fail(DX_EHIP, "hipMemcpy failed");

@@ -158,6 +158,8 @@ struct TaskParams {
   int coupled[8][2];        // qpos[c[0]] = qpos[c[1]] after uniform joint sampling
   float range_frac, goal_scale;
   const float* tdata;       // device: ref[nq] | lo[nq] | hi[nq] | position->control [nu][nq]
+                            // [| fp64 raw bits: ref, normal scale, lo, hi, uniform lower, upper]
+  int tdata_f64;            // the fp64 block is present (numpy-compatible draws)
   uint64_t seed;
 };
 
@@ -169,6 +171,10 @@ struct TaskState {
   // reorient: numpy-compatible MT19937 streams per env (dx_mt_*): the env's RandomState
   // (PropPlacer draws) and numpy's global stream (the goal draws), [625][nenv] each
   uint32_t *mt_env, *mt_goal;
+  // reach: the env's RandomState as one contiguous block per env, [nenv][DX_MTW_WORDS]
+  // (state[624], pos, has_gauss, gauss as fp64), drawn wave-cooperatively in the step
+  // kernel (dx_step.hip mtw_*)
+  uint32_t* mt_reach;
 };
 
 // numpy.random.RandomState-compatible MT19937 ([3P] numpy legacy seeding and
@@ -178,6 +184,14 @@ struct TaskState {
 // sweep across a wave's envs.  Pinned against numpy in tests/test_host_logic.py and
 // tests/test_gpu_env.py.
 #define DX_MT_WORDS 625
+#define DX_MTW_WORDS 628
+// tempering of an MT19937 state word (mt19937_genrand output stage)
+__device__ __forceinline__ uint32_t dx_mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  return y ^ (y >> 18);
+}
 __device__ __forceinline__ void dx_mt_seed(uint32_t* s, int nenv, int env, uint32_t seed) {
   for (int k = 0; k < 624; k++) {
     s[(size_t)k * nenv + env] = seed;
@@ -195,13 +209,9 @@ __device__ __forceinline__ uint32_t dx_mt_next(uint32_t* s, int nenv, int env) {
     }
     pos = 0;
   }
-  uint32_t y = s[(size_t)pos * nenv + env];
+  const uint32_t y = s[(size_t)pos * nenv + env];
   s[(size_t)624 * nenv + env] = pos + 1;
-  y ^= y >> 11;
-  y ^= (y << 7) & 0x9d2c5680u;
-  y ^= (y << 15) & 0xefc60000u;
-  y ^= y >> 18;
-  return y;
+  return dx_mt_temper(y);
 }
 // RandomState.random_sample: 53-bit double from two outputs
 __device__ __forceinline__ double dx_mt_double(uint32_t* s, int nenv, int env) {
@@ -218,7 +228,7 @@ __device__ __forceinline__ void dx_mt_uniform_quat(uint32_t* s, int nenv, int en
   const double u2 = twopi * dx_mt_double(s, nenv, env);
   const double u3 = twopi * dx_mt_double(s, nenv, env);
   const double a = sqrt(1.0 - u1), b = sqrt(u1);
-  q[0] = (float)(a * sin(u2));
+  q[0] = (float)(a * sin(u2));  // products only: no contraction to worry about
   q[1] = (float)(a * cos(u2));
   q[2] = (float)(b * sin(u3));
   q[3] = (float)(b * cos(u3));

@@ -2282,6 +2282,145 @@ __device__ __forceinline__ bool contact_now(const Ctx& c) {
   return __any(hit) != 0;
 }
 
+// numpy RandomState draws for one env, by the whole wave ([3P] numpy legacy MT19937:
+// mt19937_gen, legacy_double, legacy_gauss).  The env's 624-word state block is copied
+// to LDS scratch (the collision candidate area, free before a pass), outputs pos.. are
+// tempered in parallel, and a block that runs out is twisted in place in LDS: chunks
+// of 64 in index order, each chunk's loads before its stores, which is the serial
+// loop's dependency order (new[k] needs new[k - 227] for k >= 227, new[0] for k = 623).
+// The block goes back to HBM only when the draws really consumed past it.
+__device__ __forceinline__ void mtw_twist(uint32_t* sm) {
+  for (int base = 0; base < 624; base += DX_WAVE) {
+    const int k = base + LANE;
+    uint32_t a = 0, b = 0, c = 0;
+    if (k < 624) { a = sm[k]; b = sm[(k + 1) % 624]; c = sm[(k + 397) % 624]; }
+    SYNC();
+    if (k < 624) {
+      const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+      sm[k] = c ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+    }
+    SYNC();
+  }
+}
+struct MtWave {
+  uint32_t* g;   // the env's HBM block (DX_MTW_WORDS)
+  uint32_t* sm;  // 624 words of LDS
+  int pos;       // read position in the current block (uniform)
+  bool twisted;  // LDS holds the next block
+};
+__device__ __forceinline__ MtWave mtw_begin(uint32_t* g, uint32_t* sm) {
+  MtWave w;
+  w.g = g;
+  w.sm = sm;
+  // this wave may have rewritten the block earlier in the launch: invalidate the vector
+  // L1 so the reloads see those stores
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  for (int k = LANE; k < 624; k += DX_WAVE) sm[k] = g[k];
+  w.pos = (int)g[624];
+  w.twisted = false;
+  SYNC();
+  return w;
+}
+// Outputs [pos, pos + n) of the stream, lane j gets outputs pos + stride*j + t, t < cnt
+// (cnt <= 4, n = stride * 64 at most 624); advances pos by `used` (<= n) afterwards
+// through mtw_consume.
+__device__ __forceinline__ void mtw_fetch(MtWave& w, int stride, int cnt, uint32_t* out) {
+  const int n = stride * DX_WAVE;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const int q = w.pos + stride * LANE + t;
+    out[t] = (t < cnt && q < 624) ? dx_mt_temper(w.sm[q]) : 0u;
+  }
+  if (w.pos + n > 624) {  // part of the batch lies in the next block
+    SYNC();
+    mtw_twist(w.sm);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+      const int q = w.pos + stride * LANE + t;
+      if (t < cnt && q >= 624) out[t] = dx_mt_temper(w.sm[q - 624]);
+    }
+    w.twisted = true;
+  }
+}
+__device__ __forceinline__ void mtw_consume(MtWave& w, int used) {
+  if (w.twisted && w.pos + used >= 624) {
+    w.pos = w.pos + used - 624;
+    for (int k = LANE; k < 624; k += DX_WAVE) w.g[k] = w.sm[k];
+  } else if (w.twisted) {  // speculative twist: the stream is still in the old block
+    for (int k = LANE; k < 624; k += DX_WAVE) w.sm[k] = w.g[k];
+    w.pos += used;
+  } else {
+    w.pos += used;
+  }
+  w.twisted = false;
+  if (LANE == 0) w.g[624] = (uint32_t)w.pos;
+  SYNC();
+}
+__device__ __forceinline__ double mt_to_double(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
+// RandomState.uniform(lo, hi) for lanes < n: lo + (hi - lo) * random_sample()
+__device__ __forceinline__ double mtw_uniform(MtWave& w, int n, double lo, double hi) {
+  uint32_t o[4];
+  mtw_fetch(w, 2, 2, o);
+  const double u = mt_to_double(o[0], o[1]);
+  mtw_consume(w, 2 * n);
+  return __dadd_rn(lo, __dmul_rn(hi - lo, u));
+}
+// RandomState.normal(loc, scale) for lanes < n (legacy_gauss: polar pairs, the second
+// value of a pair cached in the state for the next call).  Candidate pairs come 64 at
+// a time (lane j: outputs 4j..4j+3); accepted ones are ranked by a ballot.
+__device__ __forceinline__ double mtw_normal(MtWave& w, int n, double loc, double scale, double* pairs) {
+  int has = (int)w.g[625];
+  double cached;
+  {
+    const uint64_t lo32 = w.g[626], hi32 = w.g[627];
+    cached = __longlong_as_double((long long)(lo32 | (hi32 << 32)));
+  }
+  const int need = n - has;          // gaussians to draw from pairs
+  const int npairs = (need + 1) / 2;
+  int got = 0;
+  while (got < npairs) {
+    uint32_t o[4];
+    mtw_fetch(w, 4, 4, o);
+    const double x1 = 2.0 * mt_to_double(o[0], o[1]) - 1.0;
+    const double x2 = 2.0 * mt_to_double(o[2], o[3]) - 1.0;
+    const double r2 = __dadd_rn(__dmul_rn(x1, x1), __dmul_rn(x2, x2));
+    const bool acc = r2 < 1.0 && r2 != 0.0;
+    const uint64_t m = __ballot(acc);
+    const int rank = got + __popcll(m & ((1ull << LANE) - 1ull));
+    if (acc && rank < npairs) {
+      const double f = sqrt(-2.0 * log(r2) / r2);
+      pairs[2 * rank] = __dmul_rn(f, x2);      // returned first
+      pairs[2 * rank + 1] = __dmul_rn(f, x1);  // cached for the next call
+    }
+    const int take = min(npairs - got, __popcll(m));
+    int used = 4 * DX_WAVE;  // the whole batch unless the last needed pair is in it
+    if (take == npairs - got) {
+      // lane index of the take-th accepted candidate
+      uint64_t mm = m;
+      for (int t = 1; t < take; t++) mm &= mm - 1;
+      used = 4 * (__ffsll((long long)mm) - 1 + 1);
+    }
+    got += take;
+    mtw_consume(w, used);
+  }
+  SYNC();
+  const int i = LANE;
+  double g = 0.0;
+  if (i < n) g = (has && i == 0) ? cached : pairs[i - has];
+  // state: a leftover second value of the last pair stays cached
+  if (LANE == 0 && n > 0) {  // the cached value (if any) was used; an odd count leaves one
+    const bool odd = (need & 1) != 0;
+    const uint64_t bits = (uint64_t)__double_as_longlong(odd ? pairs[need] : 0.0);
+    w.g[625] = odd ? 1u : 0u;
+    w.g[626] = (uint32_t)bits;
+    w.g[627] = (uint32_t)(bits >> 32);
+  }
+  SYNC();
+  return __dadd_rn(loc, __dmul_rn(scale, g));
+}
+
 // FingertipCartesianPosition.next_goal (fingertip_position.py:72-125) and
 // DexterousHand.sample_collision_free_joint_angles (dexterous_hand.py:144-168) for
 // one environment, with the reference's side effects on the physics state: after a
@@ -2301,6 +2440,20 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
   const float* lo = ref + nq;
   const float* hi = lo + nq;
   const float* p2c = hi + nq;
+  // numpy-compatible draws (P.tdata_f64): the env's RandomState block and the fp64
+  // constants after the fp32 tables, lane = joint
+  const bool npy = P.tdata_f64 && T.mt_reach;
+  const float* f64 = p2c + (size_t)nu * nq;  // raw bits, two words per double (4-byte aligned)
+  auto ld64 = [&](int i) -> double {
+    const uint64_t lo32 = (uint32_t)__float_as_int(f64[2 * i]), hi32 = (uint32_t)__float_as_int(f64[2 * i + 1]);
+    return __longlong_as_double((long long)(lo32 | (hi32 << 32)));
+  };
+  // (the fp64 constants are loaded at each draw: kept live across the physics rollouts
+  // they would push this kernel's registers into scratch)
+  const int jl = min(LANE, nq - 1);
+  uint32_t* mt_block = npy ? T.mt_reach + (size_t)env * DX_MTW_WORDS : nullptr;
+  uint32_t* mt_sm = (uint32_t*)c.f(c.L.cand);  // free before each collision pass
+  double* mt_pairs = (double*)c.f(c.L.cand + 624);
   const float q_init = LANE < nq ? qpos[LANE] : 0.f;
   const float c_init = LANE < nu ? ctrl[LANE] : 0.f;
   if (need & 1) {
@@ -2309,7 +2462,11 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
     bool ok = false;
     for (int a = 0; a < P.max_reject; a++) {
       // qpos_desired ~ N(midrange, scale * range), clipped to the joint range
-      if (LANE < nq) {
+      if (npy) {
+        MtWave w = mtw_begin(mt_block, mt_sm);
+        const double q = mtw_normal(w, nq, ld64(jl), ld64(nq + jl), mt_pairs);
+        if (LANE < nq) qpos[LANE] = (float)fmin(ld64(3 * nq + jl), fmax(ld64(2 * nq + jl), q));
+      } else if (LANE < nq) {
         int draw = 0x100000 + (((g & 4095) * 128 + (a & 127)) * 64 + LANE) * 2;
         float u1 = dx_urand(P.seed, env, ep, draw), u2 = dx_urand(P.seed, env, ep, draw + 1);
         float z = sqrtf(-2.0f * logf(fmaxf(u1, 1e-12f))) * cosf(6.283185307179586f * u2);
@@ -2356,7 +2513,11 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
   if (need & 2) {
     // uniform within range_fraction * range, coupled joints equalised, until no contact
     for (int a = 0; a < 1000; a++) {
-      if (LANE < nq) {
+      if (npy) {
+        MtWave w = mtw_begin(mt_block, mt_sm);
+        const double q = mtw_uniform(w, nq, ld64(4 * nq + jl), ld64(5 * nq + jl));
+        if (LANE < nq) qpos[LANE] = (float)q;
+      } else if (LANE < nq) {
         float u = dx_urand(P.seed, env, ep, 0x200000 + a * 64 + LANE);
         float l = P.range_frac * lo[LANE], h = P.range_frac * hi[LANE];
         qpos[LANE] = l + (h - l) * u;
@@ -2509,7 +2670,8 @@ __device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int 
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
 // mode 2: reach sampling pass (goal rollouts / joint sampling), state out only
 template <class SP>
-__device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode) {
+__device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub, int mode,
+                                          bool prep = false) {
   extern __shared__ float smem[];
   if ((int)blockIdx.x >= B.nenv) return;
   // longest-first dispatch: the order kernel sorts envs by their last step's cost
@@ -2520,7 +2682,7 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   c.I = (int*)(smem + c.L.ints);
   c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
   float time = env_begin(c, B, env);
-  if (mode == 2) {  // reach sampling pass: new state only, no outputs
+  if (prep) {  // reach sampling pass (mode 2): new state only, no outputs
     reach_prep(c, B, env, time);
     env_store_state(c, B, env, time);
     return;
@@ -2631,6 +2793,14 @@ dx_step_kernel_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub
   if (mode == 3) step_queue<SP>(m, B, L, nsub);
   else step_body<SP>(m, B, L, nsub, mode);
 }
+// Mode 2 (reach goal rollouts / joint sampling) is its own kernel, so the rarely-run
+// sampling code does not share the step kernel's register allocation.
+template <class SP>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_prep_kernel_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  step_body<SP>(m, B, L, 1, 2, true);
+}
 
 template <class SP>
 static bool spec_matches(const DevModel& d, const Lds& L) {
@@ -2651,7 +2821,10 @@ static bool spec_matches(const DevModel& d, const Lds& L) {
   bool dx_match_##SP(const DevModel& d, const Lds& L) { return spec_matches<SP>(d, L); }             \
   hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
                             const Lds& L, int nsub, int mode) {                                       \
-    hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
+    if (mode == 2)                                                                                    \
+      hipLaunchKernelGGL(dx_prep_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L);         \
+    else                                                                                              \
+      hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
     return hipGetLastError();                                                                         \
   }
 #define DX_SPEC_DEFINE1(SP) DX_SPEC_DEFINE(SP)
@@ -2666,6 +2839,11 @@ dx_step_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
   else step_body<SpecRT>(m, B, L, nsub, mode);
+}
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_prep_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  step_body<SpecRT>(m, B, L, 1, 2, true);
 }
 
 // Index of the specialization whose layout and dimensions equal the model's, or -1.
@@ -2712,7 +2890,10 @@ hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, co
   DX_SPECS(DX_LAUNCH)
 #undef DX_LAUNCH
   (void)k;
-  hipLaunchKernelGGL(dx_step_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode);
+  if (mode == 2)
+    hipLaunchKernelGGL(dx_prep_kernel, dim3(grid), dim3(64), lds, stream, m, B, L);
+  else
+    hipLaunchKernelGGL(dx_step_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode);
   return hipGetLastError();
 }
 

@@ -38,6 +38,23 @@ extern "C" __global__ void dx_mt_seed_kernel(int nenv, uint64_t seed, uint32_t* 
   dx_mt_seed(mt_goal, nenv, env, s);
 }
 
+// Reach: env e's RandomState(seed + e) as a contiguous block (state, pos = 624, no
+// cached gaussian).
+extern "C" __global__ void dx_mtw_seed_kernel(int nenv, uint64_t seed, uint32_t* mt) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= nenv) return;
+  uint32_t* s = mt + (size_t)env * DX_MTW_WORDS;
+  uint32_t v = (uint32_t)(seed + (uint64_t)env);
+  for (int k = 0; k < 624; k++) {
+    s[k] = v;
+    v = 1812433253u * (v ^ (v >> 30)) + (uint32_t)(k + 1);
+  }
+  s[624] = 624;
+  s[625] = 0;
+  s[626] = 0;
+  s[627] = 0;
+}
+
 // orientation distance || axisangle(quat_diff_active(cur, goal)) || = 2 acos(|<goal, cur>|)
 // (prop_orientation.py:40-50, [3P] dm_robotics quat_diff_active / quat_to_axisangle)
 __device__ __forceinline__ float quat_distance(const float* g, const float* c) {
@@ -78,8 +95,9 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
       dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);
       if (P.prop_qadr >= 0) {
         for (int k = 0; k < 3; k++)
-          q[P.prop_qadr + k] = (float)(P.bbox_lo_d[k] + (P.bbox_hi_d[k] - P.bbox_lo_d[k]) *
-                                                            dx_mt_double(S.mt_env, P.nenv, env));
+          // random_uniform: low + (high - low) * u, rounded as numpy does (no fma)
+          q[P.prop_qadr + k] = (float)__dadd_rn(P.bbox_lo_d[k], __dmul_rn(P.bbox_hi_d[k] - P.bbox_lo_d[k],
+                                                                          dx_mt_double(S.mt_env, P.nenv, env)));
         dx_mt_uniform_quat(S.mt_env, P.nenv, env, q + P.prop_qadr + 3);
       }
     } else {

@@ -224,7 +224,12 @@ class Reach:
         mid = self.joint_range.mean(axis=1)  # fingertip_position.py:80-82
         tail = np.concatenate([mid, lo, hi, np.asarray(self.position_to_control, dtype=np.float64).ravel()])
         assert tail.size == 3 * cm.nq + cm.nu * cm.nq
-        return np.concatenate([head, tail.astype(np.float32)])
+        # fp64 draw constants, as the reference computes them (raw bits): the goal's
+        # normal(loc=midrange, scale=0.1 * range) and clip (fingertip_position.py:67-86),
+        # the initial joints' uniform(range_fraction * limits) (dexterous_hand.py:137-142)
+        f64 = np.concatenate([mid, c.goal_scale * (hi - lo), lo, hi, c.init_joint_range_fraction * lo,
+                              c.init_joint_range_fraction * hi]).astype(np.float64)
+        return np.concatenate([head, tail.astype(np.float32), f64.view(np.float32)])
 
     def observation_layout(self):
         return observation_layout(self.hand_nq, self.hand_nv, self.ntips, False, self.hand_name, 3 * self.ntips)

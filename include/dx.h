@@ -178,7 +178,13 @@ enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
  *  12 max_time_per_goal  13 dense reward (1) / sparse (0)  14 init joint range fraction
  *  15 goal sampling scale  16 max rejection samples  17 n coupled joint pairs
  *  18-25 coupled pairs (joint, source joint): qpos[joint] = qpos[source]
- *  26..  joint midrange [nq], lower [nq], upper [nq], position->control [nu][nq] */
+ *  26..  joint midrange [nq], lower [nq], upper [nq], position->control [nu][nq]
+ *  then, optionally, six fp64 arrays [nq] as raw bits (two words each): the goal
+ *  sampler's mean (joint midrange) and scale (0.1 x range), the joint limits, and the
+ *  initial-joint bounds (range_fraction x limits).  With them env e draws from a
+ *  numpy-compatible RandomState(seed + e) in the reference's order (goal normals with
+ *  numpy's cached polar gaussians, then the uniform joint angles); without them, from a
+ *  counter-based stream. */
 #define DX_REACH_NPARAMS_HEAD 26
 enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT_STEP_TYPE = 3,
                   DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5, DX_OUT_GOAL_FAILURES = 6,

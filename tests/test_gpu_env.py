@@ -369,3 +369,49 @@ def test_collision_free_joint_sampling_kat(built, oracle_mod):
         touching += int(np.any(dist <= 1e-8))
     assert touching == 0
     env.close()
+
+
+@pytest.mark.parametrize("domain", ["reach", "reach_shadow"])
+def test_reach_resets_replay_numpy_random_state(built, domain):
+    """Seed-level reset parity for reach: env e's RandomState(seed + e)
+    feeds, in the reference's order, the goal sampler -- random_state.normal(midrange,
+    0.1 range) per rejection attempt (fingertip_position.py:79-86, numpy's polar
+    gaussians with the cached second value) -- and then the initial joints --
+    random_state.uniform(0.5 lo, 0.5 hi) per attempt (dexterous_hand.py:137-168), with
+    the Shadow hand's coupled joints equalised.  Replaying numpy, the device's initial
+    joints equal one of the first uniform draws after one of the first goal attempts,
+    bit for bit after the fp32 cast."""
+    from dexterity_amd import _lib, hands, manipulation
+
+    seed, n = 4321, 64
+    env = manipulation.load(domain, "state_dense", seed=seed, num_envs=n)
+    t = env.task
+    lo, hi = t.joint_range[:, 0], t.joint_range[:, 1]
+    mid = t.joint_range.mean(axis=1)
+    frac = t.config.init_joint_range_fraction
+    env.reset()
+    qpos = env.physics.get(_lib.QPOS)
+    assert np.all(env.goal_failures() == 0)
+    attempts = []
+    for e in range(n):
+        found = None
+        for kg in range(1, t.config.max_rejection_samples + 1):  # goal attempts
+            rs = np.random.RandomState(seed + e)
+            for _ in range(kg):
+                rs.normal(loc=mid, scale=t.config.goal_scale * (hi - lo))
+            # the next 400 joint attempts at once (uniform over [400, nq] consumes the
+            # stream exactly as 400 successive uniform(lo, hi) calls)
+            q = rs.uniform(frac * lo, frac * hi, size=(400, len(lo)))
+            if domain == "reach_shadow":
+                for ids in hands.COUPLED_JOINT_IDS:
+                    q[:, ids] = q[:, [ids[-1]]]
+            hit = np.nonzero(np.all(q.astype(np.float32) == qpos[e], axis=1))[0]
+            if len(hit):
+                found = (kg, int(hit[0]) + 1)
+                break
+        assert found is not None, e
+        attempts.append(found)
+    assert max(a[0] for a in attempts) >= 1
+    if domain == "reach_shadow":  # contacts disabled: every first draw is accepted
+        assert all(a == (1, 1) for a in attempts)
+    env.close()
