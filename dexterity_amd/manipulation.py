@@ -400,6 +400,8 @@ SUITE = {
 }
 ALL_TASKS = tuple(sorted(SUITE))
 ALL_NAMES = [".".join(t) for t in ALL_TASKS]
+# manipulation/__init__.py:53 (_get_tasks_by_domain)
+TASKS_BY_DOMAIN = {d: tuple(t for dd, t in ALL_TASKS if dd == d) for d in sorted({d for d, _ in ALL_TASKS})}
 
 
 def load(domain_name: str, task_name: str, seed: Optional[int] = None,
@@ -418,4 +420,4 @@ def load(domain_name: str, task_name: str, seed: Optional[int] = None,
 
 
 __all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "Reach", "ReachConfig", "ALL_TASKS",
-           "ALL_NAMES", "StepType"]
+           "ALL_NAMES", "TASKS_BY_DOMAIN", "StepType"]

@@ -415,3 +415,33 @@ def test_reach_resets_replay_numpy_random_state(built, domain):
     if domain == "reach_shadow":  # contacts disabled: every first draw is accepted
         assert all(a == (1, 1) for a in attempts)
     env.close()
+
+
+@pytest.mark.parametrize("name", ["reach.state_dense", "reach.state_sparse", "reach_shadow.state_dense",
+                                  "reorient.state_dense"])
+def test_task_runs(built, name):
+    """manipulation_test.py:23-46 for every registered task: 5 episodes x 10 steps from
+    seed 12345 with uniform random actions within the action spec; every observation
+    matches its spec (shape, finite) and every discount lies in [0, 1].  Batched: 16
+    envs; a FIRST step reports reward 0 and discount 1 where dm_env has None."""
+    from dexterity_amd import manipulation
+
+    domain, task = name.split(".")
+    n = 16
+    env = manipulation.load(domain, task, seed=12345, num_envs=n)
+    rs = np.random.RandomState(12345)
+    obs_spec, act_spec = env.observation_spec(), env.action_spec()
+    assert np.all(np.isfinite(act_spec.minimum)) and np.all(np.isfinite(act_spec.maximum))
+    for _ in range(5):
+        ts = env.reset()
+        for _ in range(10):
+            assert list(ts.observation) == list(obs_spec)
+            for k, spec in obs_spec.items():
+                v = ts.observation[k]
+                assert v.shape == (n,) + spec.shape and np.all(np.isfinite(v)), k
+            first = ts.step_type == 0
+            assert np.all(ts.reward[first] == 0) and np.all(ts.discount[first] == 1)
+            assert np.all((ts.discount >= 0) & (ts.discount <= 1))
+            action = rs.uniform(act_spec.minimum, act_spec.maximum, size=(n,) + act_spec.shape)
+            ts = env.step(action.astype(act_spec.dtype))
+    env.close()

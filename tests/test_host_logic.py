@@ -234,3 +234,17 @@ def test_prop_spawn_never_touches_the_hand(oracle_mod, reorient_compiled):
                          np.sqrt(u1) * np.cos(u3)]
         d.kinematics()
         assert not any(gb[int(c[13])] == prop or gb[int(c[14])] == prop for c in d.contacts())
+
+
+def test_loader_constants():
+    """loader_test.py:8-12 and manipulation/__init__.py:47-53."""
+    from dexterity_amd import manipulation
+
+    assert manipulation.ALL_TASKS and manipulation.ALL_NAMES and manipulation.TASKS_BY_DOMAIN
+    assert ("reorient", "state_dense") in manipulation.ALL_TASKS
+    assert manipulation.TASKS_BY_DOMAIN["reach"] == ("state_dense", "state_sparse")
+    assert "reorient.state_dense" in manipulation.ALL_NAMES
+    with pytest.raises(ValueError):
+        manipulation.load("nope", "state_dense")
+    with pytest.raises(ValueError):
+        manipulation.load("reorient", "nope")
