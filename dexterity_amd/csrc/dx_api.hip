@@ -900,11 +900,12 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
   // substep queue state (DX_NO_QUEUE=1: one workgroup per env for the whole step)
   b->queue = !getenv("DX_NO_QUEUE");
-  rc |= balloc(b, (void**)&B.qhead, 4);
+  rc |= balloc(b, (void**)&B.qhead, DX_QUEUES * DX_QHEAD_STRIDE * 4);
   rc |= balloc(b, (void**)&B.progress, E * 4);
   rc |= balloc(b, (void**)&B.qerr, 4);
   B.epoch = 0;
-  B.qbase = 0;
+  // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
+  B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
@@ -1075,22 +1076,19 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   const bool queued = mode == 0 && b->queue && nsub < 32;
   const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots) : b->nenv;
   if (queued) {
-    // substep queue: a new progress epoch; the task counter is never reset -- this
-    // launch's tasks are the claims qbase .. qbase + ntask - 1 (mod 2^32)
+    // substep queue: a new progress epoch and zeroed task counters
     DevBatch& B = b->db;
     if (++B.epoch >= (1u << 26)) {  // tags wrap: start over from zeroed progress
       HIPCHK(hipMemsetAsync(B.progress, 0, (size_t)b->nenv * 4, b->stream));
       B.epoch = 1;
     }
+    HIPCHK(hipMemsetAsync(B.qhead, 0, DX_QUEUES * DX_QHEAD_STRIDE * 4, b->stream));
   }
   hipEvent_t t0;
   timing_begin(b, &t0);
   hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
   HIPCHK(e);
-  // every workgroup of a queued launch makes exactly one claim past the last task
-  // (advanced only for a launch that was enqueued: the device counter moved with it)
-  if (queued) b->db.qbase += (unsigned)b->nenv * (unsigned)nsub + (unsigned)grid;
   // torque sensors from the last substep's stash (mode 0 step, mode 1 forward)
   if (b->db.sen_stash && mode != 2)
     HIPCHK(dx_launch_sensor(b->nenv, ((size_t)b->model->lds.total + 6 * DX_MAX_NV) * 4, b->stream, b->dm_dev, b->db,

@@ -14,6 +14,8 @@
 // 0-2 pos, 3-11 frame (normal, tangents), 12 dist, 13 geom pair, 14 nnz | nrows << 8
 // (key while sorting), 15 first efc row, 16-17 friction (mu1, mu2), 18-19 dof support mask
 #define DX_MAX_NV 64      // dof bitmasks are uint64
+#define DX_QUEUES 8         // substep queues: one per XCD (MI355X: 8 XCDs)
+#define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
 #ifndef DX_NPG
 #define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
@@ -108,12 +110,14 @@ struct DevBatch {
   unsigned* cost;                 // [nenv] shader cycles / 1024 of the env's last step, or null
   const TaskParams* tp;           // device copies, reach sampling pass only (mode 2)
   const TaskState* ts;
-  // substep queue (mode 3, dx_step.hip step_queue): task counter, per-env progress
-  // tags (epoch * 32 + substeps done), launch epoch, the
-  // counter value of this launch's first task, timeout mark
+  // substep queue (mode 3, dx_step.hip step_queue): one task counter per queue
+  // ([DX_QUEUES][DX_QHEAD_STRIDE], zeroed on the stream before each queued launch),
+  // per-env progress tags (epoch * 32 + substeps done), launch epoch, the number of
+  // queues in use (1 or DX_QUEUES: one per XCD), timeout mark
   unsigned* qhead;
   unsigned* progress;
-  unsigned epoch, qbase;
+  unsigned epoch;
+  int nqueue;
   int* qerr;
   // torque sensors (dx_sensor.hip): the last substep's pre-integration state, solved
   // qacc and contact forces, [nenv][dx_sensor_stash_words]; null when the field is off

@@ -2703,8 +2703,14 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
 }
 
 // Substep queue (mode 0): one task = one physics step of one environment, claimed in
-// order from a device counter -- substep s of every env (longest-first within the
-// round) before substep s + 1 of any.  The env's state moves through HBM between
+// order from a device counter -- substep s of every env of the queue (longest-first
+// within the round) before substep s + 1 of any.  There is one queue per XCD: queue q
+// holds the envs at positions q, q + 8, q + 16, ... of the longest-first order, and a
+// workgroup claims from its own XCD's queue (HW_REG_XCC_ID), so an env's five tasks
+// normally run under one L2 and its hand-offs and separating-direction cache are L2
+// hits, not fabric round trips.  When its queue is empty the workgroup takes tasks
+// from the next queues.  Placement only decides speed: the hand-off protocol below is
+// the cross-XCD one whichever workgroup takes a task.  The env's state moves through HBM between
 // its tasks (~0.5 KB + its separating-direction cache), so the wave slots stay
 // busy until the last round instead of idling behind the few environments whose
 // control step is 2-3x the mean (a whole control step per workgroup left most of
@@ -2721,14 +2727,24 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   extern __shared__ float smem[];
   CtxT<SP> c(m, Lrt, smem, nullptr, nullptr);
   c.I = (int*)(smem + c.L.ints);
-  const unsigned ntask = (unsigned)B.nenv * (unsigned)nsub;
+  const int nqueue = B.nqueue;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  int q = (int)((xcc & 7u) % (unsigned)nqueue);
+  int empty = 0;  // queues found drained, in the order this workgroup visits them
   for (;;) {
+    // queue q: order positions q + nqueue * j, j < nq
+    const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
     unsigned t = 0;
-    if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - B.qbase;
+    if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __builtin_amdgcn_readfirstlane(t);
-    if (t >= ntask) break;
-    const int s = (int)(t / (unsigned)B.nenv);
-    const int k = (int)(t - (unsigned)s * (unsigned)B.nenv);
+    if (t >= nq * (unsigned)nsub) {
+      if (++empty >= nqueue) break;
+      q = q + 1 == nqueue ? 0 : q + 1;
+      continue;
+    }
+    const int s = (int)(t / nq);
+    const int k = q + nqueue * (int)(t - (unsigned)s * nq);
     const int env = B.order ? B.order[k] : k;
     if (s > 0) {
       int abort = 0;

