@@ -903,6 +903,8 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.qhead, DX_QUEUES * DX_QHEAD_STRIDE * 4);
   rc |= balloc(b, (void**)&B.progress, E * 4);
   rc |= balloc(b, (void**)&B.qerr, 4);
+  B.hand_stride = (d.nq + 2 * d.nv + 2 + 31) / 32 * 32;
+  rc |= balloc(b, (void**)&B.hand, E * B.hand_stride * 4);
   B.epoch = 0;
   // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;

@@ -119,6 +119,12 @@ struct DevBatch {
   unsigned epoch;
   int nqueue;
   int* qerr;
+  // the state an env's task hands to its next substep's task: [nenv][hand_stride]
+  // floats = qpos | qvel | warm start | time | cost so far, each record on whole
+  // 128-B lines (hand_stride a multiple of 32), so a hand-off writes back and reads
+  // only its own lines
+  float* hand;
+  int hand_stride;
   // torque sensors (dx_sensor.hip): the last substep's pre-integration state, solved
   // qacc and contact forces, [nenv][dx_sensor_stash_words]; null when the field is off
   float* sen_stash;

@@ -989,8 +989,10 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
           float depth, nrm[3], pos[3];
           int r = mpr_step(A, B, M, depth, nrm, pos, st);
           if (r && c.sep && SL == 0) {
-            // remember a separating direction; forget it once the pair touches
-            if (r == 1) c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1));
+            // remember a separating direction (unless it is the cached one, still
+            // separating: phase -1); forget it once the pair touches
+            if (r == 1 && M.phase != -1)
+              c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1));
             else if (cached) c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(0.f, 0.f, 0.f, 0.f);
           }
           if (r) {
@@ -2538,8 +2540,10 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
 // ------------------------------------------------------------------------ //
 // Per-env pieces shared by the launch-per-env kernel and the substep queue.
 // env_begin: zero the env's LDS block, load its state; returns its time.
+// rec: the env's hand-off record (substeps after the first of a queued step), or null
+// for the batch arrays.
 template <class Ctx>
-__device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env) {
+__device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env, const float* rec = nullptr) {
   const Lds& L = c.L;
   float* smem = c.S;
   // Zero the whole per-env LDS block: the Cholesky solve reads a few words past its
@@ -2556,14 +2560,24 @@ __device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env) {
   float* qvel = c.f(L.qvel);
   float* ctrl = c.f(L.ctrl);
   float* ws = c.f(L.v5);
-  for (int i = LANE; i < c.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * c.nq + i];
-  for (int i = LANE; i < c.nv; i += DX_WAVE) {
-    qvel[i] = B.qvel[(size_t)env * c.nv + i];
-    ws[i] = B.qacc_ws[(size_t)env * c.nv + i];
+  float time;
+  if (rec) {
+    for (int i = LANE; i < c.nq; i += DX_WAVE) qpos[i] = rec[i];
+    for (int i = LANE; i < c.nv; i += DX_WAVE) {
+      qvel[i] = rec[c.nq + i];
+      ws[i] = rec[c.nq + c.nv + i];
+    }
+    time = rec[c.nq + 2 * c.nv];
+  } else {
+    for (int i = LANE; i < c.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * c.nq + i];
+    for (int i = LANE; i < c.nv; i += DX_WAVE) {
+      qvel[i] = B.qvel[(size_t)env * c.nv + i];
+      ws[i] = B.qacc_ws[(size_t)env * c.nv + i];
+    }
+    time = B.time[env];
   }
   for (int i = LANE; i < c.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * c.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
-  const float time = B.time[env];
   SYNC();
   return time;
 }
@@ -2579,6 +2593,23 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
     B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
   }
   if (LANE == 0) B.time[env] = time;
+}
+
+// The hand-off record (DevBatch::hand) of a task whose env has substeps left.
+template <class Ctx>
+__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, float time, unsigned cost) {
+  const float* qpos = c.f(c.L.qpos);
+  const float* qvel = c.f(c.L.qvel);
+  const float* ws = c.f(c.L.v5);
+  for (int i = LANE; i < c.nq; i += DX_WAVE) rec[i] = qpos[i];
+  for (int i = LANE; i < c.nv; i += DX_WAVE) {
+    rec[c.nq + i] = qvel[i];
+    rec[c.nq + c.nv + i] = ws[i];
+  }
+  if (LANE == 0) {
+    rec[c.nq + 2 * c.nv] = time;
+    rec[c.nq + 2 * c.nv + 1] = __uint_as_float(cost);
+  }
 }
 
 // Torque sensors (dx_sensor.hip), when enabled: the state the sensors of mj_step2
@@ -2710,8 +2741,9 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
 // normally run under one L2 and its hand-offs and separating-direction cache are L2
 // hits, not fabric round trips.  When its queue is empty the workgroup takes tasks
 // from the next queues.  Placement only decides speed: the hand-off protocol below is
-// the cross-XCD one whichever workgroup takes a task.  The env's state moves through HBM between
-// its tasks (~0.5 KB + its separating-direction cache), so the wave slots stay
+// the cross-XCD one whichever workgroup takes a task.  The env's state moves between its tasks
+// through its hand-off record (DevBatch::hand, 3 lines for a Shadow hand) and its
+// separating-direction cache, so the wave slots stay
 // busy until the last round instead of idling behind the few environments whose
 // control step is 2-3x the mean (a whole control step per workgroup left most of
 // the second round's slots waiting on them).  Task (s, e) waits for (s - 1, e),
@@ -2773,13 +2805,17 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     c.stage_acc = B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr;
     c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
-    float time = env_begin(c, B, env);
+    float* rec = B.hand + (size_t)env * B.hand_stride;
+    // cost so far (shader cycles / 1024), carried in the record between substeps
+    const unsigned cost0 = s > 0 ? __float_as_uint(rec[c.nq + 2 * c.nv + 1]) : 0u;
+    float time = env_begin(c, B, env, s > 0 ? rec : nullptr);
     if (!(B.skip && B.skip[env])) env_substep(c, B, time, s == nsub - 1 ? env : -1);  // a freshly reset env is only observed
-    if (s == nsub - 1) env_finish(c, B, env, time);
-    else env_store_state(c, B, env, time);
-    if (LANE == 0 && B.cost) {
-      const unsigned dt = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
-      B.cost[env] = s == 0 ? dt : B.cost[env] + dt;
+    if (s == nsub - 1) {
+      env_finish(c, B, env, time);
+      if (LANE == 0 && B.cost)
+        B.cost[env] = cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+    } else {
+      env_store_hand(c, rec, time, cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull));
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
