@@ -118,16 +118,22 @@ static void quat2mat_h(float* R, const float* q) {
 // ------------------------------------------------------------------------ //
 // direction-binned hulls (support-point acceleration, exact)
 // ------------------------------------------------------------------------ //
-// A hull with more than 64 vertices gets a cube map of n x n cells per face over
-// the local direction sphere (cell rule: dx_step.hip hull_cell).  Each cell stores
-// the vertices that can be a support point for some direction in the cell, sorted
-// by vertex index and padded to the mesh's capacity `cap` (a multiple of 16, at
-// most 64), so the device scans one cell with one 16-lane pass and one memory round
-// trip.  A vertex is dropped only if a single other vertex beats it by more than
-// 1e-5 R at all four corner directions of the (slightly enlarged) cell, hence at
-// every direction of the cell: every maximiser -- ties included -- of every
-// direction in the cell is kept, and the lowest-index maximiser over the cell's list
-// is the vertex the full scan returns (the oracle's rule).
+// A hull with more than 16 vertices gets a cube map of n x n cells per face over the
+// local direction sphere (cell rule: dx_step.hip hull_cell).  Each cell lists the
+// vertices that can be a support point for some direction in the cell, sorted by
+// vertex index.  A vertex is dropped only if a single other vertex beats it by more
+// than 1e-5 R at all four corner directions of the (slightly enlarged) cell, hence at
+// every direction of the cell: every maximiser -- ties included -- of every direction
+// in the cell is kept, and the lowest-index maximiser over the cell's list is the
+// vertex the full scan returns (the oracle's rule).
+// Layout: one 16-slot block per cell (x, y, z, vertex index; index -1 pads), so the
+// device reads a cell with one memory round trip of two 16-B loads per lane.  A cell
+// with more than 16 candidates (the faces of a hull with many coplanar vertices: all
+// of them tie along the face normal) keeps candidates 0..14 in its block and a header
+// in slot 15 = (overflow offset in float4s from the hull's first cell, candidate
+// count, 0, index -2); candidates 15.. follow in the hull's overflow run, padded to a
+// multiple of 16.  n is the smallest of 1, 2, 3, 4, 6, 8 with at most 2 % of the
+// cells overflowing.
 static void cell_corners(int face, int n, int iu, int iv, double eps, double c[4][3]) {
   int ax = face >> 1;
   double sgn = (face & 1) ? -1.0 : 1.0;
@@ -175,50 +181,66 @@ static void build_hull_bins(dx_model* m) {
   int nmesh = (int)num.size();
   std::vector<int> bn(std::max(nmesh, 1), 0), bcap(std::max(nmesh, 1), 0), badr(std::max(nmesh, 1), 0);
   std::vector<float> b4;
-  static const int kN[] = {4, 6, 8, 12, 16};
+  static const int kN[] = {1, 2, 3, 4, 6, 8};
   const char* env_minn = getenv("DX_HULL_BIN_MINN");  // (experiments: finer cube maps)
-  const int minn = env_minn ? atoi(env_minn) : 4;
+  const int minn = env_minn ? atoi(env_minn) : 1;
   for (int i = 0; i < nmesh; i++) {
     int nv = num[i];
-    if (nv <= 64) continue;
+    if (nv <= 16) continue;
     std::vector<double> V(3 * nv);
     double R = 0;
     for (int j = 0; j < nv; j++) {
       for (int k = 0; k < 3; k++) V[3 * j + k] = mv[3 * (adr[i] + j) + k];
       R = std::max(R, std::sqrt(V[3 * j] * V[3 * j] + V[3 * j + 1] * V[3 * j + 1] + V[3 * j + 2] * V[3 * j + 2]));
     }
-    for (int n : kN) {
-      if (n < minn) continue;
-      std::vector<std::vector<int>> cells(6 * n * n);
-      int cap = 0;
-      for (int f = 0; f < 6 && cap <= 64; f++)
-        for (int iu = 0; iu < n && cap <= 64; iu++)
-          for (int iv = 0; iv < n && cap <= 64; iv++) {
+    std::vector<std::vector<int>> cells;
+    int n = 0;
+    for (int nn : kN) {
+      if (nn < minn && nn != kN[5]) continue;
+      cells.assign(6 * nn * nn, {});
+      int over = 0;
+      for (int f = 0; f < 6; f++)
+        for (int iu = 0; iu < nn; iu++)
+          for (int iv = 0; iv < nn; iv++) {
             double c[4][3];
-            cell_corners(f, n, iu, iv, 1e-3, c);
-            auto& L = cells[(f * n + iu) * n + iv];
+            cell_corners(f, nn, iu, iv, 1e-3, c);
+            auto& L = cells[(f * nn + iu) * nn + iv];
             hull_cell_candidates(V, nv, R, c, L);
-            cap = std::max(cap, (int)L.size());
+            over += L.size() > 16;
           }
-      if (cap > 64) continue;
-      cap = (cap + 15) & ~15;
-      bn[i] = n;
-      bcap[i] = cap;
-      badr[i] = (int)(b4.size() / 4);
-      for (auto& L : cells) {
-        for (int s = 0; s < cap; s++) {
-          float e[4] = {0.f, 0.f, 0.f, 0.f};
-          int idx = -1;
-          if (s < (int)L.size()) {
-            idx = L[s];
-            for (int k = 0; k < 3; k++) e[k] = mv[3 * (adr[i] + idx) + k];
-          }
-          memcpy(&e[3], &idx, 4);
-          b4.insert(b4.end(), e, e + 4);
-        }
-      }
-      break;
+      n = nn;
+      if (over <= 0.02 * (double)cells.size()) break;
     }
+    const size_t base = b4.size() / 4;  // this hull's first cell, in float4s
+    const size_t ncell = cells.size();
+    b4.resize(4 * (base + 16 * ncell), 0.f);
+    auto put = [&](size_t slot, int idx) {
+      float* e = b4.data() + 4 * slot;
+      for (int k = 0; k < 3; k++) e[k] = idx >= 0 ? mv[3 * (adr[i] + idx) + k] : 0.f;
+      memcpy(e + 3, &idx, 4);
+    };
+    for (size_t cidx = 0; cidx < ncell; cidx++) {
+      const auto& L = cells[cidx];
+      const size_t blk = base + 16 * cidx;
+      if (L.size() <= 16) {
+        for (int s = 0; s < 16; s++) put(blk + s, s < (int)L.size() ? L[s] : -1);
+        continue;
+      }
+      for (int s = 0; s < 15; s++) put(blk + s, L[s]);
+      const size_t ov = b4.size() / 4;  // overflow run: candidates 15.., padded to 16
+      const int nov = (int)L.size() - 15;
+      b4.resize(4 * (ov + (size_t)(nov + 15) / 16 * 16), 0.f);
+      for (int s = 0; s < (nov + 15) / 16 * 16; s++) put(ov + s, s < nov ? L[15 + s] : -1);
+      float* h = b4.data() + 4 * (blk + 15);
+      const int off = (int)(ov - base), cnt = (int)L.size(), tag = -2;
+      memcpy(h, &off, 4);
+      memcpy(h + 1, &cnt, 4);
+      h[2] = 0.f;
+      memcpy(h + 3, &tag, 4);
+    }
+    bn[i] = n;
+    bcap[i] = 16;
+    badr[i] = (int)base;
   }
   if (b4.empty()) b4.assign(4, 0.f);
   m->hf["mesh_bin4"] = b4;
@@ -696,8 +718,14 @@ extern "C" int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[
     }
   }
   if (cell >= 0) {
-    for (int s = 0; s < cap; s++) {
-      const float* e = b4 + 4 * ((size_t)cell * cap + s);
+    // the cell's block, then its overflow run when slot 15 is a header
+    const float* blk = b4 + 4 * (size_t)cell * 16;
+    int hdr;
+    memcpy(&hdr, blk + 4 * 15 + 3, 4);
+    int off = 0, cnt = 16;
+    if (hdr == -2) { memcpy(&off, blk + 4 * 15, 4); memcpy(&cnt, blk + 4 * 15 + 1, 4); }
+    for (int s = 0; s < cnt; s++) {
+      const float* e = hdr == -2 && s >= 15 ? b4 + 4 * ((size_t)off + s - 15) : blk + 4 * s;
       int idx;
       memcpy(&idx, e + 3, 4);
       if (idx < 0) continue;

@@ -251,14 +251,16 @@ __device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i,
   h.y = t ? v.y : h.y;
   h.z = t ? v.z : h.z;
 }
-// Group reduction: lowest slot among the lanes holding the maximum.  Slots are in
-// ascending vertex-index order (whole hull, or a binned cell's sorted list), so this
-// is the vertex the oracle's serial scan returns; its coordinates come from the lane
-// that scanned it (slot s is scanned by group lane s % 16) through ds_bpermute.
+// Group reduction: the lowest vertex index among the lanes holding the maximum (a
+// cell's list is sorted by vertex index, a whole hull is scanned in index order, so
+// this is the vertex the oracle's serial scan returns); its coordinates come from the
+// lane that scanned it, found by ballot and read through ds_bpermute.
 __device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
   float vmax = row_max_f(h.d);
   int bi = row_min_i(h.d == vmax ? h.i : 0x7fffffff);
-  int src = GBASE | (bi & (DX_NPG - 1));
+  const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
+  const unsigned grp = (unsigned)(own >> GBASE) & ((1u << DX_NPG) - 1u);
+  int src = GBASE | (grp ? __builtin_ctz(grp) : 0);
   lp[0] = __shfl(h.x, src, 64);
   lp[1] = __shfl(h.y, src, 64);
   lp[2] = __shfl(h.z, src, 64);
@@ -281,56 +283,113 @@ __device__ __forceinline__ int hull_cell(const float* ld, int n) {
   int face = 2 * ax + (a < 0 ? 1 : 0);
   return (face * n + iu) * n + iv;
 }
-// The slots a support scan of `s` along local direction ld must visit.
-__device__ __forceinline__ void hull_span(const Shape& s, const float* ld, const DXG float4*& p, int& cnt) {
-  p = s.vert4;
-  cnt = s.nvert;
+// One hull's support scan by a lane group.  First a 16-slot block -- the direction's
+// cube-map cell (dx_api.hip build_hull_bins), or the first 16 vertices of a hull that
+// is not binned / a zero direction -- two 16-B loads per lane, one memory round trip;
+// then, rarely, an overflow run: the rest of a cell whose slot 15 is a header, or the
+// rest of a whole-hull scan.
+constexpr int DX_SLK = 16 / DX_NPG;  // block slots per lane
+struct HullScan {
+  HullBest h;
+  const DXG float4* ov;  // overflow run (a valid address even when empty)
+  int nov;               // its slots
+  bool cell;             // cell scan: the vertex index is the slot's w; else the slot number
+};
+__device__ __forceinline__ void hull_block(const Shape& s, const float* ld, const DXG float4*& blk, int& n1, bool& cell) {
+  blk = s.vert4;
+  n1 = min(s.nvert, 16);
+  cell = false;
   if (s.bin_n > 0) {
-    int cell = hull_cell(ld, s.bin_n);
-    if (cell >= 0) {
-      p = s.bin4 + cell * s.bin_cap;
-      cnt = s.bin_cap;
+    int c = hull_cell(ld, s.bin_n);
+    if (c >= 0) {
+      blk = s.bin4 + 16 * c;
+      n1 = 16;
+      cell = true;
     }
   }
 }
+__device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[DX_SLK],
+                                                const DXG float4* blk, int n1, bool cell, HullScan& H) {
+#pragma unroll
+  for (int u = 0; u < DX_SLK; u++) {
+    const int sl = u * DX_NPG + SL;
+    const int idx = cell ? __float_as_int(v[u].w) : sl;
+    hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < n1 && idx >= 0);
+  }
+  // slot 15 (the group's last lane, last load) of a cell: a header (index -2) names
+  // the overflow run.  The header is rare: the lanes that hold one are found by ballot
+  // and only then is it broadcast to its group.
+  H.cell = cell;
+  H.ov = blk;
+  H.nov = 0;
+  const bool hdr = cell && SL == DX_NPG - 1 && __float_as_int(v[DX_SLK - 1].w) == -2;
+  if (__any(hdr)) {
+    const int src = GBASE | (DX_NPG - 1);
+    const int tag = __shfl(__float_as_int(v[DX_SLK - 1].w), src, 64);
+    const int off = __shfl(__float_as_int(v[DX_SLK - 1].x), src, 64);
+    const int cnt = __shfl(__float_as_int(v[DX_SLK - 1].y), src, 64);
+    if (cell && tag == -2) {
+      H.ov = s.bin4 + off;
+      H.nov = cnt - 15;
+    }
+  }
+  if (!cell && s.nvert > 16) {
+    H.ov = s.vert4 + 16;
+    H.nov = s.nvert - 16;
+  }
+}
+__device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)[DX_SLK], int base, HullScan& H) {
+#pragma unroll
+  for (int u = 0; u < DX_SLK; u++) {
+    const int sl = base + u * DX_NPG + SL;
+    const int idx = H.cell ? __float_as_int(v[u].w) : 16 + sl;
+    hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < H.nov && idx >= 0);
+  }
+}
 
-// Support points of A along dir and of B along -dir, by one lane group.  Both
-// hulls (or their direction cells, <= 64 slots) are scanned in the same pass from L2:
-// eight float4 loads in flight per lane, one memory round trip.
+// Support points of A along dir and of B along -dir, by one lane group: both hulls'
+// blocks in the same round trip (four 16-B loads per lane), then the overflow runs of
+// either, 16 slots a pass, while any group of the wave has one left.
 __device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, const float* dir, float* outA,
                                              float* outB) {
   float nd[3] = {-dir[0], -dir[1], -dir[2]};
   float la[3], lb[3];
   mattvec3(la, A.mat, dir);
   mattvec3(lb, B.mat, nd);
-  const DXG float4 *VA, *VB;
-  int nA, nB;  // 0 unless a hull
-  hull_span(A, la, VA, nA);
-  hull_span(B, lb, VB, nB);
-  HullBest hA = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff}, hB = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
-  const int n = max(nA, nB);
-  for (int base = 0; base < n; base += 64) {
-    // (all 64 slots every pass: skipping the unneeded tail under a uniform mask was
-    // measured 5 % slower -- it breaks up the batch of loads in flight)
-    float4 va[64 / DX_NPG], vb[64 / DX_NPG];
+  const bool hA = A.type == DXG_MESH, hB = B.type == DXG_MESH;
+  HullScan SA, SB;
+  SA.h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+  SB.h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+  SA.nov = SB.nov = 0;
+  if (hA || hB) {
+    const DXG float4 *bA = A.vert4, *bB = B.vert4;
+    int nA = 0, nB = 0;
+    bool cA = false, cB = false;
+    if (hA) hull_block(A, la, bA, nA, cA);
+    if (hB) hull_block(B, lb, bB, nB, cB);
+    float4 va[DX_SLK], vb[DX_SLK];
 #pragma unroll
-    for (int u = 0; u < 64 / DX_NPG; u++) {
-      int i = base + u * DX_NPG + SL;
-      va[u] = VA[i < nA ? i : 0];
-      vb[u] = VB[i < nB ? i : 0];
+    for (int u = 0; u < DX_SLK; u++) {
+      const int sl = u * DX_NPG + SL;
+      va[u] = bA[sl < nA ? sl : 0];
+      vb[u] = bB[sl < nB ? sl : 0];
     }
+    if (hA) hull_take_block(A, la, va, bA, nA, cA, SA);
+    if (hB) hull_take_block(B, lb, vb, bB, nB, cB, SB);
+    for (int base = 0; __any(base < SA.nov || base < SB.nov); base += 16) {
 #pragma unroll
-    for (int u = 0; u < 64 / DX_NPG; u++) {
-      int i = base + u * DX_NPG + SL;
-      hull_take(hA, va[u], va[u].x * la[0] + va[u].y * la[1] + va[u].z * la[2], i,
-                i < nA && __float_as_int(va[u].w) >= 0);
-      hull_take(hB, vb[u], vb[u].x * lb[0] + vb[u].y * lb[1] + vb[u].z * lb[2], i,
-                i < nB && __float_as_int(vb[u].w) >= 0);
+      for (int u = 0; u < DX_SLK; u++) {
+        const int sl = base + u * DX_NPG + SL;
+        va[u] = SA.ov[sl < SA.nov ? sl : 0];
+        vb[u] = SB.ov[sl < SB.nov ? sl : 0];
+      }
+      if (base < SA.nov) hull_take_run(la, va, base, SA);
+      if (base < SB.nov) hull_take_run(lb, vb, base, SB);
     }
   }
   float pa[3], pb[3];
-  if (nA > 0) hull_reduce(hA, pa); else support_prim(A, la, pa);
-  if (nB > 0) hull_reduce(hB, pb); else support_prim(B, lb, pb);
+  if (hA) hull_reduce(SA.h, pa); else support_prim(A, la, pa);
+  if (hB) hull_reduce(SB.h, pb); else support_prim(B, lb, pb);
   support_world(A, pa, dir, outA);
   support_world(B, pb, nd, outB);
 }
@@ -339,25 +398,28 @@ __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, fl
   float ld[3], lp[3];
   mattvec3(ld, s.mat, dir);
   if (s.type == DXG_MESH) {
-    const DXG float4* V;
-    int cnt;
-    hull_span(s, ld, V, cnt);
-    HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
-    for (int base = 0; base < cnt; base += 64) {
-      float4 v[64 / DX_NPG];
+    const DXG float4* blk;
+    int n1;
+    bool cell;
+    hull_block(s, ld, blk, n1, cell);
+    HullScan S;
+    S.h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+    float4 v[DX_SLK];
 #pragma unroll
-      for (int u = 0; u < 64 / DX_NPG; u++) {
-        int i = base + u * DX_NPG + SL;
-        v[u] = V[i < cnt ? i : 0];
-      }
-#pragma unroll
-      for (int u = 0; u < 64 / DX_NPG; u++) {
-        int i = base + u * DX_NPG + SL;
-        hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], i,
-                  i < cnt && __float_as_int(v[u].w) >= 0);
-      }
+    for (int u = 0; u < DX_SLK; u++) {
+      const int sl = u * DX_NPG + SL;
+      v[u] = blk[sl < n1 ? sl : 0];
     }
-    hull_reduce(h, lp);
+    hull_take_block(s, ld, v, blk, n1, cell, S);
+    for (int base = 0; __any(base < S.nov); base += 16) {
+#pragma unroll
+      for (int u = 0; u < DX_SLK; u++) {
+        const int sl = base + u * DX_NPG + SL;
+        v[u] = S.ov[sl < S.nov ? sl : 0];
+      }
+      if (base < S.nov) hull_take_run(ld, v, base, S);
+    }
+    hull_reduce(S.h, lp);
   } else {
     support_prim(s, ld, lp);
   }
