@@ -38,6 +38,14 @@ with open(os.path.join(DST, f"{tag}_kernel_stats.md"), "w") as f:
         f.write(f"| {r['Name'][:60]} | {r['Calls']} | {float(r['TotalDurationNs'])/1e6:.3f} | "
                 f"{float(r['AverageNs'])/1e6:.4f} | {float(r['MinNs'])/1e6:.4f} | {float(r['MaxNs'])/1e6:.4f} | "
                 f"{float(r['Percentage']):.2f} |\n")
+    # the bench's timed region: the last 40 step-kernel dispatches (warmup and reset
+    # launches excluded), the launches bench.py's HIP-event mean covers
+    tr = [r for r in csv.DictReader(open(one("trace/**/run_kernel_trace.csv"))) if "dx_step_kernel" in r["Kernel_Name"]]
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    last = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in tr[-40:]]
+    if last:
+        f.write(f"\nStep kernel over the timed region (last {len(last)} dispatches): mean {statistics.mean(last):.4f} ms, "
+                f"min {min(last):.4f}, max {max(last):.4f}\n")
 
 
 def pmc(kind, counter):
