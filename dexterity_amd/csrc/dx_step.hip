@@ -480,6 +480,12 @@ __device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprStat
   }
 }
 // Returns 0: running, 1: separated (no contact), 2: penetration (depth/normal/pos set).
+// The eight groups of a wave are in different MPR phases on most trips, so the phases
+// share one code path: every phase's next direction is normalize(cross(A - C, B - C))
+// (or -v0) with its operands selected per group, and the new support point goes to one
+// portal slot chosen per group.  Each phase performs exactly the arithmetic of libccd's
+// structure (the oracle's dxo_mpr), so the results are unchanged; only the separated,
+// degenerate and final exits branch.
 __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState& S, float& depth, float* normal,
                                         float* pos, NpStats& st) {
   const float tol = 1e-6f;
@@ -492,91 +498,15 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
   support_pair(A, B, dir, p.a, p.b);
   sub3(p.v, p.a, p.b);
   st.support++;
-  if (S.phase == -1) {  // cached separating direction
-    float dt = dot3(p.v, dir);
-    if (fzero(dt) || dt < 0) return 1;
-    dir[0] = -v0[0]; dir[1] = -v0[1]; dir[2] = -v0[2];
-    normalize3(dir);
-    S.phase = 0;
-    return 0;
-  }
-  if (S.phase == 0) {
-    mp_st(P + 9, p);  // P1
-    float dt = dot3(p.v, dir);
-    if (fzero(dt) || dt < 0) return 1;
-    cross3(dir, v0, p.v);
-    if (fzero(dot3(dir, dir))) {
-      if (fzero(p.v[0]) && fzero(p.v[1]) && fzero(p.v[2])) {
-        depth = 0;
-        normal[0] = 0; normal[1] = 0; normal[2] = 1;
-      } else {
-        depth = norm3(p.v);
-        for (int k = 0; k < 3; k++) normal[k] = p.v[k];
-        normalize3(normal);
-      }
-      for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p.a[k] + p.b[k]);
-      return 2;
-    }
-    normalize3(dir);
-    S.phase = 1;
-    return 0;
-  }
-  if (S.phase == 1) {  // p = P2
-    float dt = dot3(p.v, dir);
-    if (fzero(dt) || dt < 0) return 1;
-    float va[3], vb[3];
-    sub3(va, v1, v0);
-    sub3(vb, p.v, v0);
-    cross3(dir, va, vb);
-    normalize3(dir);
-    if (dot3(dir, v0) > 0) {  // swap P1 and P2
-      MPoint q;
-      mp_ld(P + 9, q);
-      mp_st(P + 18, q);
-      mp_st(P + 9, p);
-      dir[0] = -dir[0]; dir[1] = -dir[1]; dir[2] = -dir[2];
-    } else {
-      mp_st(P + 18, p);
-    }
-    S.phase = 2;
-    S.it = 0;
-    return 0;
-  }
-  if (S.phase == 2) {  // p = P3
-    if (S.it > 1000) return 1;
-    float dt = dot3(p.v, dir);
-    if (fzero(dt) || dt < 0) return 1;
-    float va[3], vb[3];
-    cross3(va, v1, p.v);
-    dt = dot3(va, v0);
-    bool r2 = dt < 0 && !fzero(dt);
-    cross3(va, p.v, v2);
-    dt = dot3(va, v0);
-    bool r1 = !r2 && dt < 0 && !fzero(dt);
-    mp_st(P + 27, p);
-    if (r2) mp_st(P + 18, p);
-    if (r1) mp_st(P + 9, p);
-    v3sel(v2, p.v, r2);
-    v3sel(v1, p.v, r1);
-    S.it++;
-    if (r1 || r2) {
-      sub3(va, v1, v0);
-      sub3(vb, v2, v0);
-      cross3(dir, va, vb);
-      normalize3(dir);
-    } else {
-      portal_dir_v(v1, v2, p.v, dir);
-      S.phase = dot3(dir, v1) >= 0 ? 4 : 3;
-      S.it = 0;
-    }
-    return 0;
-  }
-  // phases 3 and 4 share one path: 3 stops on separation, 4 on convergence
-  if (S.it > maxit) st.maxit++;
-  float dv4 = dot3(p.v, dir);
-  bool stop = fminf(dv4 - dot3(v1, dir), fminf(dv4 - dot3(v2, dir), dv4 - dot3(v3, dir))) <= tol || S.it > maxit;
-  if (S.phase == 3 && (stop || dv4 < 0)) return 1;
-  if (S.phase == 4 && stop) {
+  const int ph = S.phase;
+  const float dt = dot3(p.v, dir);  // (phases 3 and 4: dv4)
+  const bool behind = fzero(dt) || dt < 0;
+  if (ph >= 3 && S.it > maxit) st.maxit++;
+  const bool stop =
+      fminf(dt - dot3(v1, dir), fminf(dt - dot3(v2, dir), dt - dot3(v3, dir))) <= tol || S.it > maxit;
+  // exits: separated (phases -1..3) and converged penetration (phase 4)
+  if ((ph <= 1 && behind) || (ph == 2 && (S.it > 1000 || behind)) || (ph == 3 && (stop || dt < 0))) return 1;
+  if (ph == 4 && stop) {
     float cl[3];
     float d2 = tri_origin_dist2(v1, v2, v3, cl);
     depth = sqrtf(d2);
@@ -591,20 +521,85 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
     find_pos(Q0, Q1, Q2, Q3, pos);
     return 2;
   }
-  // expand the portal towards v4 = p (expand_portal)
+  // phase 2 (portal discovery): does p replace P2 (r2) or P1 (r1)?
+  float t[3];
+  cross3(t, v1, p.v);
+  float dd = dot3(t, v0);
+  const bool r2 = ph == 2 && dd < 0 && !fzero(dd);
+  cross3(t, p.v, v2);
+  dd = dot3(t, v0);
+  const bool r1 = ph == 2 && !r2 && dd < 0 && !fzero(dd);
+  // phases 3 / 4 (expand_portal): which vertex p replaces
   float v4v0[3];
   cross3(v4v0, p.v, v0);
-  bool c1 = dot3(v1, v4v0) > 0, c2 = dot3(v2, v4v0) > 0, c3 = dot3(v3, v4v0) > 0;
-  bool to1 = c1 ? c2 : !c3, to2 = !c1 && c3, to3 = c1 && !c2;
-  if (to1) mp_st(P + 9, p);
-  if (to2) mp_st(P + 18, p);
-  if (to3) mp_st(P + 27, p);
-  v3sel(v1, p.v, to1);
-  v3sel(v2, p.v, to2);
-  v3sel(v3, p.v, to3);
-  S.it++;
-  portal_dir_v(v1, v2, v3, dir);
-  if (S.phase == 3 && dot3(dir, v1) >= 0) { S.phase = 4; S.it = 0; }
+  const bool c1 = dot3(v1, v4v0) > 0, c2 = dot3(v2, v4v0) > 0, c3 = dot3(v3, v4v0) > 0;
+  const bool x1 = ph >= 3 && (c1 ? c2 : !c3), x2 = ph >= 3 && !c1 && c3, x3 = ph >= 3 && c1 && !c2;
+  // portal vertices after this step (registers; the LDS slots are written below)
+  v3sel(v1, p.v, r1 || x1);
+  v3sel(v2, p.v, r2 || x2);
+  v3sel(v3, p.v, x3);
+  // next direction: X = cross(a - c, b - c)
+  //   0: (v0, p, 0)   1: (v1, p, v0)   2: (v1', v2', v0) if p replaced P1/P2, else (v2, p, v1)
+  //   3/4: (v2', v3', v1')   -1: X = -v0
+  const bool rr = r1 || r2;
+  float a[3], b[3], cc[3];
+  for (int k = 0; k < 3; k++) {
+    a[k] = ph == 0 ? v0[k] : (ph == 1 || (ph == 2 && rr)) ? v1[k] : v2[k];
+    b[k] = ph >= 3 ? v3[k] : (ph == 2 && rr) ? v2[k] : p.v[k];
+    cc[k] = ph == 0 ? 0.f : (ph == 1 || ph == 2 && rr) ? v0[k] : v1[k];
+  }
+  float ea[3], eb[3];
+  sub3(ea, a, cc);
+  sub3(eb, b, cc);
+  float X[3];
+  cross3(X, ea, eb);
+  if (ph == -1) { X[0] = -v0[0]; X[1] = -v0[1]; X[2] = -v0[2]; }
+  if (ph == 0 && fzero(dot3(X, X))) {  // p on the line through the origin and v0
+    dir[0] = X[0]; dir[1] = X[1]; dir[2] = X[2];
+    if (fzero(p.v[0]) && fzero(p.v[1]) && fzero(p.v[2])) {
+      depth = 0;
+      normal[0] = 0; normal[1] = 0; normal[2] = 1;
+    } else {
+      depth = norm3(p.v);
+      for (int k = 0; k < 3; k++) normal[k] = p.v[k];
+      normalize3(normal);
+    }
+    for (int k = 0; k < 3; k++) pos[k] = 0.5f * (p.a[k] + p.b[k]);
+    return 2;
+  }
+  normalize3(X);
+  // phase 1: orient the portal so that the origin is on dir's side (swap P1, P2)
+  const bool swap = ph == 1 && dot3(X, v0) > 0;
+  if (swap) {
+    MPoint q;
+    mp_ld(P + 9, q);
+    mp_st(P + 18, q);
+    X[0] = -X[0]; X[1] = -X[1]; X[2] = -X[2];
+  }
+  dir[0] = X[0]; dir[1] = X[1]; dir[2] = X[2];
+  // the new support point's slot: 0 -> P1; 1 -> P2 (P1 on a swap); 2 -> P3 (and P1 or
+  // P2 when it replaces one); 3 / 4 -> the replaced vertex
+  const int slot = (ph == 0 || swap || x1) ? 1 : (ph == 1 || x2) ? 2 : 3;
+  if (ph >= 0) mp_st(P + 9 * slot, p);
+  if (rr) mp_st(P + (r2 ? 18 : 9), p);
+  // phase bookkeeping
+  if (ph == -1) {
+    S.phase = 0;
+  } else if (ph == 0) {
+    S.phase = 1;
+  } else if (ph == 1) {
+    S.phase = 2;
+    S.it = 0;
+  } else if (ph == 2) {
+    S.it++;
+    if (!rr) {
+      S.phase = dot3(dir, v1) >= 0 ? 4 : 3;
+      S.it = 0;
+    }
+  } else {
+    S.it++;
+    if (ph == 3 && dot3(dir, v1) >= 0) { S.phase = 4; S.it = 0; }
+  }
   return 0;
 }
 
