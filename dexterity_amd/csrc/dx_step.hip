@@ -19,6 +19,16 @@
 // parity-tested against) and DESIGN.md §3.
 #include "dx_device.h"
 
+// 16-byte write-through (sc1) store into a per-env block whose base is wave-uniform:
+// the substep queue hands these bytes to the env's next task without a release fence
+// (MI355X guide, Guideline 16 R1: sc1 payload, vmcnt(0), flag; the consumer acquires).
+typedef unsigned int dx_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_sc1_f4(void* base, int nbytes, int off, float4 v) {
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(base, 0, nbytes, 0x00020000);
+  dx_u32x4 d = {__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
+  __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, off, 0, 16);
+}
+
 // ------------------------------------------------------------------------ //
 // collision
 // ------------------------------------------------------------------------ //
@@ -1048,9 +1058,10 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
           if (r && c.sep && SL == 0) {
             // remember a separating direction (unless it is the cached one, still
             // separating: phase -1); forget it once the pair touches
+            const int so = 16 * (gp & (DX_SEP_SLOTS - 1));
             if (r == 1 && M.phase != -1)
-              c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1));
-            else if (cached) c.sep[gp & (DX_SEP_SLOTS - 1)] = make_float4(0.f, 0.f, 0.f, 0.f);
+              st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1)));
+            else if (cached) st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(0.f, 0.f, 0.f, 0.f));
           }
           if (r) {
             done = true;
@@ -2652,20 +2663,26 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
   if (LANE == 0) B.time[env] = time;
 }
 
-// The hand-off record (DevBatch::hand) of a task whose env has substeps left.
+// The hand-off record (DevBatch::hand) of a task whose env has substeps left: lane t
+// gathers words 4t .. 4t + 3 from LDS and writes them with one 16-byte sc1 store.
 template <class Ctx>
-__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, float time, unsigned cost) {
+__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int stride, float time, unsigned cost) {
   const float* qpos = c.f(c.L.qpos);
   const float* qvel = c.f(c.L.qvel);
   const float* ws = c.f(c.L.v5);
-  for (int i = LANE; i < c.nq; i += DX_WAVE) rec[i] = qpos[i];
-  for (int i = LANE; i < c.nv; i += DX_WAVE) {
-    rec[c.nq + i] = qvel[i];
-    rec[c.nq + c.nv + i] = ws[i];
-  }
-  if (LANE == 0) {
-    rec[c.nq + 2 * c.nv] = time;
-    rec[c.nq + 2 * c.nv + 1] = __uint_as_float(cost);
+  const int nw = c.nq + 2 * c.nv + 2;
+  time = rl(time, 0);  // euler advances time in lane 0 only
+  for (int t = LANE; 4 * t < nw; t += DX_WAVE) {
+    float w[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int m = 4 * t + u;
+      w[u] = m < c.nq ? qpos[m]
+           : m < c.nq + c.nv ? qvel[m - c.nq]
+           : m < c.nq + 2 * c.nv ? ws[m - c.nq - c.nv]
+           : m == c.nq + 2 * c.nv ? time : __uint_as_float(cost);
+    }
+    st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
   }
 }
 
@@ -2805,10 +2822,10 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
 // control step is 2-3x the mean (a whole control step per workgroup left most of
 // the second round's slots waiting on them).  Task (s, e) waits for (s - 1, e),
 // which was claimed earlier by a running workgroup, so the wait always ends; it is
-// bounded anyway (B.qerr records a timeout).  Hand-off: plain stores, vmcnt(0),
-// agent release, vmcnt(0), relaxed agent flag store; the consumer polls relaxed,
-// then agent acquire + vmcnt(0) before its plain loads (MI355X_MICROARCH.md,
-// inter-workgroup visibility).
+// bounded anyway (B.qerr records a timeout).  Hand-off (MI355X guide, Guideline 16
+// R1): the producer stores the handed-off bytes write-through (sc1), drains vmcnt and
+// stores the progress tag relaxed at agent scope (sc1); the consumer polls relaxed,
+// then one agent acquire + vmcnt(0) before its plain loads.
 __device__ __forceinline__ unsigned qtag(unsigned epoch, int s) { return epoch * 32u + (unsigned)s; }
 
 template <class SP>
@@ -2872,11 +2889,18 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       if (LANE == 0 && B.cost)
         B.cost[env] = cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
     } else {
-      env_store_hand(c, rec, time, cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull));
+      env_store_hand(c, rec, B.hand_stride, time,
+                     cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull));
     }
+    // publish: the bytes the env's next task reads (hand-off record, separating-
+    // direction cache) were stored write-through (sc1), so a drained vmcnt suffices
+    // and no release fence (a write-back of the whole XCD L2) is needed.  Profiling
+    // runs also carry stage_acc across tasks with plain stores: those keep the release.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (B.stage_acc) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     if (LANE == 0) __hip_atomic_store(B.progress + env, qtag(B.epoch, s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
