@@ -565,6 +565,41 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     }
     m->hf["dof_rec"] = dr;
   }
+  {
+    // Tree-sparse LDL^T of M (dx_device.h tree_solve): the elimination items (k, i, j)
+    // -- dof k, a proper ancestor i of k, j = i or an ancestor of i -- grouped by the
+    // height of k above the leaves (a level's dofs are never ancestors of one another),
+    // each level padded to whole 64-item slots; bit s of ldl_sync closes a level at
+    // slot s.  Deeper trees than DX_LDL_SLOTS slots keep the dense solver (nslot 0).
+    auto& par = m->hi["dof_parentid"];
+    std::vector<int> height(nv, 0);
+    for (int k = nv - 1; k >= 0; k--)
+      if (par[k] >= 0) height[par[k]] = std::max(height[par[k]], height[k] + 1);
+    int hmax = 0;
+    for (int k = 0; k < nv; k++) hmax = std::max(hmax, height[k]);
+    std::vector<int> tab;
+    unsigned sync = 0;
+    int nslot = 0;
+    for (int h = 0; h <= hmax; h++) {
+      std::vector<int> items;
+      for (int k = 0; k < nv; k++) {
+        if (height[k] != h) continue;
+        for (int i = par[k]; i >= 0; i = par[i])
+          for (int j = i; j >= 0; j = par[j]) items.push_back(k | (i << 8) | (j << 16));
+      }
+      if (items.empty()) continue;
+      const int ns = ((int)items.size() + DX_WAVE - 1) / DX_WAVE;
+      items.resize((size_t)ns * DX_WAVE, -1);
+      tab.insert(tab.end(), items.begin(), items.end());
+      nslot += ns;
+      if (nslot <= 32) sync |= 1u << (nslot - 1);
+    }
+    const char* dense = getenv("DX_DENSE_MSOLVE");  // A/B switch: the matrix-core Cholesky
+    if (nslot > DX_LDL_SLOTS || nv > DX_MAX_NV || (dense && dense[0] == '1')) { nslot = 0; sync = 0; tab.clear(); }
+    d.ldl_nslot = nslot;
+    d.ldl_sync = sync;
+    m->hi["ldl_tab"] = tab;
+  }
   // friction rows / limited joints / limited tendons
   std::vector<int> fric_dof, dof_fricrow(nv, -1), limj, limt;
   auto& floss = m->hf["dof_frictionloss"];
@@ -820,7 +855,7 @@ static int device_model(dx_model* m, int device, DevModel* out) {
   UF(geom_size); UF(geom_pos); UF(geom_mat); UF(geom_center); UF(geom_bsphere); UF(geom_bsphere_b); UF(geom_obb_b);
   UI(mesh_vertadr); UI(mesh_vertnum); UF(mesh_vert4);
   UI(mesh_binn); UI(mesh_bincap); UI(mesh_binadr); UF(mesh_bin4);
-  UF(geom_rec); UF(gpair_rec); UF(geom_crec); UF(bpair_rec); UF(body_rec); UF(dof_rec);
+  UF(geom_rec); UF(gpair_rec); UF(geom_crec); UF(bpair_rec); UF(body_rec); UF(dof_rec); UI(ldl_tab);
   UI(site_bodyid); UF(site_pos); UF(site_mat);
   UI(tendon_adr); UI(tendon_num); UI(wrap_dof); UI(wrap_qadr); UI(limt_ten);
   UF(tendon_range); UF(tendon_margin); UF(tendon_solref); UF(tendon_solimp); UF(tendon_invweight0);

@@ -938,3 +938,90 @@ __device__ __forceinline__ void chol_solve(const float* A, int n, DiagAdd dd, fl
 __device__ __forceinline__ void chol_solve(const float* A, int n, float* x, float* T) {
   chol_solve(A, n, DiagAdd{0.f, 0.f}, x, T);
 }
+
+// x <- (M + diag(dd))^-1 x for a matrix with the kinematic tree's sparsity (M, and
+// M + h·D in the Euler step): entry (i, j < i) is nonzero only when dof j is an
+// ancestor of dof i.  [3P] MuJoCo's mj_factorM / mj_solveM: M = L^T D L with L unit
+// lower, eliminated leaves first, which fills in nothing.
+// Factorisation: the dofs of one height level above the leaves are never ancestors of
+// one another, so a level is a set of independent items (k, i, j) -- A[i][j] -=
+// A[k][i] A[k][j] / A[k][k] for i a proper ancestor of k and j = i or an ancestor of
+// i -- spread over the lanes (DevModel::ldl_tab, loaded before the first barrier) and
+// summed into the shared ancestors with LDS float atomics.  The level's reads (rows k)
+// are never its targets.  Shadow hand + cube: 8 slots of 64 items in 6 levels,
+// against 16 rank-2 MFMA steps of the dense factorisation.
+// Substitutions, lane = dof, one readlane + one FMA per step (no writelanes): lane i
+// keeps u_i = y_i / D_i, so w = D^-1 L^-T y comes out of the k-descending chain over
+// the columns of L, and x = L^-1 w out of the ascending chain over its rows.
+// T: ti(n) words of LDS scratch (not aliasing A or x).
+template <class Ctx>
+__device__ __forceinline__ void tree_solve(const Ctx& c, const float* A, float dj, float* x, float* T) {
+  const DevModel& m = c.mdl();
+  const int n = c.nv;
+  const int ns = m.ldl_nslot;
+  const unsigned lvend = m.ldl_sync;
+  int item[DX_LDL_SLOTS];
+#pragma unroll
+  for (int s = 0; s < DX_LDL_SLOTS; s++) item[s] = s < ns ? m.ldl_tab[s * DX_WAVE + LANE] : -1;
+  for (int k = LANE; k < ti(n); k += DX_WAVE) T[k] = A[k];
+  SYNC();
+  if (LANE < n) T[ti(LANE) + LANE] += dj;
+  SYNC();
+#pragma unroll
+  for (int s = 0; s < DX_LDL_SLOTS; s++) {
+    if (s < ns) {
+      const int t = item[s];
+      if (t >= 0) {
+        const int k = t & 255, i = (t >> 8) & 255, j = t >> 16;
+        const float akk = T[ti(k) + k], aki = T[ti(k) + i], akj = T[ti(k) + j];
+        atomicAdd(T + ti(i) + j, -aki * (akj / akk));
+      }
+      if ((lvend >> s) & 1u) SYNC();
+    }
+  }
+  SYNC();
+  const int l = LANE;
+  const float dinv = l < n ? 1.0f / T[ti(l) + l] : 0.f;
+  // w = D^-1 L^-T b: lane i holds u_i = y_i / D_i; step k (descending) takes the final
+  // w_k = u_k, and L[k][i] z_k / D_i = (A[k][i] / D_k) (w_k D_k) / D_i = A[k][i] / D_i w_k
+  float u = l < n ? x[l] * dinv : 0.f;
+  for (int k1 = n - 1; k1 >= 0; k1 -= 8) {
+    float lc[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int k = k1 - q;
+      lc[q] = k >= 0 && l < k ? T[ti(k) + l] * dinv : 0.f;  // A[k][i] / D_i
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int k = max(k1 - q, 0);
+      if (k1 - q >= 0) u = fmaf(-lc[q], rl(u, k), u);
+    }
+  }
+  // x = L^-1 w: lane k holds v_k = w_k - sum_i A[k][i] / D_k x_i; step i (ascending)
+  // takes x_i = v_i
+  float v = u;
+  for (int i0 = 0; i0 < n; i0 += 8) {
+    float lr[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int i = i0 + q;
+      lr[q] = l > i && l < n ? T[ti(l) + i] * dinv : 0.f;  // A[k][i] / D_k
+    }
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+      const int i = min(i0 + q, 63);
+      if (i0 + q < n) v = fmaf(-lr[q], rl(v, i), v);
+    }
+  }
+  SYNC();
+  if (l < n) x[l] = v;
+  SYNC();
+}
+// M (+ diag) solve: the tree-sparse LDL^T when the model has its item table, else the
+// dense matrix-core Cholesky
+template <class Ctx>
+__device__ __forceinline__ void m_solve(const Ctx& c, const float* A, DiagAdd dd, float* x, float* T) {
+  if (c.mdl().ldl_nslot > 0) tree_solve(c, A, LANE < 32 ? dd.d1 : dd.d2, x, T);
+  else chol_solve(A, c.nv, dd, x, T);
+}

@@ -17,6 +17,7 @@
 #define DX_QUEUES 8         // substep queues: one per XCD (MI355X: 8 XCDs)
 #define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
+#define DX_LDL_SLOTS 16   // tree-sparse LDL^T items: at most 16 x 64 (dx_device.h tree_solve)
 #ifndef DX_NPG
 #define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
 #endif
@@ -71,6 +72,11 @@ struct DevModel {
   const DXG float4 *geom_crec, *bpair_rec;
   // tree records (dx_api.hip): body_rec [nbody][8] float4, dof_rec [nv][2] float4
   const DXG float4 *body_rec, *dof_rec;
+  // tree-sparse LDL^T of M (dx_api.hip): [ldl_nslot][64] items k | i << 8 | j << 16
+  // (-1: none) grouped by level, bit s of ldl_sync ends a level; nslot 0: dense solver
+  int ldl_nslot;
+  unsigned ldl_sync;
+  const DXG int* ldl_tab;
   // sites
   const DXG int* site_bodyid;
   const DXG float *site_pos, *site_mat;

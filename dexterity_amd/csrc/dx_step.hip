@@ -2193,7 +2193,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   const float* qs = c.f(c.L.qfrc_smooth);
   for (int i = LANE; i < nv; i += DX_WAVE) a0[i] = qs[i];
   SYNC();
-  chol_solve(M, nv, a0, H);
+  m_solve(c, M, DiagAdd{0.f, 0.f}, a0, H);
   stage_mark(c, ST_SMOOTH);
   collision(c, 0, -1, -1);
   make_constraint(c);
@@ -2228,7 +2228,7 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
     const float* M = c.f(c.L.M);
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = c.f(c.L.qfrc_smooth)[i] + c.f(c.L.qfrc_con)[i];
     SYNC();
-    chol_solve(M, nv, dd, acc, H);
+    m_solve(c, M, dd, acc, H);
   } else {
     for (int i = LANE; i < nv; i += DX_WAVE) acc[i] = qacc[i];
     SYNC();
