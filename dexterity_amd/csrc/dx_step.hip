@@ -403,6 +403,128 @@ __device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, con
   support_world(A, pa, dir, outA);
   support_world(B, pb, nd, outB);
 }
+#ifndef DX_SUPPORT_SPLIT
+#define DX_SUPPORT_SPLIT 1
+#endif
+// support_pair with the group split in halves: lanes 0-3 of a group scan A's hull block
+// along dir, lanes 4-7 B's along -dir, four slots each, and the halves swap their world
+// points at the end (DPP row_half_mirror: lane i <-> 7 - i).  Every lane then computes
+// one cube-map cell, one local direction, one reduction (over its quad: two DPP steps)
+// and one world transform instead of two of each.  Same arithmetic per vertex and the
+// same first-maximiser rule as support_pair, so the same points.
+constexpr int DX_SLH = 16 / (DX_NPG / 2);  // block slots per lane of a half group
+static_assert(DX_NPG == 8, "the split support pairs the two quads of an 8-lane group");
+__device__ __forceinline__ void support_pair_split(const Shape& A, const Shape& B, const float* dir, float* outA,
+                                                   float* outB) {
+  const bool hb = (SL & 4) != 0;  // this lane works on B
+  const int q = SL & 3;
+  const float sg = hb ? -1.f : 1.f;
+  const float d[3] = {sg * dir[0], sg * dir[1], sg * dir[2]};
+  float mat[9];
+#pragma unroll
+  for (int k = 0; k < 9; k++) mat[k] = hb ? B.mat[k] : A.mat[k];
+  float ld[3];
+  mattvec3(ld, mat, d);
+  const int type = hb ? B.type : A.type;
+  float lp[3];
+  if (__any(type == DXG_MESH)) {
+    Shape s;  // the fields the hull scan reads
+    s.type = type;
+    s.nvert = hb ? B.nvert : A.nvert;
+    s.bin_n = hb ? B.bin_n : A.bin_n;
+    s.vert4 = hb ? B.vert4 : A.vert4;
+    s.bin4 = hb ? B.bin4 : A.bin4;
+    const bool mesh = type == DXG_MESH;
+    HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
+    const DXG float4* blk = s.vert4;
+    int n1 = 0;
+    bool cell = false;
+    if (mesh) hull_block(s, ld, blk, n1, cell);
+    float4 v[DX_SLH];
+#pragma unroll
+    for (int u = 0; u < DX_SLH; u++) {
+      const int sl = 4 * u + q;
+      v[u] = blk[sl < n1 ? sl : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < DX_SLH; u++) {
+      const int sl = 4 * u + q;
+      const int idx = cell ? __float_as_int(v[u].w) : sl;
+      hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, mesh && sl < n1 && idx >= 0);
+    }
+    // overflow run: slot 15 of a cell (its quad's last lane, last load) may be a header
+    const DXG float4* ov = blk;
+    int nov = 0;
+    const bool hdr = mesh && cell && q == 3 && __float_as_int(v[DX_SLH - 1].w) == -2;
+    if (__any(hdr)) {
+      const int src = (LANE & ~3) | 3;
+      const int tag = __shfl(__float_as_int(v[DX_SLH - 1].w), src, 64);
+      const int off = __shfl(__float_as_int(v[DX_SLH - 1].x), src, 64);
+      const int cnt = __shfl(__float_as_int(v[DX_SLH - 1].y), src, 64);
+      if (mesh && cell && tag == -2) {
+        ov = s.bin4 + off;
+        nov = cnt - 15;
+      }
+    }
+    if (mesh && !cell && s.nvert > 16) {
+      ov = s.vert4 + 16;
+      nov = s.nvert - 16;
+    }
+    for (int base = 0; __any(base < nov); base += 16) {
+#pragma unroll
+      for (int u = 0; u < DX_SLH; u++) {
+        const int sl = base + 4 * u + q;
+        v[u] = ov[sl < nov ? sl : 0];
+      }
+#pragma unroll
+      for (int u = 0; u < DX_SLH; u++) {
+        const int sl = base + 4 * u + q;
+        const int idx = cell ? __float_as_int(v[u].w) : 16 + sl;
+        hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < nov && idx >= 0);
+      }
+    }
+    // quad reduction: the lowest vertex index among the maxima, coordinates from its lane
+    float vmax = fmaxf(h.d, dpp_f<0xB1, 0xF>(h.d));
+    vmax = fmaxf(vmax, dpp_f<0x4E, 0xF>(vmax));
+    int bi = h.d == vmax ? h.i : 0x7fffffff;
+    bi = min(bi, dpp_i<0xB1, 0xF>(bi));
+    bi = min(bi, dpp_i<0x4E, 0xF>(bi));
+    const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
+    const unsigned qb = (unsigned)(own >> (LANE & ~3)) & 15u;
+    const int src = (LANE & ~3) | (qb ? __builtin_ctz(qb) : 0);
+    const float hx = __shfl(h.x, src, 64), hy = __shfl(h.y, src, 64), hz = __shfl(h.z, src, 64);
+    if (mesh) { lp[0] = hx; lp[1] = hy; lp[2] = hz; }
+  }
+  if (type != DXG_MESH) {
+    Shape s;
+    s.type = type;
+    s.size[0] = hb ? B.size[0] : A.size[0];
+    s.size[1] = hb ? B.size[1] : A.size[1];
+    s.size[2] = hb ? B.size[2] : A.size[2];
+    support_prim(s, ld, lp);
+  }
+  // world point (+ the half margin along this half's direction), then the halves swap
+  float out[3];
+  matvec3(out, mat, lp);
+  out[0] += hb ? B.pos[0] : A.pos[0];
+  out[1] += hb ? B.pos[1] : A.pos[1];
+  out[2] += hb ? B.pos[2] : A.pos[2];
+  const float margin = hb ? B.margin : A.margin;
+  if (margin > 0) {
+    float n = norm3(d);
+    if (n > 1e-20f) {
+      float sc = margin / n;
+      out[0] += d[0] * sc; out[1] += d[1] * sc; out[2] += d[2] * sc;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float o = dpp_f<0x141, 0xF>(out[k]);  // row_half_mirror: the other half's point
+    outA[k] = hb ? o : out[k];
+    outB[k] = hb ? out[k] : o;
+  }
+}
+
 // Support of one shape along dir (group-cooperative for hulls).
 __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, float* out) {
   float ld[3], lp[3];
@@ -505,7 +627,11 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
   for (int k = 0; k < 3; k++) { v0[k] = P[k]; v1[k] = P[9 + k]; v2[k] = P[18 + k]; v3[k] = P[27 + k]; }
   MPoint p;
   float* dir = S.dir;
+#if DX_SUPPORT_SPLIT
+  support_pair_split(A, B, dir, p.a, p.b);
+#else
   support_pair(A, B, dir, p.a, p.b);
+#endif
   sub3(p.v, p.a, p.b);
   st.support++;
   const int ph = S.phase;
