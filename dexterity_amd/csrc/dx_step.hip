@@ -357,83 +357,27 @@ __device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)
   }
 }
 
-// Support points of A along dir and of B along -dir, by one lane group: both hulls'
-// blocks in the same round trip (four 16-B loads per lane), then the overflow runs of
-// either, 16 slots a pass, while any group of the wave has one left.
-__device__ __forceinline__ void support_pair(const Shape& A, const Shape& B, const float* dir, float* outA,
-                                             float* outB) {
-  float nd[3] = {-dir[0], -dir[1], -dir[2]};
-  float la[3], lb[3];
-  mattvec3(la, A.mat, dir);
-  mattvec3(lb, B.mat, nd);
-  const bool hA = A.type == DXG_MESH, hB = B.type == DXG_MESH;
-  HullScan SA, SB;
-  SA.h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
-  SB.h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
-  SA.nov = SB.nov = 0;
-  if (hA || hB) {
-    const DXG float4 *bA = A.vert4, *bB = B.vert4;
-    int nA = 0, nB = 0;
-    bool cA = false, cB = false;
-    if (hA) hull_block(A, la, bA, nA, cA);
-    if (hB) hull_block(B, lb, bB, nB, cB);
-    float4 va[DX_SLK], vb[DX_SLK];
-#pragma unroll
-    for (int u = 0; u < DX_SLK; u++) {
-      const int sl = u * DX_NPG + SL;
-      va[u] = bA[sl < nA ? sl : 0];
-      vb[u] = bB[sl < nB ? sl : 0];
-    }
-    if (hA) hull_take_block(A, la, va, bA, nA, cA, SA);
-    if (hB) hull_take_block(B, lb, vb, bB, nB, cB, SB);
-    for (int base = 0; __any(base < SA.nov || base < SB.nov); base += 16) {
-#pragma unroll
-      for (int u = 0; u < DX_SLK; u++) {
-        const int sl = base + u * DX_NPG + SL;
-        va[u] = SA.ov[sl < SA.nov ? sl : 0];
-        vb[u] = SB.ov[sl < SB.nov ? sl : 0];
-      }
-      if (base < SA.nov) hull_take_run(la, va, base, SA);
-      if (base < SB.nov) hull_take_run(lb, vb, base, SB);
-    }
-  }
-  float pa[3], pb[3];
-  if (hA) hull_reduce(SA.h, pa); else support_prim(A, la, pa);
-  if (hB) hull_reduce(SB.h, pb); else support_prim(B, lb, pb);
-  support_world(A, pa, dir, outA);
-  support_world(B, pb, nd, outB);
-}
-#ifndef DX_SUPPORT_SPLIT
-#define DX_SUPPORT_SPLIT 1
-#endif
-// support_pair with the group split in halves: lanes 0-3 of a group scan A's hull block
-// along dir, lanes 4-7 B's along -dir, four slots each, and the halves swap their world
-// points at the end (DPP row_half_mirror: lane i <-> 7 - i).  Every lane then computes
-// one cube-map cell, one local direction, one reduction (over its quad: two DPP steps)
-// and one world transform instead of two of each.  Same arithmetic per vertex and the
-// same first-maximiser rule as support_pair, so the same points.
+// Support points of A along dir and of B along -dir, by one lane group split in halves:
+// lanes 0-3 of a group hold A (the pair's first geom) in their Shape and scan its hull
+// block along dir, lanes 4-7 hold B and scan along -dir, four slots each; the halves swap
+// their world points at the end (DPP row_half_mirror: lane i <-> 7 - i).  Every lane
+// computes one cube-map cell, one local direction, one reduction (over its quad: two DPP
+// steps) and one world transform, and keeps one Shape.  The vertex arithmetic and the
+// first-maximiser rule are those of the oracle's serial scan.
 constexpr int DX_SLH = 16 / (DX_NPG / 2);  // block slots per lane of a half group
 static_assert(DX_NPG == 8, "the split support pairs the two quads of an 8-lane group");
-__device__ __forceinline__ void support_pair_split(const Shape& A, const Shape& B, const float* dir, float* outA,
-                                                   float* outB) {
-  const bool hb = (SL & 4) != 0;  // this lane works on B
+__device__ __forceinline__ bool half_b() { return (SL & 4) != 0; }  // this lane holds B
+__device__ __forceinline__ void support_pair(const Shape& S, const float* dir, float* outA, float* outB) {
+  const bool hb = half_b();
   const int q = SL & 3;
   const float sg = hb ? -1.f : 1.f;
   const float d[3] = {sg * dir[0], sg * dir[1], sg * dir[2]};
-  float mat[9];
-#pragma unroll
-  for (int k = 0; k < 9; k++) mat[k] = hb ? B.mat[k] : A.mat[k];
   float ld[3];
-  mattvec3(ld, mat, d);
-  const int type = hb ? B.type : A.type;
+  mattvec3(ld, S.mat, d);
+  const int type = S.type;
   float lp[3];
   if (__any(type == DXG_MESH)) {
-    Shape s;  // the fields the hull scan reads
-    s.type = type;
-    s.nvert = hb ? B.nvert : A.nvert;
-    s.bin_n = hb ? B.bin_n : A.bin_n;
-    s.vert4 = hb ? B.vert4 : A.vert4;
-    s.bin4 = hb ? B.bin4 : A.bin4;
+    const Shape& s = S;
     const bool mesh = type == DXG_MESH;
     HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
     const DXG float4* blk = s.vert4;
@@ -495,28 +439,10 @@ __device__ __forceinline__ void support_pair_split(const Shape& A, const Shape& 
     const float hx = __shfl(h.x, src, 64), hy = __shfl(h.y, src, 64), hz = __shfl(h.z, src, 64);
     if (mesh) { lp[0] = hx; lp[1] = hy; lp[2] = hz; }
   }
-  if (type != DXG_MESH) {
-    Shape s;
-    s.type = type;
-    s.size[0] = hb ? B.size[0] : A.size[0];
-    s.size[1] = hb ? B.size[1] : A.size[1];
-    s.size[2] = hb ? B.size[2] : A.size[2];
-    support_prim(s, ld, lp);
-  }
+  if (type != DXG_MESH) support_prim(S, ld, lp);
   // world point (+ the half margin along this half's direction), then the halves swap
   float out[3];
-  matvec3(out, mat, lp);
-  out[0] += hb ? B.pos[0] : A.pos[0];
-  out[1] += hb ? B.pos[1] : A.pos[1];
-  out[2] += hb ? B.pos[2] : A.pos[2];
-  const float margin = hb ? B.margin : A.margin;
-  if (margin > 0) {
-    float n = norm3(d);
-    if (n > 1e-20f) {
-      float sc = margin / n;
-      out[0] += d[0] * sc; out[1] += d[1] * sc; out[2] += d[2] * sc;
-    }
-  }
+  support_world(S, lp, d, out);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const float o = dpp_f<0x141, 0xF>(out[k]);  // row_half_mirror: the other half's point
@@ -596,10 +522,15 @@ struct MprState {
 // cached: a separating direction of this pair from an earlier collision pass (world
 // frame), tried first (phase -1): if the supports along it do not reach the origin the
 // pair is separated -- the verdict MPR's own tests give -- in one support pass.
-__device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprState& S, const float* cached) {
+__device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const float* cached) {
   MPoint P0;
-  sub3(P0.v, A.center, B.center);
-  for (int k = 0; k < 3; k++) { P0.a[k] = A.center[k]; P0.b[k] = B.center[k]; }
+  const bool hb = half_b();
+  for (int k = 0; k < 3; k++) {
+    const float o = dpp_f<0x141, 0xF>(G.center[k]);  // the other half's shape centre
+    P0.a[k] = hb ? o : G.center[k];
+    P0.b[k] = hb ? G.center[k] : o;
+  }
+  sub3(P0.v, P0.a, P0.b);
   if (fzero(P0.v[0]) && fzero(P0.v[1]) && fzero(P0.v[2])) P0.v[0] += 1e-9f;
   mp_st(S.P, P0);
   S.dir[0] = -P0.v[0]; S.dir[1] = -P0.v[1]; S.dir[2] = -P0.v[2];
@@ -618,7 +549,7 @@ __device__ __forceinline__ void mpr_init(const Shape& A, const Shape& B, MprStat
 // portal slot chosen per group.  Each phase performs exactly the arithmetic of libccd's
 // structure (the oracle's dxo_mpr), so the results are unchanged; only the separated,
 // degenerate and final exits branch.
-__device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState& S, float& depth, float* normal,
+__device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& depth, float* normal,
                                         float* pos, NpStats& st) {
   const float tol = 1e-6f;
   const int maxit = 50;
@@ -627,11 +558,7 @@ __device__ __forceinline__ int mpr_step(const Shape& A, const Shape& B, MprState
   for (int k = 0; k < 3; k++) { v0[k] = P[k]; v1[k] = P[9 + k]; v2[k] = P[18 + k]; v3[k] = P[27 + k]; }
   MPoint p;
   float* dir = S.dir;
-#if DX_SUPPORT_SPLIT
-  support_pair_split(A, B, dir, p.a, p.b);
-#else
-  support_pair(A, B, dir, p.a, p.b);
-#endif
+  support_pair(G, dir, p.a, p.b);
   sub3(p.v, p.a, p.b);
   st.support++;
   const int ph = S.phase;
@@ -1144,7 +1071,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     bool fresh = true;
     int gp = 0;
     float margin = 0;
-    Shape A, B;
+    Shape G;  // the pair's first geom on lanes 0-3 of the group, its second on lanes 4-7
     MprState M;
     bool cached = false;
     M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
@@ -1168,19 +1095,18 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
           } else {
             st.mpr++;
             margin = pr.z;
-            make_shape_rec(c, __float_as_int(pr.x), 0.5f * margin, A);
-            make_shape_rec(c, __float_as_int(pr.y), 0.5f * margin, B);
+            make_shape_rec(c, __float_as_int(half_b() ? pr.y : pr.x), 0.5f * margin, G);
             float4 ce = c.sep ? c.sep[gp & (DX_SEP_SLOTS - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
             cached = __float_as_int(ce.w) == gp + 1;
             const float cd[3] = {ce.x, ce.y, ce.z};
-            mpr_init(A, B, M, cached ? cd : nullptr);
+            mpr_init(G, M, cached ? cd : nullptr);
             fresh = false;
             stepping = true;
           }
         }
         if (stepping) {
           float depth, nrm[3], pos[3];
-          int r = mpr_step(A, B, M, depth, nrm, pos, st);
+          int r = mpr_step(G, M, depth, nrm, pos, st);
           if (r && c.sep && SL == 0) {
             // remember a separating direction (unless it is the cached one, still
             // separating: phase -1); forget it once the pair touches
