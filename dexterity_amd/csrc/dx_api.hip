@@ -975,6 +975,11 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
     b->slots = ncu * 8;  // resident 64-lane workgroups of the step kernel (2 waves per SIMD)
+    // occupancy experiment: DX_LDS_PAD bytes of extra LDS per workgroup (fewer resident)
+    if (const char* pad = getenv("DX_LDS_PAD")) {
+      const long per = (long)m->lds.total * 4 + atol(pad);
+      b->slots = ncu * (int)std::max(1L, std::min(8L, 163840L / per));
+    }
   }
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
@@ -1138,6 +1143,7 @@ static void timing_end(dx_batch* b, hipEvent_t start);
 static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
+  if (const char* pad = getenv("DX_LDS_PAD")) lds += (size_t)atol(pad);  // occupancy experiment
   const bool queued = mode == 0 && b->queue && nsub < 32;
   const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots) : b->nenv;
   if (queued) {
