@@ -658,10 +658,19 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.qacc_smooth = take(nv); L.qfrc_smooth = take(nv); L.qfrc_con = take(nv);
   L.v1 = take(nv); L.v2 = take(nv); L.v3 = take(nv); L.v4 = take(nv); L.v5 = take(nv);
   L.M = take(ntri);
-  L.ten_len = take(std::max(d.ntendon, 1)); L.act_len = take(std::max(d.nu, 1));
-  L.act_force = take(std::max(d.nu, 1));
+  L.ten_len = take(std::max(d.ntendon, 1));  // read by the tendon-limit rows: persistent
   L.con = take(DX_NCON_MAX * DX_CON_STRIDE);
-  L.nefc_max = d.nfric + 2 * d.nlimj + 2 * d.nlimt + 4 * DX_NCON_MAX;
+  // limit rows: a joint / tendon whose range is wider than twice its margin can have only
+  // one side within the margin at a time (q - lo < margin and hi - q < margin need
+  // hi - lo < 2 margin), so it holds one row, else two
+  int nlimrow = 0;
+  {
+    auto& jr = m->hf["jnt_range"]; auto& jm = m->hf["jnt_margin"];
+    for (int j : limj) nlimrow += (jr[2 * j + 1] - jr[2 * j]) > 2.0f * jm[j] + 1e-4f ? 1 : 2;
+    auto& tr = m->hf["tendon_range"]; auto& tm = m->hf["tendon_margin"];
+    for (int t : limt) nlimrow += (tr[2 * t + 1] - tr[2 * t]) > 2.0f * tm[t] + 1e-4f ? 1 : 2;
+  }
+  L.nefc_max = d.nfric + nlimrow + 4 * DX_NCON_MAX;
   L.efc_fl = take(std::max(d.nfric, 1)); L.efc_Rf = take(std::max(d.nfric, 1));
   L.tri = 0;  // (was the wave Cholesky's index table; n > 32 now factors on the matrix cores)
   const int U0 = off;
@@ -671,6 +680,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.cinert = take(10 * nb); L.cvel = take(6 * nb); L.cdof_dot = take(6 * nv); L.scr = take(12 * nb);
   L.xanchor = take(3 * std::max(d.njnt, 1)); L.xaxis = take(3 * std::max(d.njnt, 1));
   L.xquat = take(4 * nb);
+  // actuator lengths: tendon_lengths -> the velocity stage's actuator forces
+  L.act_len = take(std::max(d.nu, 1));
+  L.act_force = L.act_len;  // (no longer stored)
   int end = off;
   L.tsm = B0;
   end = std::max(end, B0 + r4(ntri));
@@ -681,13 +693,20 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, L.cand + L.cand_max + DX_NGRP * 36 + 4 * (L.cand_max - 2 * (L.cand_max / 3)));
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
-  L.efc_jar = take(L.nefc_max); L.efc_jv = take(L.nefc_max);
+  L.efc_jar = take(L.nefc_max);
   L.cj_idx = take((DX_NCON_MAX * DX_DOFMAX + 3) / 4);  // uint8 dof ids
   L.cj_val = take(DX_NCON_MAX * 3 * DX_DOFMAX);
+  // contact-frame scratch: J x in jac_vec, the frame forces in jac_t_force (and the
+  // sensor stash right after the last one); never live at the same time
   L.cq = take(3 * DX_NCON_MAX);
-  L.cw = take(3 * DX_NCON_MAX);
-  // CG's M^-1 grad: the dead kinematic block past the Newton Hessian when it has room
-  if (U0 + r4(ntri) + r4(nv) <= B0) L.cgv = U0 + r4(ntri);
+  L.cw = L.cq;
+  // The solver's J dir (efc_jv) and CG's M^-1 grad: written only from the solve on, when
+  // the kinematic block is dead, so they go past the Newton Hessian when it has room
+  int spare = U0 + r4(ntri);
+  if (spare + r4(L.nefc_max) <= B0) { L.efc_jv = spare; spare += r4(L.nefc_max); }
+  else L.efc_jv = take(L.nefc_max);
+  if (d.solver != 1) L.cgv = 0;  // Newton: no CG scratch
+  else if (spare + r4(nv) <= B0) L.cgv = spare;
   else L.cgv = take(nv);
   end = std::max(end, off);
   L.H = U0;
@@ -974,12 +993,13 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
-    b->slots = ncu * 8;  // resident 64-lane workgroups of the step kernel (2 waves per SIMD)
-    // occupancy experiment: DX_LDS_PAD bytes of extra LDS per workgroup (fewer resident)
-    if (const char* pad = getenv("DX_LDS_PAD")) {
-      const long per = (long)m->lds.total * 4 + atol(pad);
-      b->slots = ncu * (int)std::max(1L, std::min(8L, 163840L / per));
-    }
+    // resident 64-lane workgroups of the step kernel per CU (LDS and VGPR limits; 8 when
+    // the runtime cannot say), plus the occupancy experiment DX_LDS_PAD (extra LDS bytes)
+    const char* pad = getenv("DX_LDS_PAD");
+    const size_t lds = (size_t)m->lds.total * 4 + (pad ? (size_t)atol(pad) : 0);
+    int per = dx_step_occupancy(b->spec, lds);
+    if (per < 1) per = (int)std::max<size_t>(1, std::min<size_t>(8, 163840 / lds));
+    b->slots = ncu * per;
   }
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
@@ -1366,6 +1386,11 @@ extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nf
     HIPCHK(hipSetDevice(b->device));
     HIPCHK(hipMemcpyAsync(dst, B.qerr, 4, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
+    return 0;
+  }
+  if (std::string(name) == "queue_slots") {  // int32 bits: the queued launch's persistent workgroups
+    if (nfloats < 1) return fail(DX_EINVAL, "destination too small");
+    memcpy(dst, &b->slots, 4);
     return 0;
   }
   if (!b->debug) return fail(DX_EINVAL, "debug not enabled");

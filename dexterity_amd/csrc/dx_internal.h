@@ -9,7 +9,7 @@
 
 #define DX_WAVE 64
 #define DX_NCON_MAX 32    // contacts kept per env per substep (MuJoCo pool: nconmax)
-#define DX_DOFMAX 16      // max dofs in a contact Jacobian (|chain(b1) xor chain(b2)|)
+#define DX_DOFMAX 14      // max dofs in a contact Jacobian (|chain(b1) xor chain(b2)|; checked at load)
 #define DX_CON_STRIDE 20  // words per contact record in LDS:
 // 0-2 pos, 3-11 frame (normal, tangents), 12 dist, 13 geom pair, 14 nnz | nrows << 8
 // (key while sorting), 15 first efc row, 16-17 friction (mu1, mu2), 18-19 dof support mask
@@ -265,6 +265,7 @@ __device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, i
 
 // dx_step.hip: specialized-kernel lookup and launch (host side)
 int dx_spec_find(const DevModel& d, const Lds& L);
+int dx_step_occupancy(int spec, size_t lds);
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);

@@ -2971,8 +2971,11 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
 #define DX_SPECS(X)
 #endif
 
+#ifndef DX_STEP_WAVES
+#define DX_STEP_WAVES 2  // waves per SIMD the VGPR budget is set for (3: <= 168 VGPRs, measured slower)
+#endif
 template <class SP>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DX_STEP_WAVES)))
 dx_step_kernel_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   if (mode == 3) step_queue<SP>(m, B, L, nsub);
@@ -2998,12 +3001,18 @@ static bool spec_matches(const DevModel& d, const Lds& L) {
 
 #define DX_SPEC_FNS(SP)                                                                               \
   bool dx_match_##SP(const DevModel& d, const Lds& L);                                                \
+  int dx_occ_##SP(size_t lds);                                                                        \
   hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
                             const Lds& L, int nsub, int mode);
 
 #ifdef DX_SPEC_ONLY
 #define DX_SPEC_DEFINE(SP)                                                                            \
   bool dx_match_##SP(const DevModel& d, const Lds& L) { return spec_matches<SP>(d, L); }             \
+  int dx_occ_##SP(size_t lds) {                                                                       \
+    int n = 0;                                                                                        \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dx_step_kernel_spec<SP>, 64, lds) != hipSuccess) n = 0; \
+    return n;                                                                                         \
+  }                                                                                                   \
   hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
                             const Lds& L, int nsub, int mode) {                                       \
     if (mode == 2)                                                                                    \
@@ -3019,7 +3028,7 @@ DX_SPECS(DX_SPEC_FNS)
 
 // The model struct is read through a device pointer (dx_api.hip device_model) in
 // the constant address space rather than passed by value in the kernarg segment.
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DX_STEP_WAVES)))
 dx_step_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   if (mode == 3) step_queue<SpecRT>(m, B, L, nsub);
@@ -3029,6 +3038,19 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 dx_prep_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L) {
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
   step_body<SpecRT>(m, B, L, 1, 2, true);
+}
+
+// Resident step-kernel workgroups per CU at `lds` bytes of LDS each (0: unknown), for
+// the persistent grid of the substep queue.
+int dx_step_occupancy(int spec, size_t lds) {
+  int k = 0;
+#define DX_OCC(SP) if (spec == k) return dx_occ_##SP(lds); k++;
+  DX_SPECS(DX_OCC)
+#undef DX_OCC
+  (void)k;
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dx_step_kernel, 64, lds) != hipSuccess) n = 0;
+  return n;
 }
 
 // Index of the specialization whose layout and dimensions equal the model's, or -1.

@@ -160,7 +160,7 @@ class BatchedPhysics:
             "contact": (self.nenv, self.model.ncon_max, 16),
             "efc_count": (self.nenv, 2),
         }
-        if name == "queue_timeouts":
+        if name in ("queue_timeouts", "queue_slots"):
             out = np.zeros(1, dtype=np.int32)
             _lib.check(_lib.load().dx_debug_get(self.ptr, name.encode(), out.ctypes.data, 1))
             return out
