@@ -169,8 +169,9 @@ def main():
     L = _lib.load()
     comm = distributed.Comm.from_env(device=local) if world > 1 else None
     B = args.envs_per_gpu
-    env = manipulation.load("reorient", "state_dense", seed=distributed.rank_seed(12345, rank), num_envs=B,
-                            device=local)
+    # rank r steps envs [env0, env0 + B) of the job; env i draws from seed 12345 + i
+    env0, _ = distributed.env_shard(world * B, rank, world)
+    env = manipulation.load("reorient", "state_dense", seed=12345, num_envs=B, device=local, env_offset=env0)
     collator = distributed.OutputCollator(env, comm) if comm else None
 
     def one_step(i):

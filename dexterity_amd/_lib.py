@@ -16,8 +16,11 @@ LIB_PATH = os.environ.get("DX_LIB") or os.path.join(_HERE, "libdx.so")  # DX_LIB
 # dx_field
 QPOS, QVEL, CTRL, QACC_WARMSTART, QACC, TIME = 0, 1, 2, 3, 4, 5
 SITE_XPOS, SITE_VEL, XPOS, XQUAT, NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST = 6, 7, 8, 9, 10, 11, 12, 13, 14
-SENSOR_TORQUE = 15
-INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST)
+SENSOR_TORQUE, DIVERGED = 15, 16
+INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST, DIVERGED)
+HEALTH_WORDS, NCON_HIST = 16, 65
+HEALTH = ("contact_overflow", "candidate_overflow", "jacobian_dof_overflow", "row_overflow", "diverged",
+          "ncon_max")
 
 EXPORTS = (
     "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_model_lds_bytes", "dx_field_width",
@@ -32,7 +35,8 @@ EXPORTS = (
     "dx_jac_site", "dx_ik_solve",
     "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
-    "dx_env_set_time_limit", "dx_set_outputs",
+    "dx_env_set_time_limit", "dx_set_outputs", "dx_env_create_shard",
+    "dx_health", "dx_health_clear", "dx_ncon_histogram",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -111,6 +115,11 @@ def load(path: str = LIB_PATH):
     L.dx_abi_version.restype = ctypes.c_int
     L.dx_env_create.restype = vp
     L.dx_env_create.argtypes = [vp, i32, i32, i32, ctypes.c_uint64, vp, i32]
+    L.dx_health.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), i32]
+    L.dx_health_clear.argtypes = [vp]
+    L.dx_ncon_histogram.argtypes = [vp, ctypes.c_int]
+    L.dx_env_create_shard.restype = vp
+    L.dx_env_create_shard.argtypes = [vp, i32, i32, i32, ctypes.c_uint64, ctypes.c_int64, vp, i32]
     L.dx_env_destroy.argtypes = [vp]
     L.dx_env_batch.restype = vp
     L.dx_env_batch.argtypes = [vp]

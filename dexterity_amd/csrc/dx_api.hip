@@ -824,7 +824,8 @@ extern "C" int dx_field_width(const dx_model* m, int field) {
     case DX_QPOS: return d.nq;
     case DX_QVEL: case DX_QACC_WARMSTART: case DX_QACC: return d.nv;
     case DX_CTRL: return d.nu;
-    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: case DX_NCAND: case DX_STEP_COST: return 1;
+    case DX_TIME: case DX_NCON: case DX_GROUND_CONTACT: case DX_NITER: case DX_NCAND: case DX_STEP_COST:
+    case DX_DIVERGED: return 1;
     case DX_SITE_XPOS: return 3 * d.nsite;
     case DX_SITE_VEL: return 6 * d.nsite;
     case DX_XPOS: return 3 * d.nbody;
@@ -920,6 +921,7 @@ struct dx_batch {
   bool debug;
   float* sensor = nullptr;  // DX_SENSOR_TORQUE [nenv][nbody][3] (allocated by dx_sensor_enable)
   float* sen_stash = nullptr;
+  unsigned* ncon_hist = nullptr;  // dx_ncon_histogram
 };
 
 static int balloc(dx_batch* b, void** p, size_t bytes) {
@@ -973,6 +975,8 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.niter, E * 4);
   rc |= balloc(b, (void**)&B.ncand, E * 4);
   rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
+  rc |= balloc(b, (void**)&B.health, DX_HEALTH_WORDS * 4);
+  rc |= balloc(b, (void**)&B.bad, E * 4);
   if (!getenv("DX_NO_LPT_ORDER")) {
     void* po = nullptr;
     rc |= balloc(b, (void**)&B.cost, E * 4);
@@ -1054,6 +1058,7 @@ static void* field_base(dx_batch* b, int field) {
     case DX_NCAND: return B.ncand;
     case DX_STEP_COST: return B.cost;
     case DX_SENSOR_TORQUE: return b->sensor;
+    case DX_DIVERGED: return B.bad;
   }
   return nullptr;
 }
@@ -1189,14 +1194,54 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   return 0;
 }
 
+// DX_DIVERGED of a physics-level call reports that call only (a dx_env's task kernel
+// consumes and clears the flags itself)
+static int clear_bad(dx_batch* b) {
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemsetAsync(b->db.bad, 0, (size_t)b->nenv * 4, b->stream));
+  return 0;
+}
+
 extern "C" int dx_step(dx_batch* b, int32_t nsubstep) {
   if (!b || nsubstep < 1) return fail(DX_EINVAL, "bad batch or nsubstep");
+  if (int rc = clear_bad(b)) return rc;
   return launch_step(b, nsubstep, 0);
 }
 
 extern "C" int dx_forward(dx_batch* b) {
   if (!b) return fail(DX_EINVAL, "null batch");
+  if (int rc = clear_bad(b)) return rc;
   return launch_step(b, 1, 1);
+}
+
+extern "C" int dx_health(dx_batch* b, uint32_t* out, int32_t n) {
+  if (!b || !out || n < 0) return fail(DX_EINVAL, "null batch or output");
+  HIPCHK(hipSetDevice(b->device));
+  uint32_t h[DX_HEALTH_WORDS + DX_NCON_HIST];
+  memset(h, 0, sizeof(h));
+  HIPCHK(hipMemcpyAsync(h, b->db.health, DX_HEALTH_WORDS * 4, hipMemcpyDeviceToHost, b->stream));
+  if (b->db.ncon_hist)
+    HIPCHK(hipMemcpyAsync(h + DX_HEALTH_WORDS, b->db.ncon_hist, DX_NCON_HIST * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
+  memcpy(out, h, std::min<size_t>(n, DX_HEALTH_WORDS + DX_NCON_HIST) * 4);
+  return queue_check(b);
+}
+
+extern "C" int dx_health_clear(dx_batch* b) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  HIPCHK(hipSetDevice(b->device));
+  HIPCHK(hipMemsetAsync(b->db.health, 0, DX_HEALTH_WORDS * 4, b->stream));
+  if (b->db.ncon_hist) HIPCHK(hipMemsetAsync(b->db.ncon_hist, 0, DX_NCON_HIST * 4, b->stream));
+  return 0;
+}
+
+extern "C" int dx_ncon_histogram(dx_batch* b, int enable) {
+  if (!b) return fail(DX_EINVAL, "null batch");
+  if (enable && !b->ncon_hist) {
+    if (int rc = balloc(b, (void**)&b->ncon_hist, DX_NCON_HIST * 4)) return rc;
+  }
+  b->db.ncon_hist = enable ? b->ncon_hist : nullptr;
+  return 0;
 }
 
 // ------------------------------------------------------------------------ //
@@ -1388,6 +1433,9 @@ extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nf
     HIPCHK(hipStreamSynchronize(b->stream));
     return 0;
   }
+  if (std::string(name) == "health") {  // uint32 bits: dx_health's counters (+ histogram)
+    return dx_health(b, (uint32_t*)dst, (int32_t)std::min<size_t>(nfloats, DX_HEALTH_WORDS + DX_NCON_HIST));
+  }
   if (std::string(name) == "queue_slots") {  // int32 bits: the queued launch's persistent workgroups
     if (nfloats < 1) return fail(DX_EINVAL, "destination too small");
     memcpy(dst, &b->slots, 4);
@@ -1430,6 +1478,12 @@ struct dx_env {
 
 extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task,
                                  uint64_t seed, const float* params, int32_t nparams) {
+  return dx_env_create_shard(m, nenv, device, task, seed, 0, params, nparams);
+}
+
+extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t device, int32_t task,
+                                       uint64_t seed, int64_t env0, const float* params, int32_t nparams) {
+  if (env0 < 0 || env0 + (int64_t)nenv > 0x7fffffffll) { fail(DX_EINVAL, "env0 out of range"); return nullptr; }
   if (task != DX_TASK_REORIENT && task != DX_TASK_REACH) { fail(DX_EINVAL, "unknown task kind"); return nullptr; }
   if (!m) { fail(DX_EINVAL, "null model"); return nullptr; }
   const int nq = m->dm.nq, nu = m->dm.nu;
@@ -1448,6 +1502,7 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   P.kind = task == DX_TASK_REACH ? DX_KIND_REACH : DX_KIND_REORIENT;
   P.nenv = nenv; P.nq = d.nq; P.nv = d.nv; P.nu = d.nu; P.nsite = d.nsite;
   P.seed = seed;
+  P.env0 = (int)env0;
   e->nsub = (int)params[0];
   P.hand_nq = (int)params[1]; P.hand_nv = (int)params[2];
   int watch_geom = -1, watch_body = -1;
@@ -1517,7 +1572,7 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
     rc |= al((void**)&S.mt_env, E * DX_MT_WORDS * 4);
     rc |= al((void**)&S.mt_goal, E * DX_MT_WORDS * 4);
     if (!rc) {
-      hipLaunchKernelGGL(dx_mt_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv, seed, S.mt_env,
+      hipLaunchKernelGGL(dx_mt_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv, seed + (uint64_t)env0, S.mt_env,
                          S.mt_goal);
       if (hipGetLastError() != hipSuccess) rc = fail(DX_EHIP, "MT19937 seeding kernel launch failed");
     }
@@ -1534,12 +1589,15 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
       P.tdata_f64 = 1;
       rc |= al((void**)&S.mt_reach, E * DX_MTW_WORDS * 4);
       if (!rc) {
-        hipLaunchKernelGGL(dx_mtw_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv, seed,
-                           S.mt_reach);
+        hipLaunchKernelGGL(dx_mtw_seed_kernel, dim3((nenv + 63) / 64), dim3(64), 0, b->stream, nenv,
+                           seed + (uint64_t)env0, S.mt_reach);
         if (hipGetLastError() != hipSuccess) rc = fail(DX_EHIP, "MT19937 seeding kernel launch failed");
       }
     }
     rc |= al((void**)&tdata, nt * 4);
+    // balloc zeroes on the batch's (non-blocking) stream: drain it before the
+    // synchronous copies below, or a late memset can wipe what they wrote
+    if (!rc && hipStreamSynchronize(b->stream) != hipSuccess) rc = fail(DX_EHIP, "stream sync failed");
     if (!rc && hipMemcpy(tdata, params + DX_REACH_NPARAMS_HEAD, nt * 4, hipMemcpyHostToDevice) != hipSuccess)
       rc = fail(DX_EHIP, "hipMemcpy failed");
     P.tdata = tdata;
@@ -1547,6 +1605,7 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
   if (!rc) rc |= al((void**)&dP, sizeof(TaskParams));
   if (!rc) rc |= al((void**)&dS, sizeof(TaskState));
   std::vector<int> neg(E, -1);
+  if (!rc && hipStreamSynchronize(b->stream) != hipSuccess) rc = fail(DX_EHIP, "stream sync failed");
   if (!rc && (hipMemcpy(S.episode, neg.data(), E * 4, hipMemcpyHostToDevice) != hipSuccess ||
               hipMemcpy(dP, &P, sizeof(P), hipMemcpyHostToDevice) != hipSuccess ||
               hipMemcpy(dS, &S, sizeof(S), hipMemcpyHostToDevice) != hipSuccess))
@@ -1629,7 +1688,7 @@ extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
 }
 
 extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
-                                                    int step, float* out);
+                                                    int step, int env0, float* out);
 
 extern "C" int dx_env_action_buffer(dx_env* e, void** devptr) {
   if (!e || !devptr) return fail(DX_EINVAL, "null argument");
@@ -1650,7 +1709,7 @@ extern "C" int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step) {
   HIPCHK(hipSetDevice(b->device));
   int n = e->P.nenv * e->P.nu;
   hipLaunchKernelGGL(dx_sample_actions_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
-                     e->P.nu, b->dm.actuator_ctrlrange, seed, step, (float*)buf);
+                     e->P.nu, b->dm.actuator_ctrlrange, seed, step, e->P.env0, (float*)buf);
   HIPCHK(hipGetLastError());
   return 0;
 }

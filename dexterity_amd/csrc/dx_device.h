@@ -263,7 +263,9 @@ __device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
   if (c.stage_acc && LANE == 0) c.stage_acc[k] += n;
 }
 // misc int slots
-enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NINT };
+// I_OVF: capacity bits of the substep (1 candidates, 2 contacts, 4 Jacobian dofs, 8 rows);
+// I_NRAW: most contacts any collision pass of the substep found (before the DX_NCON_MAX cap)
+enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NRAW, I_NINT };
 
 // ------------------------------------------------------------------------ //
 // position stage

@@ -134,7 +134,17 @@ struct DevBatch {
   // torque sensors (dx_sensor.hip): the last substep's pre-integration state, solved
   // qacc and contact forces, [nenv][dx_sensor_stash_words]; null when the field is off
   float* sen_stash;
+  // always-on health counters ([DX_HEALTH_WORDS], include/dx.h dx_health), the optional
+  // histogram of contacts found per env-substep ([DX_NCON_HIST], null: off) and the
+  // per-env divergence flag (set when a substep produced a non-finite or runaway state
+  // and the env was reset, MuJoCo's BADQACC; cleared by the task post kernel)
+  unsigned* health;
+  unsigned* ncon_hist;
+  int* bad;
 };
+#define DX_HEALTH_WORDS 16
+#define DX_NCON_HIST 65   // bins 0..63, and >= 64
+#define DX_MAXVAL 1e10f   // mjMAXVAL: |qacc| beyond this is a diverged state (mj_checkAcc)
 #define DX_NSTAGE 40
 
 // Offsets (in 4-byte words) of every per-env LDS array.
@@ -177,6 +187,8 @@ struct TaskParams {
                             // [| fp64 raw bits: ref, normal scale, lo, hi, uniform lower, upper]
   int tdata_f64;            // the fp64 block is present (numpy-compatible draws)
   uint64_t seed;
+  int env0;                 // global index of this batch's env 0 (a shard of a sharded job):
+                            // env e is the job's env env0 + e and draws from seed + env0 + e
 };
 
 struct TaskState {

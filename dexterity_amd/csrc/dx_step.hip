@@ -1172,6 +1172,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     for (int k = 0; k < 7; k++) stage_count(c, CNT_PLANE_BOX + k, wave_sum_i(lead ? v[k] : 0));
   }
   stage_mark(c, ST_NP_MPR);
+  if (LANE == 0 && !watch_only) I[I_NRAW] = max(I[I_NRAW], ncon);
   if (ncon > DX_NCON_MAX) {
     if (LANE == 0) I[I_OVF] |= 2;
     ncon = DX_NCON_MAX;
@@ -2590,7 +2591,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
         if (LANE < nq) qpos[LANE] = (float)fmin(ld64(3 * nq + jl), fmax(ld64(2 * nq + jl), q));
       } else if (LANE < nq) {
         int draw = 0x100000 + (((g & 4095) * 128 + (a & 127)) * 64 + LANE) * 2;
-        float u1 = dx_urand(P.seed, env, ep, draw), u2 = dx_urand(P.seed, env, ep, draw + 1);
+        float u1 = dx_urand(P.seed, P.env0 + env, ep, draw), u2 = dx_urand(P.seed, P.env0 + env, ep, draw + 1);
         float z = sqrtf(-2.0f * logf(fmaxf(u1, 1e-12f))) * cosf(6.283185307179586f * u2);
         float l = lo[LANE], h = hi[LANE];
         qpos[LANE] = fminf(h, fmaxf(l, ref[LANE] + P.goal_scale * (h - l) * z));
@@ -2640,7 +2641,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
         const double q = mtw_uniform(w, nq, ld64(4 * nq + jl), ld64(5 * nq + jl));
         if (LANE < nq) qpos[LANE] = (float)q;
       } else if (LANE < nq) {
-        float u = dx_urand(P.seed, env, ep, 0x200000 + a * 64 + LANE);
+        float u = dx_urand(P.seed, P.env0 + env, ep, 0x200000 + a * 64 + LANE);
         float l = P.range_frac * lo[LANE], h = P.range_frac * hi[LANE];
         qpos[LANE] = l + (h - l) * u;
       }
@@ -2768,15 +2769,63 @@ __device__ __forceinline__ void sensor_stash(const Ctx& c, const DevBatch& B, in
   }
 }
 
-// One physics step (mj_step): forward, warm start <- solved qacc, Euler.
+// After a physics step: the capacity bits of its collision / constraint passes go to
+// the batch's always-on health counters (include/dx.h dx_health), and a state that is no
+// longer finite -- or an acceleration beyond mjMAXVAL -- is MuJoCo's BADQACC
+// ([3P] mj_checkAcc): the env's data is reset (mj_resetData: qpos0, zero velocity, warm
+// start, ctrl and time), the env is flagged (B.bad, which the task turns into dm_control's
+// divergent-physics step: LAST, reward 0, discount 0) and counted.
 template <class Ctx>
-__device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time, int env = -1) {
+__device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, int env, float& time) {
+  const DevModel& m = c.mdl();
+  int* I = c.I;
+  const int ovf = I[I_OVF], nraw = I[I_NRAW];
+  const float* qpos = c.f(c.L.qpos);
+  const float* qvel = c.f(c.L.qvel);
+  const float* qacc = c.f(c.L.qacc);
+  bool badl = false;
+  for (int i = LANE; i < c.nq; i += DX_WAVE) badl |= !isfinite(qpos[i]);
+  for (int i = LANE; i < c.nv; i += DX_WAVE) badl |= !isfinite(qvel[i]) || !(fabsf(qacc[i]) <= DX_MAXVAL);
+  const bool bad = __any(badl) != 0;
+  if (LANE == 0 && B.health) {
+    if (ovf & 1) atomicAdd(B.health + 1, 1u);
+    if (ovf & 2) atomicAdd(B.health + 0, 1u);
+    if (ovf & 4) atomicAdd(B.health + 2, 1u);
+    if (ovf & 8) atomicAdd(B.health + 3, 1u);
+    if (bad) atomicAdd(B.health + 4, 1u);
+    if (nraw > DX_NCON_MAX / 2) atomicMax(B.health + 5, (unsigned)nraw);
+    if (B.ncon_hist) atomicAdd(B.ncon_hist + min(nraw, DX_NCON_HIST - 1), 1u);
+  }
+  SYNC();
+  if (LANE == 0) { I[I_OVF] = 0; I[I_NRAW] = 0; }
+  if (bad) {
+    float* q = c.f(c.L.qpos);
+    for (int i = LANE; i < c.nq; i += DX_WAVE) q[i] = m.qpos0[i];
+    for (int i = LANE; i < c.nv; i += DX_WAVE) {
+      c.f(c.L.qvel)[i] = 0.f;
+      c.f(c.L.v5)[i] = 0.f;  // warm start
+      c.f(c.L.qacc)[i] = 0.f;
+    }
+    for (int i = LANE; i < c.nu; i += DX_WAVE) {
+      c.f(c.L.ctrl)[i] = 0.f;
+      if (env >= 0) B.ctrl[(size_t)env * c.nu + i] = 0.f;  // later substeps (queued tasks) reload it
+    }
+    time = 0.f;
+    if (LANE == 0 && B.bad && env >= 0) B.bad[env] = 1;
+  }
+  SYNC();
+}
+
+// One physics step (mj_step): forward, warm start <- solved qacc, Euler, health check.
+template <class Ctx>
+__device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time, int env, bool last) {
   forward(c, B.xfrc);
-  if (env >= 0 && B.sen_stash) sensor_stash(c, B, env);
+  if (last && B.sen_stash) sensor_stash(c, B, env);
   float* ws = c.f(c.L.v5);
   for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
   SYNC();
   euler(c, &time);
+  health_check(c, B, env, time);
 }
 
 // After the last substep (or a forward): debug record, per-env outputs, the
@@ -2848,10 +2897,11 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
   for (int s = 0; s < steps; s++) {
     if (mode == 0) {
-      env_substep(c, B, time, s == steps - 1 ? env : -1);
+      env_substep(c, B, time, env, s == steps - 1);
     } else {
       forward(c, B.xfrc);
       if (B.sen_stash) sensor_stash(c, B, env);
+      health_check(c, B, env, time);
     }
   }
   env_finish(c, B, env, time);
@@ -2935,7 +2985,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     // cost so far (shader cycles / 1024), carried in the record between substeps
     const unsigned cost0 = s > 0 ? __float_as_uint(rec[c.nq + 2 * c.nv + 1]) : 0u;
     float time = env_begin(c, B, env, s > 0 ? rec : nullptr);
-    if (!(B.skip && B.skip[env])) env_substep(c, B, time, s == nsub - 1 ? env : -1);  // a freshly reset env is only observed
+    if (!(B.skip && B.skip[env])) env_substep(c, B, time, env, s == nsub - 1);  // a freshly reset env is only observed
     if (s == nsub - 1) {
       env_finish(c, B, env, time);
       if (LANE == 0 && B.cost)

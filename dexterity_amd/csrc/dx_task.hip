@@ -29,7 +29,8 @@ __device__ __forceinline__ float urand(uint64_t seed, int env, int episode, int 
   return dx_urand(seed, env, episode, draw);
 }
 // Seeds every env's two MT19937 streams with seed + env (numpy RandomState(seed + env)
-// and np.random.seed(seed + env) of the env's process in the reference).
+// and np.random.seed(seed + env) of the env's process in the reference); the host passes
+// seed + env0 for a shard whose env 0 is the job's env env0.
 extern "C" __global__ void dx_mt_seed_kernel(int nenv, uint64_t seed, uint32_t* mt_env, uint32_t* mt_goal) {
   const int env = blockIdx.x * blockDim.x + threadIdx.x;
   if (env >= nenv) return;
@@ -175,6 +176,14 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
       S.step_type[env] = ST_FIRST;
       S.reward[env] = 0;
       S.discount[env] = 1;
+    } else if (B.bad && B.bad[env]) {
+      // a substep diverged and the physics reset the env (dx_step.hip health_check):
+      // [3P] composer.Environment.step with a PhysicsError it does not raise ends the
+      // episode with reward 0 and discount 0; the next step re-initialises the env
+      B.bad[env] = 0;
+      S.step_type[env] = ST_LAST;
+      S.reward[env] = 0;
+      S.discount[env] = 0;
     } else {
       // GoalTask.after_step (task.py:167-185)
       float time = B.time[env];
@@ -261,12 +270,14 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
 
 // Uniform random actions within the actuator ctrlrange: the synthetic agent of
 // manipulation_test.py:44-45 (random_state.uniform(spec.minimum, spec.maximum)).
+// Keyed by the job-wide env index env0 + env, so a shard draws what the same envs of
+// one unsharded batch draw.
 extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
-                                                    int step, float* out) {
+                                                    int step, int env0, float* out) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= nenv * nu) return;
   int env = t / nu, i = t % nu;
-  float u = urand(seed, env, step, 1000 + i);
+  float u = urand(seed, env0 + env, step, 1000 + i);
   float lo = ctrlrange[2 * i], hi = ctrlrange[2 * i + 1];
   out[t] = lo + (hi - lo) * u;
 }

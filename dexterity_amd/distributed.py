@@ -2,6 +2,8 @@
 
 Environments are independent. Rank r of W owns the contiguous env range
 `env_shard(B_global, r, W)` on its own GPU and steps it with no data-path collective.
+Its dx_env is created with `env_offset` = the range's first env, so every per-env
+stream (reset draws, device-sampled actions) is keyed by the job-wide env index.
 The only exchange is one all-gather per control step of each rank's packed
 `[obs | reward | discount | step_type]` rows. That gather is `dx_allgather_obs` in
 libdx, which calls RCCL (librccl) directly over xGMI: about 2 MB per rank at 4096 envs.
@@ -36,9 +38,19 @@ def env_shard(global_envs: int, rank: int, world: int) -> Tuple[int, int]:
     return env0, n
 
 
-def rank_seed(seed: int, rank: int) -> int:
-    """Per-rank task seed (env i of the whole job draws from seed + rank stream)."""
-    return int(seed) + int(rank)
+def env_seeds(seed: int, global_envs: int, rank: int, world: int):
+    """Global env ids and reset-stream seeds of rank `rank`'s shard.
+
+    The reference loads one environment per process with one RandomState
+    (manipulation/__init__.py:56-86); a batch of them here gives env i of the job the
+    seed `seed + i` (include/dx.h dx_env_create_shard), whichever rank steps it.  Rank r
+    creates its dx_env with env_offset = env0(r), so the seeds of a sharded job are
+    disjoint across ranks and equal those of one unsharded batch of all the envs."""
+    import numpy as np
+
+    env0, n = env_shard(global_envs, rank, world)
+    ids = np.arange(env0, env0 + n, dtype=np.int64)
+    return ids, (int(seed) + ids) & 0xFFFFFFFF
 
 
 def gathered_rows(rank: int, n_per_rank: int) -> slice:

@@ -244,9 +244,13 @@ class GoalEnvironment:
     """
 
     def __init__(self, task: ReOrient, num_envs: int, seed: Optional[int] = None, device: int = 0,
-                 time_limit: Optional[float] = None, strip_singleton_obs_buffer_dim: bool = True):
+                 time_limit: Optional[float] = None, strip_singleton_obs_buffer_dim: bool = True,
+                 env_offset: int = 0):
         self.task = task
         self.num_envs = int(num_envs)
+        # this batch's env e is env env_offset + e of the job (a shard of a sharded
+        # job, dexterity_amd.distributed.env_shard); it draws from seed + env_offset + e
+        self.env_offset = int(env_offset)
         # composer.Environment(time_limit=..., strip_singleton_obs_buffer_dim=...)
         # (manipulation/__init__.py:81-86); the tasks' own time_limit is inf
         self.time_limit = float("inf") if time_limit is None else float(time_limit)
@@ -255,10 +259,10 @@ class GoalEnvironment:
         L = _lib.load()
         p = task.params()
         self._seed = 0 if seed is None else int(seed)
-        self.ptr = L.dx_env_create(self.model.ptr, self.num_envs, device, task.kind,
-                                   self._seed, p.ctypes.data, len(p))
+        self.ptr = L.dx_env_create_shard(self.model.ptr, self.num_envs, device, task.kind,
+                                         self._seed, self.env_offset, p.ctypes.data, len(p))
         if not self.ptr:
-            raise _lib.DxError(f"dx_env_create failed: {L.dx_last_error().decode()}")
+            raise _lib.DxError(f"dx_env_create_shard failed: {L.dx_last_error().decode()}")
         batch_ptr = L.dx_env_batch(self.ptr)
         self.physics = physics_lib.BatchedPhysics.borrowed(self.model, batch_ptr, self.num_envs, device)
         # gravity compensation (shadow_hand_e.py:35-41 in initialize_episode)
@@ -406,17 +410,19 @@ TASKS_BY_DOMAIN = {d: tuple(t for dd, t in ALL_TASKS if dd == d) for d in sorted
 
 def load(domain_name: str, task_name: str, seed: Optional[int] = None,
          strip_singleton_obs_buffer_dim: bool = True, time_limit: Optional[float] = None,
-         num_envs: int = 1, device: int = 0) -> GoalEnvironment:
+         num_envs: int = 1, device: int = 0, env_offset: int = 0) -> GoalEnvironment:
     """manipulation/__init__.py:56-86, batched: the reference's arguments in its order,
     then the batch size and the GPU.  `time_limit=None` keeps the task's own limit
-    (inf for every suite task)."""
+    (inf for every suite task).  Env e of the batch is the reference's environment
+    loaded with seed `seed + env_offset + e`; `env_offset` places a shard of a sharded
+    job (distributed.env_shard) in the job's env numbering."""
     key = (domain_name, task_name)
     if domain_name not in {d for d, _ in SUITE}:
         raise ValueError(f"Unknown domain: {domain_name}")
     if key not in SUITE:
         raise ValueError(f"Unknown task: {task_name}")
     return GoalEnvironment(SUITE[key](), num_envs=num_envs, seed=seed, device=device, time_limit=time_limit,
-                           strip_singleton_obs_buffer_dim=strip_singleton_obs_buffer_dim)
+                           strip_singleton_obs_buffer_dim=strip_singleton_obs_buffer_dim, env_offset=env_offset)
 
 
 __all__ = ["load", "GoalEnvironment", "ReOrient", "ReOrientConfig", "Reach", "ReachConfig", "ALL_TASKS",

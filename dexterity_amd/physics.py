@@ -151,6 +151,22 @@ class BatchedPhysics:
     def debug(self, enable: bool = True) -> None:
         _lib.check(_lib.load().dx_debug_enable(self.ptr, int(enable)))
 
+    def health(self) -> dict:
+        """The always-on health counters (include/dx.h dx_health): capacity overflows,
+        diverged env-substeps, the most contacts one env-substep found and, when
+        `ncon_histogram(True)` is on, the histogram of contacts per env-substep."""
+        out = np.zeros(_lib.HEALTH_WORDS + _lib.NCON_HIST, dtype=np.uint32)
+        _lib.check(_lib.load().dx_health(self.ptr, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), out.size))
+        h = {k: int(out[i]) for i, k in enumerate(_lib.HEALTH)}
+        h["ncon_hist"] = out[_lib.HEALTH_WORDS:].astype(np.int64)
+        return h
+
+    def health_clear(self) -> None:
+        _lib.check(_lib.load().dx_health_clear(self.ptr))
+
+    def ncon_histogram(self, enable: bool = True) -> None:
+        _lib.check(_lib.load().dx_ncon_histogram(self.ptr, int(enable)))
+
     def debug_get(self, name: str) -> np.ndarray:
         nv = self.model.nv
         sizes = {

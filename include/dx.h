@@ -77,6 +77,9 @@ enum dx_field {
                            sensors of shadow_hand_e.py:176-196 / adroit_hand.py:153-172
                            (mj_rnePostConstraint + mj_sensorAcc of the last substep, before
                            its integration, as after dm_control's physics.step()) */
+  DX_DIVERGED = 16,     /* 1  (int32 bits) r: the env's state diverged during the last dx_step /
+                           dx_forward (a non-finite qpos / qvel / qacc, or |qacc| > 1e10: MuJoCo's
+                           BADQACC, [3P] mj_checkAcc) and was reset to qpos0 (mj_resetData) */
   DX_NFIELD
 };
 
@@ -141,12 +144,32 @@ int dx_set_outputs(dx_batch* b, int bodies);
  * sensor (one extra small kernel per call; nothing when disabled). */
 int dx_sensor_enable(dx_batch* b, int enable);
 
+/* Health (always on) ----------------------------------------------------- */
+/* Counters of capacity overflows and divergences since the batch was created or last
+ * cleared, out[0 .. min(n, DX_HEALTH_WORDS)):
+ *   0 env-substeps that found more contacts than the DX_NCON_MAX = 32 kept (MuJoCo keeps
+ *     up to nconmax = 200 in the Shadow scenes, shadow_hand_series_e.xml:8; the rest
+ *     are dropped, as MuJoCo drops contacts beyond nconmax with mjWARN_CONTACTFULL)
+ *   1 env-substeps whose broadphase / narrowphase candidate lists overflowed
+ *   2 contacts whose Jacobian spans more than DX_DOFMAX dofs (truncated)
+ *   3 env-substeps with more constraint rows than the LDS block holds (truncated)
+ *   4 env-substeps that diverged (DX_DIVERGED) and reset their env
+ *   5 the most contacts one env-substep found, when above DX_NCON_MAX / 2 (else 0)
+ * then, when the histogram is on (dx_ncon_histogram), out[16 .. 16 + 65): env-substeps
+ * by contacts found (bins 0..63, then >= 64).  Synchronises the batch's stream. */
+#define DX_HEALTH_WORDS 16
+#define DX_NCON_HIST 65
+int dx_health(dx_batch* b, uint32_t* out, int32_t n);
+int dx_health_clear(dx_batch* b);
+int dx_ncon_histogram(dx_batch* b, int enable);
+
 /* Debug / parity -------------------------------------------------------- */
 /* When enabled, dx_forward/dx_step record per-env intermediates of the LAST
  * substep: qacc_smooth, qfrc_bias(+applied), qfrc_actuator, M (nv*nv), contacts. */
 int dx_debug_enable(dx_batch* b, int enable);
 /* name: "qacc_smooth" "qfrc_smooth" "M" "contact" (16 floats/contact: pos3 frame9
  * dist geom1 geom2 condim) "efc_count" ; dst is host memory for all envs.
+ * "health" (no dx_debug_enable needed): dx_health's words, as uint32 bits.
  * "queue_timeouts" (1 word, int32 bits, no dx_debug_enable needed): nonzero if a
  * task of the substep queue ever stopped waiting for its predecessor. */
 int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
@@ -192,6 +215,14 @@ enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT
                                           (fingertip_position.py:136-139) */ };
 dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device, int32_t task, uint64_t seed,
                       const float* params, int32_t nparams);
+/* One shard of a job's environments: this handle's env e is the job's env env0 + e.
+ * Every per-env stream is keyed by the job-wide index (numpy-compatible MT19937 seeded
+ * with seed + env0 + e, dx_env_sample_actions keyed by env0 + e), so shard r of a
+ * sharded job behaves exactly like envs [env0, env0 + nenv) of one unsharded batch --
+ * the reference's one-RandomState-per-env seed contract (manipulation/__init__.py:56-86)
+ * with env i seeded seed + i.  dx_env_create(...) = dx_env_create_shard(..., 0, ...). */
+dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t device, int32_t task, uint64_t seed,
+                            int64_t env0, const float* params, int32_t nparams);
 void dx_env_destroy(dx_env* e);
 dx_batch* dx_env_batch(dx_env* e);
 int dx_env_obs_dim(const dx_env* e);

@@ -445,3 +445,86 @@ def test_task_runs(built, name):
             action = rs.uniform(act_spec.minimum, act_spec.maximum, size=(n,) + act_spec.shape)
             ts = env.step(action.astype(act_spec.dtype))
     env.close()
+
+
+def _snapshot(env):
+    from dexterity_amd import _lib
+
+    ts = env.timestep()
+    obs = np.concatenate([ts.observation[k] for k in ts.observation], axis=1).astype(np.float32)
+    return {"qpos": env.physics.get(_lib.QPOS), "qvel": env.physics.get(_lib.QVEL), "goal": env.goals(),
+            "obs": obs, "reward": ts.reward, "step_type": ts.step_type}
+
+
+@pytest.mark.parametrize("domain", ["reorient", "reach"])
+def test_shard_matches_unsharded_batch(built, domain):
+    """A dx_env created for rank 1 of a two-rank job (env_offset = B) is envs B..2B-1 of
+    one 2B-env batch with the same seed: resets (goals, prop pose, reach joints), the
+    device-sampled actions and every output over 12 control steps agree bit for bit."""
+    from dexterity_amd import manipulation
+
+    seed, n = 4242, 48
+    whole = manipulation.load(domain, "state_dense", seed=seed, num_envs=2 * n)
+    shard = manipulation.load(domain, "state_dense", seed=seed, num_envs=n, env_offset=n)
+    whole.reset()
+    shard.reset()
+    for i in range(13):
+        a, b = _snapshot(whole), _snapshot(shard)
+        for k in a:
+            np.testing.assert_array_equal(a[k][n:], b[k], err_msg=f"{k} at step {i}")
+        if i == 12:
+            break
+        pa, pb = whole.sample_actions(i), shard.sample_actions(i)
+        ha = np.empty((2 * n, whole.model.nu), np.float32)
+        hb = np.empty((n, shard.model.nu), np.float32)
+        whole.physics.sync()
+        shard.physics.sync()
+        manipulation._copy_d2h(ha, pa)
+        manipulation._copy_d2h(hb, pb)
+        np.testing.assert_array_equal(ha[n:], hb)
+        whole.step(pa, device_action=True)
+        shard.step(pb, device_action=True)
+    whole.close()
+    shard.close()
+
+
+def _shard_worker(rank, world, n, seed, steps, q):
+    from dexterity_amd import distributed, manipulation
+
+    env0, cnt = distributed.env_shard(world * n, rank, world)
+    env = manipulation.load("reorient", "state_dense", seed=seed, num_envs=cnt, env_offset=env0)
+    env.reset()
+    for i in range(steps):
+        env.step(env.sample_actions(i), device_action=True)
+    q.put((rank, _snapshot(env)))
+    env.close()
+
+
+def test_sharded_job_two_processes(built):
+    """The sharded job of bench.py on one GPU: two processes step their own shards
+    (env_offset from distributed.env_shard); their rows, placed at
+    distributed.gathered_rows, equal one process stepping the whole job."""
+    import multiprocessing as mp
+
+    from dexterity_amd import distributed, manipulation
+
+    world, n, seed, steps = 2, 64, 12345, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, n, seed, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    whole = manipulation.load("reorient", "state_dense", seed=seed, num_envs=world * n)
+    whole.reset()
+    for i in range(steps):
+        whole.step(whole.sample_actions(i), device_action=True)
+    ref = _snapshot(whole)
+    for r in range(world):
+        sl = distributed.gathered_rows(r, n)
+        for k in ref:
+            np.testing.assert_array_equal(ref[k][sl], got[r][k], err_msg=f"rank {r} {k}")
+    whole.close()

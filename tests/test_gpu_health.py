@@ -1,0 +1,118 @@
+"""Always-on health reporting (include/dx.h dx_health, DX_DIVERGED): capacity overflows
+are counted rather than silently dropped, and a diverged environment is reset the way
+MuJoCo resets a BADQACC state ([3P] mj_checkAcc -> mj_resetData) and ends its episode
+the way composer ends one on a PhysicsError it does not raise (reward 0, discount 0)."""
+
+import numpy as np
+import pytest
+
+from dexterity_amd import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def _box_field(n_boxes):
+    """A ground plane and `n_boxes` free cubes (half-size 2 cm) resting 1 mm into it,
+    apart from one another: every cube-plane pair yields 4 contacts (plane-box corners),
+    so 10 cubes give 40 contacts, above the 32 kept per env-substep.  Built from the
+    compiler's own primitives (no reference files), so it compiles on the GPU box."""
+    from dexterity_amd.mjcf.compiler import Scene
+
+    s = Scene(timestep=0.005)
+    s.add_world_geom("ground", "plane", (1, 1, 0.1), friction="0.4 0.005 0.0001", solimp="0.95 0.99 0.001",
+                     solref="0.002 1")
+    for i in range(n_boxes):
+        s.add_free_box(f"box{i}", 0.02, [0.1 * (i % 5) - 0.2, 0.1 * (i // 5), 0.019])
+    return s.compile()
+
+
+def test_contact_overflow_is_counted():
+    from dexterity_amd import physics
+
+    cm = _box_field(10)
+    model = physics.Model(cm)
+    ph = physics.BatchedPhysics(model, 8)
+    ph.ncon_histogram(True)
+    ph.health_clear()
+    ph.step(1)
+    h = ph.health()
+    assert h["contact_overflow"] == 8, h
+    assert h["ncon_max"] == 40, h
+    assert h["ncon_hist"][40] == 8 and h["ncon_hist"].sum() == 8
+    assert h["diverged"] == 0
+    assert np.all(ph.get(_lib.NCON)[:, 0] == 32)
+    # below the cap nothing is reported
+    ph2 = physics.BatchedPhysics(physics.Model(_box_field(7)), 8)
+    ph2.step(2)
+    h2 = ph2.health()
+    assert h2["contact_overflow"] == 0 and h2["ncon_max"] == 28, h2
+    assert np.all(ph2.get(_lib.NCON)[:, 0] == 28)
+
+
+def _reorient_physics(n):
+    from dexterity_amd import manipulation, physics
+
+    task = manipulation.ReOrient()
+    ph = physics.BatchedPhysics(physics.Model(task.compiled), n)
+    ph.set_xfrc(task.gravity_compensation)
+    return task, ph
+
+
+def test_nan_state_resets_env_like_badqacc():
+    """A non-finite velocity injected into env 3 makes its next physics step diverge:
+    the env is flagged (DX_DIVERGED), counted, reset to qpos0 with zero velocity, warm
+    start, ctrl and time, and continues from there; every other env is bit-identical to
+    the same batch stepped without the injection."""
+    n, bad = 16, 3
+    task, ph = _reorient_physics(n)
+    _, ref = _reorient_physics(n)
+    rng = np.random.RandomState(0)
+    lo, hi = task.compiled.actuator_ctrlrange.T
+    ctrl = rng.uniform(lo, hi, size=(n, task.compiled.nu)).astype(np.float32)
+    for p in (ph, ref):
+        p.set(_lib.CTRL, ctrl)
+        p.step(5)
+    qvel = ph.get(_lib.QVEL)
+    qvel[bad, 2] = np.nan
+    ph.set(_lib.QVEL, qvel)
+    ph.health_clear()
+    ph.step(5)
+    ref.step(5)
+    h = ph.health()
+    assert h["diverged"] >= 1, h
+    div = ph.get(_lib.DIVERGED)[:, 0]
+    assert div[bad] == 1 and div.sum() == 1
+    others = np.arange(n) != bad
+    for f in (_lib.QPOS, _lib.QVEL, _lib.QACC_WARMSTART, _lib.TIME):
+        np.testing.assert_array_equal(ph.get(f)[others], ref.get(f)[others])
+    assert np.all(np.isfinite(ph.get(_lib.QPOS))) and np.all(np.isfinite(ph.get(_lib.QVEL)))
+    assert np.all(ph.get(_lib.CTRL)[bad] == 0)
+    # reset in the first substep, then 4 clean substeps from qpos0 at t = 0
+    np.testing.assert_allclose(ph.get(_lib.TIME)[bad, 0], 4 * 0.005, rtol=1e-6)
+    # the next step is clean: the flag reports that call only
+    ph.step(1)
+    assert ph.get(_lib.DIVERGED)[:, 0].sum() == 0
+    assert ph.health()["diverged"] == h["diverged"]
+
+
+def test_nan_state_ends_episode_reward0_discount0():
+    """At the environment level the divergence ends the env's episode as composer does
+    when physics is divergent (LAST, reward 0, discount 0); the next step resets it
+    (FIRST) and the other envs are unaffected."""
+    from dexterity_amd import manipulation
+
+    n, bad = 16, 5
+    env = manipulation.load("reorient", "state_dense", seed=11, num_envs=n)
+    env.reset()
+    for i in range(3):
+        env.step(env.sample_actions(i), device_action=True)
+    qvel = env.physics.get(_lib.QVEL)
+    qvel[bad, 0] = np.inf
+    env.physics.set(_lib.QVEL, qvel)
+    env.step(env.sample_actions(3), device_action=True)
+    ts = env.timestep()
+    assert ts.step_type[bad] == 2 and ts.reward[bad] == 0 and ts.discount[bad] == 0
+    env.step(env.sample_actions(4), device_action=True)
+    assert env.timestep().step_type[bad] == 0
+    assert env.physics.health()["diverged"] == 1
+    env.close()
