@@ -36,7 +36,7 @@ EXPORTS = (
     "dx_comm_unique_id", "dx_comm_init", "dx_comm_destroy", "dx_comm_rank", "dx_comm_size",
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
     "dx_env_set_time_limit", "dx_set_outputs", "dx_env_create_shard",
-    "dx_health", "dx_health_clear", "dx_ncon_histogram",
+    "dx_health", "dx_health_clear", "dx_ncon_histogram", "dx_env_set_goal_time_limit",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -127,7 +127,8 @@ def load(path: str = LIB_PATH):
     L.dx_env_goal_dim.argtypes = [vp]
     L.dx_env_reset.argtypes = [vp]
     L.dx_env_step.argtypes = [vp, vp]
-    L.dx_env_set_time_limit.argtypes = [vp, ctypes.c_float]
+    L.dx_env_set_time_limit.argtypes = [vp, ctypes.c_double]
+    L.dx_env_set_goal_time_limit.argtypes = [vp, ctypes.c_double]
     L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
     L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]

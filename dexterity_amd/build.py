@@ -68,8 +68,18 @@ def _units() -> list:
 
 
 def _compile(out: str, verbose: bool) -> None:
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    # one build of a tree at a time (several ranks, or pytest beside bench.py): the
+    # object cache and its clean-up below are shared
+    import fcntl
+
     os.makedirs(OBJ, exist_ok=True)
+    with open(os.path.join(OBJ, ".lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        _compile_locked(out, verbose)
+
+
+def _compile_locked(out: str, verbose: bool) -> None:
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     h = hashlib.sha1()
     for f in sorted(SOURCES + HEADERS + ("dx_specs.inc",)):
         path = os.path.join(CSRC, f)
@@ -83,13 +93,14 @@ def _compile(out: str, verbose: bool) -> None:
         obj = os.path.join(OBJ, f"{name}.{key}.o")
         objs.append(obj)
         if not os.path.exists(obj):
-            jobs.append([hipcc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"])
+            jobs.append(([hipcc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", f"{obj}.{os.getpid()}.tmp"], obj))
 
-    def run(cmd):
+    def run(job):
+        cmd, obj = job
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.run(cmd, check=True)
-        os.replace(cmd[-1], cmd[-1][: -len(".tmp")])
+        os.replace(cmd[-1], obj)
 
     nproc = int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))
     with concurrent.futures.ThreadPoolExecutor(max_workers=max(1, min(nproc, 8))) as ex:
@@ -151,7 +162,7 @@ def spec_text(lib_path: str) -> str:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return OUT
-    tmp = OUT + ".tmp"
+    tmp = f"{OUT}.{os.getpid()}.tmp"
     _compile(tmp, verbose)
     # regenerate the specializations with the layout code just built (in a child
     # process: this one may load libdx.so afterwards)

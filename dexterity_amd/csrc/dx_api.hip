@@ -686,7 +686,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   int end = off;
   L.tsm = B0;
   end = std::max(end, B0 + r4(ntri));
-  L.cand_max = 768;
+  L.cand_max = DX_CAND_MAX;
   L.cand = B0;
   // + MPR portal points of the DX_NGRP narrowphase groups (36 words each), then the
   // candidates' pair records (float4 per candidate slot: cand_max - 2 * (cand_max / 3))
@@ -1356,6 +1356,23 @@ extern "C" int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t*
   P.sites = ds;
   P.joints = dj;
   P.targets = dt;
+  P.starts = nullptr;
+  if (A > 1) {  // numpy-compatible random restarts (dx_ik.hip dx_ik_starts_kernel)
+    auto it = b->model->arr.find("jnt_range");
+    if (it == b->model->arr.end() || it->second.dtype != 1) return fail(DX_EMODEL, "model has no fp64 jnt_range");
+    std::vector<double> rng(2 * (size_t)njoint);
+    for (int k = 0; k < njoint; k++) {
+      rng[2 * k] = ((const double*)it->second.p)[2 * joints[k]];
+      rng[2 * k + 1] = ((const double*)it->second.p)[2 * joints[k] + 1];
+    }
+    double* drng = (double*)S.get(rng.size() * 8);
+    uint32_t* mt = (uint32_t*)S.get(E * DX_MT_WORDS * 4);
+    float* st = (float*)S.get(E * (A - 1) * njoint * 4);
+    if (!drng || !mt || !st) return fail(DX_ENOMEM, "device scratch allocation failed");
+    HIPCHK(hipMemcpyAsync(drng, rng.data(), rng.size() * 8, hipMemcpyHostToDevice, b->stream));
+    HIPCHK(dx_launch_ik_starts((int)E, (int)A - 1, njoint, opt->seed, drng, mt, st, b->stream));
+    P.starts = st;
+  }
   HIPCHK(dx_launch_ik((int)(E * A), lds, b->stream, b->dm_dev, b->db, b->model->lds, P));
   HIPCHK(dx_launch_ik_select((int)E, b->stream, b->dm, P, oq, os, oe, oa, ot));
   if (qpos_out) HIPCHK(hipMemcpyAsync(qpos_out, oq, E * njoint * 4, hipMemcpyDefault, b->stream));
@@ -1567,6 +1584,8 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
   rc |= al((void**)&S.step_type, E * 4); rc |= al((void**)&S.episode, E * 4);
   rc |= al((void**)&S.skip, E * 4); rc |= al((void**)&S.failure, E * 4);
   rc |= al((void**)&S.need, E * 4); rc |= al((void**)&S.goalnum, E * 4); rc |= al((void**)&S.goalfail, E * 4);
+  rc |= al((void**)&S.time_d, E * 8); rc |= al((void**)&S.solve_start_d, E * 8);
+  rc |= al((void**)&S.nsub_d, E * 4); rc |= al((void**)&S.solve_n, E * 4);
   if (task == DX_TASK_REACH) rc |= al((void**)&S.goal_qpos, E * nq * 4);
   if (task == DX_TASK_REORIENT) {
     rc |= al((void**)&S.mt_env, E * DX_MT_WORDS * 4);
@@ -1578,6 +1597,9 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
     }
   }
   P.time_limit = INFINITY;
+  P.time_limit_d = INFINITY;
+  P.h_d = getd(m, "timestep");
+  P.max_time_d = P.max_time;  // dx_env_set_goal_time_limit gives the fp64 value
   float* tdata = nullptr;
   TaskParams* dP = nullptr;
   TaskState* dS = nullptr;
@@ -1655,13 +1677,25 @@ extern "C" int dx_env_reset(dx_env* e) {
   return env_run(e, nullptr);
 }
 
-extern "C" int dx_env_set_time_limit(dx_env* e, float seconds) {
-  if (!e || !(seconds > 0)) return fail(DX_EINVAL, "null env or non-positive time limit");
-  e->P.time_limit = seconds;
+static int env_params_upload(dx_env* e) {
   HIPCHK(hipSetDevice(e->batch->device));
   HIPCHK(hipStreamSynchronize(e->batch->stream));  // the device copy is read by the sampling pass
   HIPCHK(hipMemcpy((void*)e->batch->db.tp, &e->P, sizeof(TaskParams), hipMemcpyHostToDevice));
   return 0;
+}
+
+extern "C" int dx_env_set_time_limit(dx_env* e, double seconds) {
+  if (!e || !(seconds > 0)) return fail(DX_EINVAL, "null env or non-positive time limit");
+  e->P.time_limit = (float)seconds;
+  e->P.time_limit_d = seconds;
+  return env_params_upload(e);
+}
+
+extern "C" int dx_env_set_goal_time_limit(dx_env* e, double seconds) {
+  if (!e || !(seconds >= 0)) return fail(DX_EINVAL, "null env or negative time");
+  e->P.max_time = (float)seconds;
+  e->P.max_time_d = seconds;
+  return env_params_upload(e);
 }
 
 extern "C" int dx_env_step(dx_env* e, const float* action) {

@@ -136,11 +136,12 @@ extern "C" __global__ void __launch_bounds__(64) dx_ik_kernel(const DevModel* __
   SYNC();
   if (P.mode == 0) {
     // ik_solver.py:122-129: attempt 0 from the nullspace reference (joint midrange),
-    // later attempts uniformly within the joint range
+    // later attempts from np.random.uniform over the joint ranges (dx_ik_starts_kernel)
     for (int k = LANE; k < P.njoint; k += DX_WAVE) {
       const int j = P.joints[k];
       const float lo = m.jnt_range[2 * j], hi = m.jnt_range[2 * j + 1];
-      qpos[m.jnt_qposadr[j]] = att == 0 ? 0.5f * (lo + hi) : lo + (hi - lo) * dx_urand(P.seed, env, att, k);
+      qpos[m.jnt_qposadr[j]] =
+          att == 0 ? 0.5f * (lo + hi) : P.starts[((size_t)env * (P.nattempt - 1) + att - 1) * P.njoint + k];
     }
     SYNC();
   }
@@ -267,5 +268,31 @@ hipError_t dx_launch_ik_select(int nenv, hipStream_t stream, const DevModel& m, 
                                int* success, float* err_out, int* attempt_out, int* steps_out) {
   hipLaunchKernelGGL(dx_ik_select_kernel, dim3((nenv + 255) / 256), dim3(256), 0, stream, nenv, P, m.jnt_range,
                      qpos_out, success, err_out, attempt_out, steps_out);
+  return hipGetLastError();
+}
+
+// Random restarts of IKSolver.solve (ik_solver.py:127-130): attempt a >= 1 starts at
+// np.random.uniform(*range.T) -- numpy's global stream, which env e's process seeded with
+// np.random.seed(seed + e) -- so attempt a takes draws (a - 1) * njoint .. a * njoint - 1,
+// one per joint in order: low + (high - low) * random_sample(), in fp64 as numpy computes
+// it (no fma), then rounded to the fp32 state.  One thread per env; its MT19937 state is
+// interleaved over the envs (dx_mt_* in dx_internal.h).
+extern "C" __global__ void dx_ik_starts_kernel(int nenv, int natt, int nj, uint64_t seed, const double* range,
+                                               uint32_t* mt, float* out) {
+  const int env = blockIdx.x * blockDim.x + threadIdx.x;
+  if (env >= nenv) return;
+  dx_mt_seed(mt, nenv, env, (uint32_t)(seed + (uint64_t)env));
+  for (int a = 0; a < natt; a++)
+    for (int k = 0; k < nj; k++) {
+      const double lo = range[2 * k], hi = range[2 * k + 1];
+      const double u = dx_mt_double(mt, nenv, env);
+      out[((size_t)env * natt + a) * nj + k] = (float)__dadd_rn(lo, __dmul_rn(hi - lo, u));
+    }
+}
+
+hipError_t dx_launch_ik_starts(int nenv, int natt, int njoint, uint64_t seed, const double* range, uint32_t* mt,
+                               float* out, hipStream_t stream) {
+  hipLaunchKernelGGL(dx_ik_starts_kernel, dim3((nenv + 63) / 64), dim3(64), 0, stream, nenv, natt, njoint, seed, range,
+                     mt, out);
   return hipGetLastError();
 }

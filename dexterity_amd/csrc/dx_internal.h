@@ -8,7 +8,12 @@
 #include <stdint.h>
 
 #define DX_WAVE 64
+#ifndef DX_NCON_MAX
 #define DX_NCON_MAX 32    // contacts kept per env per substep (MuJoCo pool: nconmax)
+#endif
+#ifndef DX_CAND_MAX
+#define DX_CAND_MAX 768   // collision candidate-list words per env (dx_api.hip LDS layout)
+#endif
 #define DX_DOFMAX 14      // max dofs in a contact Jacobian (|chain(b1) xor chain(b2)|; checked at load)
 #define DX_CON_STRIDE 20  // words per contact record in LDS:
 // 0-2 pos, 3-11 frame (normal, tangents), 12 dist, 13 geom pair, 14 nnz | nrows << 8
@@ -22,6 +27,7 @@
 #define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
 #endif
 #define DX_NGRP (DX_WAVE / DX_NPG)
+#define DX_GOAL_RETRIES 64  // reach goal sampling: GoalInitializationError retries per goal (bounded)
 
 enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };
 enum { DXJ_FREE = 0, DXJ_HINGE = 3 };
@@ -189,6 +195,9 @@ struct TaskParams {
   uint64_t seed;
   int env0;                 // global index of this batch's env 0 (a shard of a sharded job):
                             // env e is the job's env env0 + e and draws from seed + env0 + e
+  // fp64 time bookkeeping, as MuJoCo's d->time (mjtNum): the physics timestep, the
+  // per-goal limit (max_time_per_goal) and composer's time_limit (+inf: none)
+  double h_d, max_time_d, time_limit_d;
 };
 
 struct TaskState {
@@ -203,6 +212,12 @@ struct TaskState {
   // (state[624], pos, has_gauss, gauss as fp64), drawn wave-cooperatively in the step
   // kernel (dx_step.hip mtw_*)
   uint32_t* mt_reach;
+  // fp64 time (TaskParams::h_d): the env's time as MuJoCo accumulates it (time += h per
+  // physics step, from 0 at the episode's mj_resetData), the substeps it covers, the
+  // time the current goal was set, and (reach) the substep at which the sampling pass
+  // set it (-1: none pending)
+  double *time_d, *solve_start_d;
+  int *nsub_d, *solve_n;
 };
 
 // numpy.random.RandomState-compatible MT19937 ([3P] numpy legacy seeding and
@@ -300,7 +315,10 @@ struct IkDev {
   float* att_err;            // [nenv][nattempt][nsite]
   int* att_steps;            // [nenv][nattempt]
   float *jacp, *jacr;        // mode 1: [nenv][nsite][3][nv] (either may be null)
+  const float* starts;       // [nenv][nattempt - 1][njoint]: attempts >= 1 start here
 };
+hipError_t dx_launch_ik_starts(int nenv, int natt, int njoint, uint64_t seed, const double* range, uint32_t* mt,
+                               float* out, hipStream_t stream);
 int dx_ik_lds_words(const DevModel& d, int nsite);
 hipError_t dx_launch_ik(int nwave, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                         const Lds& L, const IkDev& P);

@@ -2583,14 +2583,30 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
     const int g = T.goalnum[env];
     float gc = 0;
     bool ok = false;
-    for (int a = 0; a < P.max_reject; a++) {
+    int fails = 0;
+    for (int att = 0;; att++) {
+      // max_rejection_samples draws without a collision-free goal: the reference raises
+      // GoalInitializationError (fingertip_position.py:112-117) and GoalEnvironment
+      // retries the reset / step (environment.py:14-34) from the continuing RandomState.
+      // A retried step re-runs next_goal on the state the failed call restored (the loop
+      // below just goes on); a retried reset first resets the physics (mj_resetData)
+      if (att > 0 && att % P.max_reject == 0) {
+        if (++fails >= DX_GOAL_RETRIES) break;  // bounded here (the reference loops forever)
+        if (need & 2) {
+          for (int i = LANE; i < c.nv; i += DX_WAVE) { c.f(c.L.qvel)[i] = 0.f; ws[i] = 0.f; }
+          time = 0.f;
+          SYNC();
+        }
+      }
+      const int a = att;
       // qpos_desired ~ N(midrange, scale * range), clipped to the joint range
       if (npy) {
         MtWave w = mtw_begin(mt_block, mt_sm);
         const double q = mtw_normal(w, nq, ld64(jl), ld64(nq + jl), mt_pairs);
         if (LANE < nq) qpos[LANE] = (float)fmin(ld64(3 * nq + jl), fmax(ld64(2 * nq + jl), q));
       } else if (LANE < nq) {
-        int draw = 0x100000 + (((g & 4095) * 128 + (a & 127)) * 64 + LANE) * 2;
+        const int draw = (int)(0x100000u + (((uint32_t)(g & 4095) * 128u + (uint32_t)(a & 127)) * 64u + LANE) * 2u +
+                               ((uint32_t)a >> 7) * 0x4000000u);
         float u1 = dx_urand(P.seed, P.env0 + env, ep, draw), u2 = dx_urand(P.seed, P.env0 + env, ep, draw + 1);
         float z = sqrtf(-2.0f * logf(fmaxf(u1, 1e-12f))) * cosf(6.283185307179586f * u2);
         float l = lo[LANE], h = hi[LANE];
@@ -2622,12 +2638,13 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
     if (LANE < 3 * P.ntips) T.goal[(size_t)env * P.goal_dim + LANE] = gc;
     if (LANE == 0) {
       T.goalnum[env] = g + 1;
-      if (!ok) T.goalfail[env] += 1;  // the reference raises GoalInitializationError here
+      T.goalfail[env] += fails + (ok ? 0 : 1);  // GoalInitializationErrors the reference raised (and retried)
       // GoalTask.initialize_episode / before_step bookkeeping (task.py:137-165)
       T.counter[env] = 0;
       T.exceeded[env] = 0;
       T.registered[env] = 0;
       T.solve_start[env] = time;
+      T.solve_n[env] = (int)rintf(time / c.mdl().timestep);  // fp64 start: dx_task_post_kernel
     }
     if (LANE < nq) qpos[LANE] = q_init;
     if (LANE < nu) ctrl[LANE] = c_init;

@@ -113,6 +113,10 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
     S.exceeded[env] = 0;
     S.failure[env] = 0;
     S.solve_start[env] = 0;
+    S.time_d[env] = 0.0;
+    S.nsub_d[env] = 0;
+    S.solve_start_d[env] = 0.0;
+    S.solve_n[env] = -1;
     S.skip[env] = 1;
     return;
   }
@@ -124,6 +128,7 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
       S.counter[env] = 0;
       S.exceeded[env] = 0;
       S.solve_start[env] = B.time[env];
+      S.solve_start_d[env] = S.time_d[env];
       S.registered[env] = 0;
     } else {
       S.need[env] = 1;  // next_goal and the bookkeeping run in the sampling pass
@@ -185,12 +190,27 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
       S.reward[env] = 0;
       S.discount[env] = 0;
     } else {
+      // physics time in fp64, as MuJoCo accumulates d->time (time += h per mj_step): the
+      // fp32 batch time rounds to the substeps taken since the reset, and the fp64 sum
+      // is advanced by that many additions (the reach sampling pass's accepted rollouts
+      // included); the goal's start time is taken at the substep the pass recorded
+      const int n_now = (int)rintf(B.time[env] / (float)P.h_d);
+      int n = S.nsub_d[env];
+      double time = S.time_d[env];
+      const int sn = S.solve_n[env];
+      if (sn >= 0 && sn <= n) S.solve_start_d[env] = time;
+      for (; n < n_now; n++) {
+        time = __dadd_rn(time, P.h_d);
+        if (n + 1 == sn) S.solve_start_d[env] = time;
+      }
+      S.solve_n[env] = -1;
+      S.nsub_d[env] = n;
+      S.time_d[env] = time;
       // GoalTask.after_step (task.py:167-185)
-      float time = B.time[env];
       if (all_close) {
         S.counter[env] += 1;
         if (!S.registered[env]) { S.successes[env] += 1; S.registered[env] = 1; }
-      } else if (P.max_time > 0 && time - S.solve_start[env] > P.max_time) {
+      } else if (P.max_time_d > 0 && time - S.solve_start_d[env] > P.max_time_d) {
         S.exceeded[env] = 1;
       }
       // ReOrient.after_step: fall detection (prop-ground contact at the new state)
@@ -199,7 +219,7 @@ extern "C" __global__ void dx_task_post_kernel(TaskParams P, TaskState S, DevBat
       bool success_done = S.successes[env] >= P.successes_needed;
       // composer.Environment.step: should_terminate_episode or time >= time_limit
       // (a time-limit truncation keeps the task's discount)
-      bool terminate = success_done || S.exceeded[env] || failure || time >= P.time_limit;
+      bool terminate = success_done || S.exceeded[env] || failure || time >= P.time_limit_d;
       float r;
       if (reach) {
         r = rsum / (float)P.ntips;

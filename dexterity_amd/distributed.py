@@ -60,8 +60,22 @@ def gathered_rows(rank: int, n_per_rank: int) -> slice:
 
 
 def job_key() -> str:
-    """Same string on every rank of one launcher job, different across jobs."""
-    return f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}"
+    """Same string on every rank of one launcher attempt, different across jobs and
+    across the elastic restarts of one job (torchrun keeps MASTER_PORT and the agent
+    pid over --max-restarts, so the restart count and run id are part of the key: a
+    rank of a new attempt never reads an id file a failed attempt left behind)."""
+    attempt = os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")
+    run = "".join(ch for ch in os.environ.get("TORCHELASTIC_RUN_ID", "") if ch.isalnum())[:32]
+    return f"{os.environ.get('MASTER_PORT', '0')}_{os.getppid()}_{attempt}_{run}"
+
+
+def check_single_node() -> None:
+    """The id file lives in this node's temp directory: every rank must be on one node."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != local:
+        raise RuntimeError(f"WORLD_SIZE {world} != LOCAL_WORLD_SIZE {local}: the communicator bootstrap "
+                           "(a node-local id file) supports one node")
 
 
 def exchange_id(rank: int, key: str, make_id: Callable[[], bytes], timeout: float = 120.0,
@@ -74,6 +88,10 @@ def exchange_id(rank: int, key: str, make_id: Callable[[], bytes], timeout: floa
     directory = directory or tempfile.gettempdir()
     path = os.path.join(directory, f"dx_comm_{key}.id")
     if rank == 0:
+        try:  # never leave an older id where a reader could take it
+            os.remove(path)
+        except FileNotFoundError:
+            pass
         data = bytes(make_id())
         tmp = f"{path}.{os.getpid()}.tmp"
         with open(tmp, "wb") as f:
@@ -125,6 +143,7 @@ class Comm:
 
     @classmethod
     def from_env(cls, device: Optional[int] = None) -> "Comm":
+        check_single_node()
         rank = int(os.environ.get("RANK", "0"))
         world = int(os.environ.get("WORLD_SIZE", "1"))
         local = int(os.environ.get("LOCAL_RANK", "0"))

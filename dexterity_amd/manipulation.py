@@ -252,8 +252,9 @@ class GoalEnvironment:
         # job, dexterity_amd.distributed.env_shard); it draws from seed + env_offset + e
         self.env_offset = int(env_offset)
         # composer.Environment(time_limit=..., strip_singleton_obs_buffer_dim=...)
-        # (manipulation/__init__.py:81-86); the tasks' own time_limit is inf
-        self.time_limit = float("inf") if time_limit is None else float(time_limit)
+        # (manipulation/__init__.py:81-86): `time_limit or task.time_limit`, so None and 0
+        # both mean the task's own limit, inf for every suite task
+        self.time_limit = float(time_limit) if time_limit else float("inf")
         self.strip_singleton_obs_buffer_dim = bool(strip_singleton_obs_buffer_dim)
         self.model = physics_lib.Model(task.compiled)
         L = _lib.load()
@@ -275,6 +276,8 @@ class GoalEnvironment:
         self._dev_action = self._out(-1)
         if np.isfinite(self.time_limit):
             _lib.check(L.dx_env_set_time_limit(self.ptr, self.time_limit))
+        # max_time_per_goal in fp64 (the params carry it as a float)
+        _lib.check(L.dx_env_set_goal_time_limit(self.ptr, float(task.config.max_time_per_goal)))
 
     def close(self):
         if getattr(self, "physics", None) is not None:
@@ -333,9 +336,6 @@ class GoalEnvironment:
     def _read(self, which: int, dtype, width: int) -> np.ndarray:
         out = np.empty((self.num_envs, width), dtype=dtype)
         ptr = self._out(which)
-        L = _lib.load()
-        stream = L.dx_stream(self.physics.ptr)
-        del stream
         self.physics.sync()
         _copy_d2h(out, ptr)
         return out

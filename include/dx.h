@@ -235,11 +235,18 @@ int dx_env_step(dx_env* e, const float* action);
 /* composer.Environment's time_limit (manipulation/__init__.py:61,83): an episode also
  * ends (LAST, with the task's discount) once its physics time reaches `seconds`.
  * Default: none (task.time_limit = inf). */
-int dx_env_set_time_limit(dx_env* e, float seconds);
+int dx_env_set_time_limit(dx_env* e, double seconds);
+/* max_time_per_goal (task.py:120-135, 180-183) in fp64; default: the float in the task
+ * params.  Both limits compare against the env's time accumulated in fp64 as MuJoCo
+ * accumulates d->time (one += timestep per physics step), so a limit on a control-step
+ * boundary ends the episode at the same step as the reference. */
+int dx_env_set_goal_time_limit(dx_env* e, double seconds);
 /* Device pointers of the outputs: obs [nenv][obs_dim] f32, reward/discount [nenv] f32,
  * step_type [nenv] i32 (0 FIRST, 1 MID, 2 LAST), goal [nenv][goal_dim] f32, successes i32,
- * goal failures i32 (reach goals that exhausted the rejection samples: the reference
- * raises GoalInitializationError there, fingertip_position.py:118-122). */
+ * goal failures i32 (the GoalInitializationErrors the reference would have raised: goal
+ * draws that exhausted max_rejection_samples, fingertip_position.py:112-117; like
+ * GoalEnvironment, environment.py:14-34, the env retries -- the step's goal draw, or the
+ * whole reset -- from its continuing RandomState, up to 64 times per goal). */
 int dx_env_output(dx_env* e, int which, void** devptr);
 /* Library-owned [nenv][nu] device action buffer, and a fill of it with actions
  * drawn uniformly within each actuator's ctrlrange (the random agent of
@@ -289,9 +296,9 @@ int dx_jac_site(dx_batch* b, const int32_t* sites, int32_t nsite, float* jacp, f
  * joints to their range, and re-runs kinematics, for at most max_steps steps
  * (ik_solver.py:169-236; early stop when every site is within linear_tol, abort
  * when error / progress > progress_threshold for any site).  Attempt 0 starts the
- * solved joints at their midrange, attempt a > 0 uniformly within their range
- * (counter-based RNG keyed by (seed, env, a); the reference draws from numpy's
- * global stream, so individual random starts are not seed-identical); the other
+ * solved joints at their midrange, attempt a > 0 at numpy's a-th
+ * np.random.uniform(*range.T) over the passed joints (ik_solver.py:127-130), env e
+ * replaying a global stream seeded np.random.seed(seed + e) bit for bit; the other
  * qpos entries come from the batch.  The attempts run in parallel, one wavefront
  * each; the selection follows ik_solver.py:132-152: among attempts with every
  * error <= linear_tol, the first one (stop_on_first_successful_attempt) or the one

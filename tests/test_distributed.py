@@ -157,4 +157,26 @@ def test_id_exchange_times_out(tmp_path):
 
 def test_job_key_is_shared_by_launcher_children(monkeypatch):
     monkeypatch.setenv("MASTER_PORT", "29511")
-    assert distributed.job_key() == f"29511_{os.getppid()}"
+    monkeypatch.delenv("TORCHELASTIC_RESTART_COUNT", raising=False)
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    assert distributed.job_key() == f"29511_{os.getppid()}_0_"
+    # an elastic restart of the same job gets a fresh key (no stale id is read)
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "1")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "abc-123")
+    assert distributed.job_key() == f"29511_{os.getppid()}_1_abc123"
+
+
+def test_single_node_check(monkeypatch):
+    monkeypatch.setenv("WORLD_SIZE", "16")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    with pytest.raises(RuntimeError):
+        distributed.check_single_node()
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "16")
+    distributed.check_single_node()
+
+
+def test_rank0_replaces_stale_id(tmp_path):
+    key = "stale"
+    (tmp_path / f"dx_comm_{key}.id").write_bytes(b"old")
+    got = distributed.exchange_id(0, key, lambda: b"new", directory=str(tmp_path))
+    assert got == b"new" and (tmp_path / f"dx_comm_{key}.id").read_bytes() == b"new"

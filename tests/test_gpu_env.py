@@ -194,6 +194,56 @@ def test_time_limit(built):
     env.close()
 
 
+def _fp64_time_steps(limit, h, nsub, strict=False):
+    """Control step (1-based) at which MuJoCo's fp64 time (time += h per physics step)
+    first reaches `limit` (composer's time >= time_limit) or exceeds it (strict: the
+    per-goal test time - start > max_time_per_goal)."""
+    t, k = 0.0, 0
+    while True:
+        k += 1
+        for _ in range(nsub):
+            t += h
+        if (t > limit) if strict else (t >= limit):
+            return k
+
+
+@pytest.mark.parametrize("limit", [0.05, 0.25, 1.05])
+def test_time_limit_on_control_step_boundary(built, limit):
+    """A time limit that is an exact multiple of the control step ends the episode at the
+    step fp64 time accumulation gives (MuJoCo's d->time, compared by composer as
+    time >= time_limit): 0.05 is reached only after the 3rd control step (the fp64 sum of
+    ten 0.005 steps is 0.049999...), 0.25 after the 10th.  An fp32 running time would end
+    the 0.25 episode one step late."""
+    from dexterity_amd import manipulation
+
+    cfg = manipulation.ReOrientConfig(fall_termination=False)
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(cfg), num_envs=8, seed=4, time_limit=limit)
+    k = _fp64_time_steps(limit, cfg.physics_timestep, cfg.n_sub_steps)
+    env.reset()
+    rec = _run(env, k + 1)
+    for i in range(k - 1):
+        assert np.all(rec[i]["st"] == 1), (limit, i, k)
+    assert np.all(rec[k - 1]["st"] == 2), (limit, k)
+    assert np.all(rec[k]["st"] == 0)
+    env.close()
+
+
+def test_goal_time_limit_on_control_step_boundary(built):
+    """max_time_per_goal = 2 control steps (0.05 s): GoalTask's time - start > max_time
+    in fp64 is first true after the 3rd step (task.py:180-183)."""
+    from dexterity_amd import manipulation
+
+    cfg = manipulation.ReOrientConfig(max_steps_single_solve=2, fall_termination=False, orientation_threshold=0.0)
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(cfg), num_envs=8, seed=5)
+    k = _fp64_time_steps(cfg.max_time_per_goal, cfg.physics_timestep, cfg.n_sub_steps, strict=True)
+    assert k == 3
+    env.reset()
+    rec = _run(env, k + 1)
+    assert all(np.all(rec[i]["st"] == 1) for i in range(k - 1))
+    assert np.all(rec[k - 1]["st"] == 2) and np.all(rec[k - 1]["disc"] == 1.0)
+    env.close()
+
+
 def test_goal_change_after_successes(built):
     """GoalTask.before_step / after_step (task.py:154-185): with every step a success
     (threshold above any orientation distance), the success counter passes
@@ -371,8 +421,8 @@ def test_collision_free_joint_sampling_kat(built, oracle_mod):
     env.close()
 
 
-@pytest.mark.parametrize("domain", ["reach", "reach_shadow"])
-def test_reach_resets_replay_numpy_random_state(built, domain):
+@pytest.mark.parametrize("domain,max_reject", [("reach", 100), ("reach_shadow", 100), ("reach", 1), ("reach", 2)])
+def test_reach_resets_replay_numpy_random_state(built, domain, max_reject):
     """Seed-level reset parity for reach: env e's RandomState(seed + e)
     feeds, in the reference's order, the goal sampler -- random_state.normal(midrange,
     0.1 range) per rejection attempt (fingertip_position.py:79-86, numpy's polar
@@ -384,18 +434,28 @@ def test_reach_resets_replay_numpy_random_state(built, domain):
     from dexterity_amd import _lib, hands, manipulation
 
     seed, n = 4321, 64
-    env = manipulation.load(domain, "state_dense", seed=seed, num_envs=n)
+    if max_reject == 100:
+        env = manipulation.load(domain, "state_dense", seed=seed, num_envs=n)
+    else:
+        # forced GoalInitializationErrors: with 1 or 2 rejection samples per next_goal
+        # call most resets raise and are retried (environment.py:14-34); the retries
+        # continue the env's RandomState, so the replay below is unchanged
+        cfg = manipulation.ReachConfig(max_rejection_samples=max_reject)
+        env = manipulation.GoalEnvironment(manipulation.Reach(cfg, hand="adroit"), num_envs=n, seed=seed)
     t = env.task
     lo, hi = t.joint_range[:, 0], t.joint_range[:, 1]
     mid = t.joint_range.mean(axis=1)
     frac = t.config.init_joint_range_fraction
     env.reset()
     qpos = env.physics.get(_lib.QPOS)
-    assert np.all(env.goal_failures() == 0)
+    fails = env.goal_failures()
     attempts = []
     for e in range(n):
         found = None
-        for kg in range(1, t.config.max_rejection_samples + 1):  # goal attempts
+        # goal attempts: the accepted draw follows fails[e] exhausted batches of max_reject
+        # (one GoalInitializationError each), so it is draw fails * max_reject + 1 .. + max_reject
+        kgs = range(1, 101) if max_reject == 100 else range(fails[e] * max_reject + 1, (fails[e] + 1) * max_reject + 1)
+        for kg in kgs:
             rs = np.random.RandomState(seed + e)
             for _ in range(kg):
                 rs.normal(loc=mid, scale=t.config.goal_scale * (hi - lo))
@@ -409,9 +469,13 @@ def test_reach_resets_replay_numpy_random_state(built, domain):
             if len(hit):
                 found = (kg, int(hit[0]) + 1)
                 break
-        assert found is not None, e
+        assert found is not None, (e, fails[e])
         attempts.append(found)
+        if max_reject == 100:
+            assert fails[e] == 0
     assert max(a[0] for a in attempts) >= 1
+    if max_reject < 100:
+        assert max(a[0] for a in attempts) > max_reject and fails.sum() > 0  # the retry path ran
     if domain == "reach_shadow":  # contacts disabled: every first draw is accepted
         assert all(a == (1, 1) for a in attempts)
     env.close()

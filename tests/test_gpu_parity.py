@@ -127,9 +127,15 @@ def _load_states(gpu, model, xfrc, states):
     return phys
 
 
+def _normal_tol(dist):
+    """Normal tolerance of a contact at depth |dist| (see _contact_tie), capped at 0.05 rad
+    so a very shallow contact cannot excuse an arbitrary normal."""
+    return min(0.05, max(2e-3, 1e-7 / max(abs(dist), 1e-12)))
+
+
 def _contact_match(r, o):
     return (abs(r[12] - o[12]) < 2e-5 and np.abs(r[0:3] - o[0:3]).max() < 2e-4
-            and np.abs(r[3:6] - o[3:6]).max() < max(2e-3, 1e-7 / max(abs(o[12]), 1e-12)))
+            and np.abs(r[3:6] - o[3:6]).max() < _normal_tol(o[12]))
 
 
 def _contact_tie(cm, ds, r):
@@ -162,7 +168,7 @@ def _contact_tie(cm, ds, r):
     assert abs(r[12] - o[12]) < 2e-5
     tie = False
     nerr = np.abs(r[3:6] - o[3:6]).max()
-    if nerr >= max(2e-3, 1e-7 / max(abs(o[12]), 1e-12)):
+    if nerr >= _normal_tol(o[12]):
         assert nerr < 0.05
         assert _separation(cm, d, int(o[13]), int(o[14]), r[3:6]) - o[12] > -5e-4
         tie = True
@@ -207,14 +213,34 @@ def _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
         degenerate += ties > 0
         assert n == d.nefc
         ncontact_states += len(oc) > 0
+        # qacc from one oracle pass (either side of an MPR discontinuity, _oracle_pair)
+        err = min((np.abs(qacc[e] - dd.qacc) for dd in ds), key=lambda x: x.max())
+        sc = max(1.0, scale)
         if ties == 0:
             # the cube's own six dofs get the bimanual test's 3e-3: a shallow contact's
             # normal carries the fp32 error of _contact_tie (5e-3 rad at 11 um), which
             # tilts that contact's force and the cube's angular acceleration with it
-            err = np.minimum(np.abs(qacc[e] - ds[0].qacc), np.abs(qacc[e] - ds[1].qacc))
-            assert err[: cm.nv - 6].max() <= 5e-4 * max(1.0, scale), f"env {e}"
-            assert err[cm.nv - 6 :].max() <= 3e-3 * max(1.0, scale), f"env {e}"
+            assert err[: cm.nv - 6].max() <= 5e-4 * sc, f"env {e}"
+            assert err[cm.nv - 6 :].max() <= 3e-3 * sc, f"env {e}"
+        else:
+            # a tied contact sits elsewhere on the shared face (or on a neighbouring
+            # Minkowski face): its force acts at another point, so the accelerations are
+            # held to a looser bound instead of being skipped
+            TIE_ERR.append(float(err.max() / sc))
+            assert err[: cm.nv - 6].max() <= TIE_QACC_HAND * sc, (f"tie env {e}", err.max() / sc)
+            assert err[cm.nv - 6 :].max() <= TIE_QACC_CUBE * sc, (f"tie env {e}", err.max() / sc)
     return ncontact_states, degenerate
+
+
+# Tie states (_contact_tie): qacc within these fractions of max(1, |qacc_smooth|) --
+# hand dofs / cube dofs -- and one-substep qpos within TIE_QPOS.  Their errors are
+# recorded here and printed by the wide-sample test.
+# Measured (r3, test_forward_and_substep_parity_wide_sample's output): one tie state in
+# 63, its qacc error 1.3e-3 of the scale, its one-step errors qpos 3e-7 / qvel 6e-6.
+TIE_QACC_HAND, TIE_QACC_CUBE, TIE_QPOS = 5e-3, 2e-2, 1e-5
+TIE_ERR, TIE_STEP_ERR = [], []
+# states with a tie, at most, over the wide sample of 63 states (measured: 1)
+WIDE_TIES_MAX = 3
 
 
 def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
@@ -225,7 +251,7 @@ def test_forward_parity_reorient(gpu, oracle_mod, reorient_setup):
 
 
 def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
-    # states with a contact tie (_contact_tie) are excluded from the tight one-step
+    # states with a contact tie (_contact_tie) get the looser tie bound in the one-step
     # comparison
     probe = _load_states(gpu, model, xfrc, states)
     probe.debug(True)
@@ -242,8 +268,6 @@ def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
     phys.step(1)
     qpos, qvel = phys.qpos, phys.qvel
     for e, st in enumerate(states):
-        if e in skip:
-            continue
         errs = []
         for x, y in ((xfrc, st), (np.asarray(xfrc, dtype=np.float32).astype(np.float64), _f32(st))):
             d = oracle_mod.OracleData(om)
@@ -252,8 +276,12 @@ def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
             d.step()
             errs.append((np.abs(qpos[e] - d.qpos).max(),
                          np.abs(qvel[e] - d.qvel).max() / max(1.0, np.abs(d.qacc_smooth).max())))
-        # either side of an MPR discontinuity (_oracle_pair): qpos 1e-6, qvel 5e-4 of the scale
-        assert min(q for q, _ in errs) < 1e-6 and min(v for _, v in errs) < 5e-4, errs
+        # either side of an MPR discontinuity (_oracle_pair), qpos and qvel from the same
+        # pass: qpos 1e-6, qvel 5e-4 of the scale (a tie state: the looser tie bounds)
+        qt, vt = (TIE_QPOS, TIE_QACC_CUBE) if e in skip else (1e-6, 5e-4)
+        if e in skip:
+            TIE_STEP_ERR.append(min(errs, key=lambda qv: qv[0]))
+        assert any(q < qt and v < vt for q, v in errs), (e, e in skip, errs)
     return skip
 
 
@@ -270,9 +298,11 @@ def test_forward_and_substep_parity_wide_sample(gpu, oracle_mod, reorient_setup)
     om, states = _oracle_states(oracle_mod, cm, xfrc, n_traj=20, seed=7)
     ncontact_states, degenerate = _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model)
     assert ncontact_states >= 40
-    assert degenerate <= len(states) // 6
     skip = _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model)
-    assert len(skip) <= len(states) // 6
+    print(f"tie states: forward {degenerate} / substep {len(skip)} of {len(states)}; "
+          f"tie qacc errors (of scale) {sorted(round(x, 5) for x in TIE_ERR)}; "
+          f"tie one-step (qpos, qvel) errors {[(float(f'{q:.2e}'), float(f'{v:.2e}')) for q, v in TIE_STEP_ERR]}")
+    assert degenerate <= WIDE_TIES_MAX and len(skip) <= WIDE_TIES_MAX
 
 
 def test_contact_free_trajectory_parity(gpu, oracle_mod):
@@ -706,8 +736,39 @@ def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):
         assert err_cg <= 5e-4 * scale, (e, err_cg, scale)
         assert err_nt <= 5e-4 * scale
     phys.close()
-    # MuJoCo's defaults (100 iterations, 1e-8) with CG: the reorient batch steps
-    phys = _load_states(gpu, gpu.Model(cm.with_solver("CG")), xfrc, states)
-    phys.step(10)
-    assert np.all(np.isfinite(phys.qpos))
-    phys.close()
+    # MuJoCo's defaults (100 iterations, 1e-8) with CG on both sides: kernel CG vs the
+    # oracle's CG at identical settings, one substep and three, per state
+    cgd = cm.with_solver("CG")
+    om_d = oracle_mod.OracleModel(blob.pack(cgd.arrays))
+    for nsub in (1, 3):
+        phys = _load_states(gpu, gpu.Model(cgd), xfrc, states)
+        phys.step(nsub)
+        qpos, qvel = phys.qpos, phys.qvel
+        assert np.all(np.isfinite(qpos))
+        eq, ev = [], []
+        for e, st in enumerate(states):
+            best = None
+            for x, y in ((xfrc, st), (np.asarray(xfrc, dtype=np.float32).astype(np.float64), _f32(st))):
+                d = oracle_mod.OracleData(om_d)
+                d.xfrc_applied[:] = x.ravel()
+                d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = y
+                for _ in range(nsub):
+                    d.step()
+                sc = max(1.0, np.abs(d.qacc_smooth).max())
+                q, v = np.abs(qpos[e] - d.qpos).max(), np.abs(qvel[e] - d.qvel).max() / sc
+                best = (q, v) if best is None or q < best[0] else best
+            eq.append(best[0])
+            ev.append(best[1])
+        eq, ev = np.array(eq), np.array(ev)
+        print(f"CG defaults, {nsub} substep(s): |qpos| err median {np.median(eq):.2e} max {eq.max():.2e}; "
+              f"|qvel|/scale median {np.median(ev):.2e} max {ev.max():.2e}")
+        assert np.median(eq) <= 1e-6 and eq.max() <= CG_QPOS_MAX * nsub
+        assert np.median(ev) <= 1e-5 and ev.max() <= CG_QVEL_MAX
+        phys.close()
+
+
+# CG at MuJoCo's defaults stops after 100 iterations or at 1e-8 on a linearly converging
+# path that fp32 and fp64 walk differently.  Measured (r3) over the contact-rich states:
+# qpos median 9e-8 / max 2.1e-6 (1 substep), 5.9e-5 (3 substeps); qvel / scale median
+# 1.1e-6, max 2.8e-5
+CG_QPOS_MAX, CG_QVEL_MAX = 4e-5, 1e-4

@@ -17,6 +17,7 @@ early_stop; the stall exit fires on rounding noise once a fingertip is parked, s
 fp32 and fp64 can leave at different steps).
 """
 
+import ctypes
 import os
 
 import numpy as np
@@ -290,3 +291,36 @@ def test_ik_selection_rule(gpu, oracle_mod, adroit, adroit_solver):
     # the same seed gives the same attempts: a rerun is bit-identical
     again = adroit_solver.solve_batch(targets, num_attempts=8, seed=5)
     np.testing.assert_array_equal(again.qpos, best.qpos)
+
+
+@pytest.mark.gpu
+def test_ik_restarts_replay_numpy_global_stream(gpu, adroit, adroit_solver):
+    """IKSolver.solve's random restarts (ik_solver.py:127-130): attempt a >= 1 starts at
+    the a-th np.random.uniform(*range.T) of numpy's global stream; env e is the process
+    that called np.random.seed(seed + e).  With a zero velocity gain no attempt moves and
+    none succeeds (targets out of reach), so the returned joints -- the last attempt's --
+    are that attempt's start, which must equal numpy's draw bit for bit after the fp32
+    cast."""
+    from dexterity_amd import _lib
+
+    cm, _, sites, joints = adroit
+    B = adroit_solver.num_envs
+    lo, hi = np.asarray(cm.jnt_range, dtype=np.float64)[joints].T
+    s = np.asarray(sites, dtype=np.int32)
+    j = np.asarray(joints, dtype=np.int32)
+    t = np.full((B, 3 * len(s)), 10.0, np.float32)
+    seed = 12345
+    for A in (2, 3, 7):
+        opt = _lib.IkOptions(1e-3, 1e-5, 0.0, 20.0, 1, 0, A, 0, seed)
+        q = np.zeros((B, len(j)), np.float32)
+        ok = np.zeros(B, np.int32)
+        att = np.zeros(B, np.int32)
+        _lib.check(_lib.load().dx_ik_solve(adroit_solver.physics.ptr, ctypes.byref(opt), s.ctypes.data, len(s),
+                                           j.ctypes.data, len(j), t.ctypes.data, q.ctypes.data, ok.ctypes.data,
+                                           None, att.ctypes.data, None))
+        assert not ok.any() and np.all(att == A - 1)
+        for e in range(B):
+            np.random.seed(seed + e)
+            for _ in range(A - 1):
+                start = np.random.uniform(lo, hi)
+            np.testing.assert_array_equal(q[e], start.astype(np.float32), err_msg=f"env {e} attempt {A - 1}")

@@ -76,7 +76,7 @@ def test_reorient_outcome_statistics(oracle_mod):
         if k == 0:
             err = np.abs(q_g - q_o).max(axis=1)
             print(f"step 1 |qpos| error: median {np.median(err):.2e}, p95 {np.percentile(err, 95):.2e}")
-            assert np.median(err) <= 1e-4 and np.percentile(err, 95) <= 1e-2
+            assert np.median(err) <= 1e-6 and np.percentile(err, 95) <= 1e-5
         z_g.append(q_g[:, 26])
         z_o.append(q_o[:, 26].copy())
         r_g.append(_rewards(task_ref, goals, q_g, ctrls[k]))

@@ -1,0 +1,30 @@
+"""Build a variant libdx.so for same-box A/B runs (tools/ab_lib.sh):
+
+  python tools/build_variant.py NAME [-DFOO=1 ...]
+
+copies dexterity_amd/csrc to variants/NAME/csrc, builds it there with the extra flags
+(and its own scene specializations) into variants/NAME/libdx.so.  Run the bench with
+DX_LIB=variants/NAME/libdx.so."""
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from dexterity_amd import build as B  # noqa: E402
+
+name, extra = sys.argv[1], tuple(sys.argv[2:])
+vdir = os.path.join(ROOT, "variants", name)
+src = os.path.join(vdir, "csrc")
+if os.path.exists(src):
+    shutil.rmtree(src)
+shutil.copytree(B.CSRC, src)
+# csrc includes "../../include/dx.h"
+os.makedirs(os.path.join(ROOT, "variants", "include"), exist_ok=True)
+shutil.copy(os.path.join(ROOT, "include", "dx.h"), os.path.join(ROOT, "variants", "include", "dx.h"))
+B.CSRC = src
+B.SPECS = os.path.join(src, "dx_specs.inc")
+B.OUT = os.path.join(vdir, "libdx.so")
+B.OBJ = os.path.join(vdir, "obj")
+B.FLAGS = B.FLAGS + extra
+print(B.build(force=True, verbose=False))

@@ -1,6 +1,10 @@
+#!/bin/bash
+# On the GPU box: targeted tests (-k $K), then the whole -m gpu suite.
 set -o pipefail
-cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_health.py tests/test_gpu_env.py -k "health or shard or nan or overflow" > gpurun_out/t_new.log 2>&1 || { echo "new tests failed"; exit 1; }
-timeout -k 10 200 python -u tools/ncon_histogram.py 4096 500 > gpurun_out/ncon.log 2>&1 || exit 2
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/t_all.log 2>&1 || { echo "suite failed"; exit 3; }
-bash tools/pmc_mix.sh > gpurun_out/mix_run.log 2>&1
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+mkdir -p gpurun_out
+if [ -n "$K" ]; then
+  timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests -m gpu -k "$K" > gpurun_out/t_new.log 2>&1 || { echo "targeted tests failed"; exit 1; }
+fi
+timeout -k 10 900 python -u -m pytest -q --timeout 120 --timeout-method thread tests -m gpu > gpurun_out/t_all.log 2>&1 || { echo "suite failed"; tail -5 gpurun_out/t_all.log; exit 3; }
+tail -2 gpurun_out/t_all.log
