@@ -61,10 +61,13 @@ def host_threads() -> int:
     return max(1, n)
 
 
-def oracle_flops_per_env_step(states, nsub: int) -> float:
+def oracle_flops_per_env_step(states, nsub: int):
     """FLOPs of one control step on the oracle's per-stage counters, averaged over
     environment states sampled from the GPU batch at the end of the timed region (so
-    the contact mix is the bench workload's)."""
+    the contact mix is the bench workload's).  Returns the per-stage counts per
+    env-step (oracle.STAGES): the algorithmic count is every stage but "scan", the
+    surplus of the oracle's exhaustive mesh-support scan over an efficient support's
+    16 vertices (DXO_ST_SCAN in oracle/dx_oracle.c)."""
     import numpy as np
 
     from dexterity_amd import blob
@@ -79,7 +82,7 @@ def oracle_flops_per_env_step(states, nsub: int) -> float:
     qpos, qvel, ws, ctrl = (np.asarray(a, dtype=np.float64) for a in states)
     fl = []
     O.batch_step(om, qpos, qvel, ctrl, ws, xfrc, nsub=nsub, nthreads=host_threads(), flops=fl)
-    return fl[0] / qpos.shape[0]
+    return dict(zip(O.STAGES, (float(v) for v in fl[0] / qpos.shape[0])))
 
 
 def cpu_baseline(seconds: float, threads: int, states, nsub: int):
@@ -124,9 +127,10 @@ def cpu_baseline(seconds: float, threads: int, states, nsub: int):
     }
 
 
-def cpu_baseline_reach_1env(seconds: float):
-    """BASELINE.json config 1: reach (Adroit hand, the reference task's hand), 1 env,
-    1 thread, dt 0.02 x 1 substep, uniform random actions (manipulation_test.py:44-45)."""
+def cpu_baseline_reach_1env(seconds: float, hand: str = "adroit"):
+    """BASELINE.json config 1: reach, 1 env, 1 thread, dt 0.02 x 1 substep, uniform
+    random actions (manipulation_test.py:44-45); the Adroit hand is the reference task's
+    hand (reach.py:231), the Shadow hand is BASELINE.md's naming (contacts disabled)."""
     import numpy as np
 
     from dexterity_amd import blob
@@ -134,10 +138,11 @@ def cpu_baseline_reach_1env(seconds: float):
     from dexterity_amd.physics import gravity_compensation
     from oracle import oracle as O
 
-    cm = CompiledModel.load(os.path.join(ROOT, "assets", "adroit_reach.npz"))
+    asset, prefix = {"adroit": ("adroit_reach.npz", "adroit_hand/"), "shadow": ("shadow_reach.npz", "shadow_hand_e/")}[hand]
+    cm = CompiledModel.load(os.path.join(ROOT, "assets", asset))
     om = O.OracleModel(blob.pack(cm.arrays))
     d = O.OracleData(om)
-    d.xfrc_applied[:] = gravity_compensation(cm, "adroit_hand/").ravel()
+    d.xfrc_applied[:] = gravity_compensation(cm, prefix).ravel()
     lo, hi = cm.actuator_ctrlrange.T
     rng = np.random.RandomState(12345)
     steps = 0
@@ -152,7 +157,7 @@ def cpu_baseline_reach_1env(seconds: float):
         "unit": "env-steps/sec",
         "cores": 1,
         "kind": "port",
-        "sample": f"config 1: fp64 C oracle, reach (Adroit hand), 1 env, 1 thread, {steps} control steps "
+        "sample": f"config 1: fp64 C oracle, reach ({hand.capitalize()} hand), 1 env, 1 thread, {steps} control steps "
         f"(1 substep each, dt 0.02), random ctrl, {dt:.1f} s (Python call per step included)",
     }
 
@@ -186,6 +191,7 @@ def main():
     env.physics.sync()
     if comm:
         comm.barrier()
+    env.physics.health_clear()  # the timed region's own health counters
     _lib.check(L.dx_timing_enable(env.physics.ptr, 1))
     _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int32())))
     t0 = time.perf_counter()
@@ -200,21 +206,39 @@ def main():
     _lib.check(L.dx_timing_enable(env.physics.ptr, 0))
     # a substep-queue timeout would mean corrupted hand-offs: no number is reported then
     qerr = env.physics.debug_get("queue_timeouts")
-    if int(qerr[0]) != 0:
-        raise SystemExit("substep queue timed out during the timed region; refusing to report")
+    refuse = "substep queue timed out during the timed region" if int(qerr[0]) != 0 else ""
+    # health of the timed region (include/dx.h dx_health): a diverged env, or a capacity
+    # overflow that truncates work (candidate lists, Jacobian dofs, constraint rows),
+    # voids the number.  Contacts beyond the 32 kept per env-substep (MuJoCo keeps up to
+    # nconmax = 200) occur at ~3.4e-6 of env-substeps on this workload (34 in 1.0e7,
+    # profiles/r3a_ncon_hist.json); they are counted and reported, and a rate 30x that
+    # voids the number too.
+    nsub = env.task.config.n_sub_steps
+    health = env.physics.health()
+    health.pop("ncon_hist")
+    env_substeps = B * args.steps * nsub
+    bad = {k: v for k, v in health.items() if k in ("diverged", "candidate_overflow", "jacobian_dof_overflow",
+                                                    "row_overflow") and v}
+    if bad or health["contact_overflow"] > 1e-4 * env_substeps:
+        refuse = refuse or f"health counters of the timed region {health}"
+    # every rank learns whether any rank refuses (no rank is left waiting in a collective)
+    if (comm.max(1.0 if refuse else 0.0) if comm else (1.0 if refuse else 0.0)) > 0:
+        raise SystemExit(f"rank {rank}: {refuse or 'another rank refused'}; refusing to report")
+    health["env_substeps"] = env_substeps
+    health["contact_overflow_rate"] = health["contact_overflow"] / env_substeps
     if comm:
         elapsed = comm.max(elapsed)
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
     kernel_ms = kt.value / max(1, kn.value)
-    nsub = env.task.config.n_sub_steps
     if rank == 0:
         import numpy as np
 
         ph = env.physics
         idx = np.linspace(0, B - 1, min(FLOP_SAMPLE_ENVS, B)).astype(int)
         sample = [ph.get(f)[idx] for f in (_lib.QPOS, _lib.QVEL, _lib.QACC_WARMSTART, _lib.CTRL)]
-        flops = oracle_flops_per_env_step(sample, nsub)
+        by_stage = oracle_flops_per_env_step(sample, nsub)
+        flops = sum(v for k, v in by_stage.items() if k != "scan")
         achieved_tf = flops * B / (kernel_ms * 1e-3) / 1e12
         achieved_gbs = ALGO_BYTES_PER_ENV_STEP * B / (kernel_ms * 1e-3) / 1e9
         traffic = None
@@ -247,6 +271,9 @@ def main():
             "data": "synthetic: random actions within ctrlrange, device RNG; cube spawn/goals per reorient.py",
             "config": {
                 "workload": "reorient.state_dense, Shadow hand + cube, full contact + Newton solver",
+                # MuJoCo's default and the only solver the reference's scenes run; CG is
+                # tools/bench_configs.py's config 3' line; PGS is not built
+                "solver": "Newton",
                 "envs_per_gpu": B,
                 "global_envs": world * B,
                 "substeps_per_env_step": nsub,
@@ -266,7 +293,11 @@ def main():
                 "kernel": "dx_step_kernel",
                 "kernel_ms_avg": round(kernel_ms, 4),
                 "flops_per_env_step": round(flops),
-                "flops_sample": f"oracle stage counters over {len(idx)} env states of the GPU batch, {nsub} substeps",
+                "flops_by_stage": {k: round(v) for k, v in by_stage.items() if k != "scan"},
+                # the oracle's exhaustive hull scans, were they counted as work
+                "flops_per_env_step_full_hull_scan": round(flops + by_stage["scan"]),
+                "flops_sample": f"oracle stage counters over {len(idx)} env states of the GPU batch, {nsub} substeps; "
+                                "a mesh support is charged 16 vertices (an efficient support), not the full hull",
                 "hbm": {
                     "achieved": round(achieved_gbs, 3),
                     "peak": HBM_PEAK_GBS,
@@ -276,6 +307,7 @@ def main():
                     "traffic": traffic,
                 },
             },
+            "health": health,
             "cpu_baseline": cpu,
             "cpu_baseline_extra": extra,
         }

@@ -793,7 +793,12 @@ static void support(const Shape* s, const double* dir, double* out, double* flop
         if (v > best) { best = v; bi = i; }
       }
       memcpy(lp, s->vert + 3 * bi, 24);
-      *flops += 5.0 * s->nvert;
+      /* 5 FLOP per vertex; an efficient support reads ~16 vertices (the kernel's binned
+         cell block; MuJoCo hill-climbs the hull graph), the rest of this exhaustive scan
+         goes to DXO_ST_SCAN (flops points at flops[DXO_ST_COL]) */
+      const int eff = s->nvert < 16 ? s->nvert : 16;
+      *flops += 5.0 * eff;
+      flops[DXO_ST_SCAN - DXO_ST_COL] += 5.0 * (s->nvert - eff);
       break;
     }
   }
@@ -1971,10 +1976,10 @@ int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos,
                            const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads,
                            double* flops) {
   int err = 0;
-  double fsum = 0;
+  double fs[DXO_NSTAGE] = {0};
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel reduction(| : err) reduction(+ : fsum)
+#pragma omp parallel reduction(| : err) reduction(+ : fs[:DXO_NSTAGE])
 #endif
   {
     dxo_data* d = dxo_data_create(m);
@@ -1992,9 +1997,9 @@ int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos,
       memcpy(qvel + (size_t)e * m->nv, d->qvel, 8 * m->nv);
       memcpy(qacc_warmstart + (size_t)e * m->nv, d->qacc_warmstart, 8 * m->nv);
     }
-    for (int k = 0; k < DXO_NSTAGE; k++) fsum += d->flops[k];
+    for (int k = 0; k < DXO_NSTAGE; k++) fs[k] += d->flops[k];
     dxo_data_free(d);
   }
-  if (flops) *flops = fsum;
+  if (flops) memcpy(flops, fs, sizeof(fs));
   return err ? -1 : 0;
 }

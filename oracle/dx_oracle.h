@@ -37,6 +37,10 @@ enum {
   DXO_ST_SMOOTH,    /* comVel, passive, RNE, actuation, qacc_smooth   */
   DXO_ST_SOLVE,     /* Newton solver                                  */
   DXO_ST_INT,       /* implicit-damping Euler                         */
+  DXO_ST_SCAN,      /* mesh supports: the full hull scan's vertices beyond the 16 an
+                       efficient support reads (a direction-binned cell block, as the
+                       kernel does, or a hill climb) -- reported apart, not part of the
+                       algorithmic count                                  */
   DXO_NSTAGE
 };
 
@@ -91,7 +95,8 @@ void dxo_flops_reset(dxo_data* d);
 int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                    const double* ctrl, double* qacc_warmstart, const double* xfrc,
                    int nthreads);
-/* Same, also returning the summed FLOP counters of all envs and substeps. */
+/* Same, also returning the FLOP counters summed over all envs and substeps, per stage
+   (flops: double[DXO_NSTAGE]). */
 int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                            const double* ctrl, double* qacc_warmstart, const double* xfrc,
                            int nthreads, double* flops);

@@ -16,8 +16,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
 _lib = None
 
-NSTAGE = 7
-STAGES = ("kinematics", "crb", "collision", "constraint", "smooth", "solver", "integrate")
+NSTAGE = 8
+STAGES = ("kinematics", "crb", "collision", "constraint", "smooth", "solver", "integrate", "scan")
 
 
 def build() -> str:
@@ -191,12 +191,13 @@ class OracleData:
 def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub: int, nthreads: int = 0,
                flops: list = None):
     """Steps nenv independent envs nsub times (OpenMP over envs). Arrays are updated in
-    place (when already contiguous float64). With `flops` (a list), appends the summed
-    FLOP count of every env and substep."""
+    place (when already contiguous float64). With `flops` (a list), appends the FLOP
+    counters summed over every env and substep, per stage (STAGES): the algorithmic
+    count is the sum without "scan" (the exhaustive mesh scan's surplus)."""
     dp = ctypes.POINTER(ctypes.c_double)
     arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (qpos, qvel, ctrl, qacc_warmstart)]
     x = None if xfrc is None else np.ascontiguousarray(xfrc, dtype=np.float64)
-    fl = ctypes.c_double(0.0)
+    fl = np.zeros(len(STAGES), dtype=np.float64)
     rc = lib().dxo_batch_step_counted(
         model.ptr,
         arrs[0].shape[0],
@@ -207,8 +208,8 @@ def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub:
         arrs[3].ctypes.data_as(dp),
         None if x is None else x.ctypes.data_as(dp),
         nthreads,
-        ctypes.byref(fl),
+        fl.ctypes.data_as(dp),
     )
     if flops is not None:
-        flops.append(fl.value)
+        flops.append(fl)
     return rc, arrs[0], arrs[1], arrs[3]

@@ -179,7 +179,24 @@ def test_flop_counters_populated(oracle_mod, reorient_compiled):
     d.flops_reset()
     d.step()
     fl = d.flops()
-    assert fl.shape == (7,) and np.all(fl[[0, 1, 4, 6]] > 0)
+    assert fl.shape == (8,) and np.all(fl[[0, 1, 4, 6]] > 0) and fl[7] >= 0
+
+
+def test_flop_counters_split_full_hull_scan(oracle_mod, reorient_compiled):
+    """Mesh supports are charged at an efficient support's 16 vertices; the exhaustive
+    scan's surplus goes to the separate "scan" stage (not algorithmic work)."""
+    from dexterity_amd.physics import gravity_compensation
+
+    m, d = _data(oracle_mod, reorient_compiled)
+    cm = reorient_compiled
+    d.xfrc_applied[:] = gravity_compensation(cm, "shadow_hand_e/").ravel()
+    d.qpos[24:27] = (0.0, -0.13, 0.16)  # the cube falls into the palm: mesh-box MPR
+    for _ in range(60):
+        d.step()
+    d.flops_reset()
+    d.step()
+    fl = d.flops()
+    assert fl[2] > 0 and fl[7] > 0
 
 
 # --------------------------------------------------------------------------- #

@@ -27,11 +27,16 @@ def _kernel_ms(L, ptr):
     return kt.value / max(1, kn.value), kn.value
 
 
-def env_config(name, domain, task, nenv, steps=50, warmup=10):
+def env_config(name, domain, task, nenv, steps=50, warmup=10, solver=None):
     from dexterity_amd import _lib, manipulation
 
     L = _lib.load()
-    env = manipulation.load(domain, task, seed=7, num_envs=nenv)
+    if solver is None:
+        env = manipulation.load(domain, task, seed=7, num_envs=nenv)
+    else:  # the same task on the model compiled with <option solver=...> (MuJoCo's defaults otherwise)
+        t = manipulation.SUITE[(domain, task)]()
+        t.compiled = t.compiled.with_solver(solver)
+        env = manipulation.GoalEnvironment(t, num_envs=nenv, seed=7)
     env.reset()
     for i in range(warmup):
         env.step(env.sample_actions(i), device_action=True)
@@ -45,7 +50,7 @@ def env_config(name, domain, task, nenv, steps=50, warmup=10):
     dt = time.perf_counter() - t
     kms, kn = _kernel_ms(L, env.physics.ptr)
     env.close()
-    return {"config": name, "envs": nenv, "env_steps_per_s": round(nenv * steps / dt, 1),
+    return {"config": name, "envs": nenv, "solver": solver or "Newton", "env_steps_per_s": round(nenv * steps / dt, 1),
             "ms_per_step": round(dt / steps * 1e3, 4), "step_kernel_ms_avg": round(kms, 4),
             "step_kernel_launches_per_step": kn / steps}
 
@@ -96,10 +101,16 @@ def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
 def main():
     import torch  # noqa: F401  (one HIP runtime for torch and libdx)
 
+    from bench import cpu_baseline_reach_1env
+
     out = [
+        {"config": "1 reach (Shadow hand, contacts disabled), 1 env, CPU", **cpu_baseline_reach_1env(4.0, "shadow")},
+        {"config": "1' reach (Adroit hand), 1 env, CPU", **cpu_baseline_reach_1env(4.0, "adroit")},
         env_config("2 reach_shadow.state_dense (no contacts)", "reach_shadow", "state_dense", 1024),
         env_config("2' reach.state_dense (Adroit)", "reach", "state_dense", 1024),
         env_config("3 reorient.state_dense", "reorient", "state_dense", 4096),
+        env_config("3' reorient.state_dense, CG solver at MuJoCo's defaults", "reorient", "state_dense", 4096,
+                   solver="CG"),
         bimanual(),
     ]
     for o in out:
