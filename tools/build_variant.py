@@ -13,12 +13,27 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from dexterity_amd import build as B  # noqa: E402
 
-name, extra = sys.argv[1], tuple(sys.argv[2:])
+args = sys.argv[1:]
+rev = None
+if args and args[0].startswith("--rev="):  # the sources of a git revision instead of the tree
+    rev = args.pop(0)[len("--rev="):]
+name, extra = args[0], tuple(args[1:])
 vdir = os.path.join(ROOT, "variants", name)
 src = os.path.join(vdir, "csrc")
 if os.path.exists(src):
     shutil.rmtree(src)
-shutil.copytree(B.CSRC, src)
+if rev:
+    import subprocess
+
+    os.makedirs(src)
+    files = subprocess.run(["git", "-C", ROOT, "ls-tree", "--name-only", f"{rev}:dexterity_amd/csrc"],
+                           check=True, capture_output=True, text=True).stdout.split()
+    for f in files:
+        data = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:dexterity_amd/csrc/{f}"], check=True,
+                              capture_output=True).stdout
+        open(os.path.join(src, f), "wb").write(data)
+else:
+    shutil.copytree(B.CSRC, src)
 # csrc includes "../../include/dx.h"
 os.makedirs(os.path.join(ROOT, "variants", "include"), exist_ok=True)
 shutil.copy(os.path.join(ROOT, "include", "dx.h"), os.path.join(ROOT, "variants", "include", "dx.h"))
