@@ -60,3 +60,25 @@ def random_hand_state(compiled, rng, frac=0.5, vel=0.5):
             qpos[compiled.jnt_qposadr[j]] = rng.uniform(frac * lo, frac * hi)
     qvel = rng.uniform(-vel, vel, size=compiled.nv)
     return qpos, qvel
+
+
+def inclined_box_scene(tilt_deg: float, mu: float = 0.4, dt: float = 0.002):
+    """A free cube (half-size 2 cm) resting on a plane tilted by `tilt_deg` about the y
+    axis (gravity rotated instead of the plane), both geoms with friction mu: the
+    inclined-plane known answer for contact physics -- the cube sticks while
+    tan(tilt) < mu and otherwise slides down with a = g (sin - mu cos) (Coulomb friction,
+    which the pyramidal cone's edges bound exactly along a tangent axis).  Built from the
+    compiler's own primitives, so it compiles anywhere."""
+    import numpy as np
+
+    from dexterity_amd.mjcf.compiler import Scene
+
+    g, th = 9.81, np.radians(tilt_deg)
+    s = Scene(timestep=dt, gravity=(g * np.sin(th), 0.0, -g * np.cos(th)))
+    fr = f"{mu} 0.005 0.0001"
+    s.add_world_geom("ground", "plane", (1, 1, 0.1), friction=fr)
+    s.add_free_box("box", 0.02, [0.0, 0.0, 0.0199], friction=fr)
+    return s.compile()
+
+# tilts used with it (mu = 0.4, tan^-1 0.4 = 21.8 deg): 5-15 deg stick, 25 and 30 deg
+# slide (steeper, the sliding cube starts to tip over its leading edge)

@@ -132,3 +132,35 @@ def test_adroit_fingertip_golden_ik(gpu, oracle_mod, adroit_hand):
     tips = d.site_xpos.reshape(-1, 3)[solver.sites]
     np.testing.assert_allclose(tips, FINGERTIP_GOLDEN, atol=1e-3)
     solver.close()
+
+
+@pytest.mark.parametrize("tilt", [5.0, 10.0, 15.0, 25.0, 30.0])
+def test_inclined_plane_friction_kat(gpu, oracle_mod, tilt):
+    """The inclined-plane known answer on the fp32 kernel (tests/test_oracle.py has it on
+    the oracle): below tan^-1(0.4) the cube sticks, above it slides with
+    a = g (sin - mu cos) within 5 %; and the kernel's velocity stays within 2 % (of the
+    sliding speed, or 2e-4 m/s when sticking) of the oracle's over the same 0.6 s."""
+    from tests.conftest import inclined_box_scene
+
+    cm = inclined_box_scene(tilt)
+    model = gpu.Model(cm)
+    ph = gpu.BatchedPhysics(model, 4)
+    ph.step(100)
+    v0 = ph.qvel[:, 0].astype(np.float64)
+    ph.step(200)
+    v = ph.qvel.astype(np.float64)
+    q = ph.qpos.astype(np.float64)
+    a = (v[:, 0] - v0) / (200 * 0.002)
+    th, mu, g = np.radians(tilt), 0.4, 9.81
+    if np.tan(th) < mu:
+        assert np.all(np.abs(v[:, 0]) < 2e-3) and np.all(np.abs(a) < 1e-2), (tilt, v[:, 0], a)
+    else:
+        expect = g * (np.sin(th) - mu * np.cos(th))
+        assert np.all(np.abs(a - expect) <= 0.05 * expect), (tilt, a, expect)
+    assert np.all(np.abs(q[:, 2] - 0.02) < 1e-3)
+    d = oracle_mod.OracleData(oracle_mod.OracleModel(model.blob))
+    d.qpos[:] = cm.qpos0
+    for _ in range(300):
+        d.step()
+    assert np.all(np.abs(v[:, 0] - d.qvel[0]) <= max(2e-4, 0.02 * abs(d.qvel[0]))), (v[:, 0], d.qvel[0])
+    ph.close()

@@ -287,3 +287,31 @@ def test_oracle_cg_reaches_the_newton_optimum(oracle_mod, reorient_compiled):
         assert b.niter >= 1
         checked += a.ncon > 0
     assert checked >= 3
+
+
+@pytest.mark.parametrize("tilt", [5.0, 10.0, 15.0, 25.0, 30.0])
+def test_oracle_inclined_plane_friction_kat(oracle_mod, tilt):
+    """Contact physics against a physical law rather than the restatement: a cube on a
+    plane tilted below tan^-1(mu) stays put (|v| < 2e-3 m/s after 0.6 s: MuJoCo's soft
+    contacts creep slightly), and above it slides with a = g (sin - mu cos) within 5 %
+    (the soft constraint's regularisation makes friction a little weaker than Coulomb's).
+    tests/test_gpu_kat.py runs the same case on the GPU kernel."""
+    from dexterity_amd import blob
+    from tests.conftest import inclined_box_scene
+
+    cm = inclined_box_scene(tilt)
+    d = oracle_mod.OracleData(oracle_mod.OracleModel(blob.pack(cm.arrays)))
+    d.qpos[:] = cm.qpos0
+    for _ in range(100):
+        d.step()
+    v0 = d.qvel[0]
+    for _ in range(200):
+        d.step()
+    a = (d.qvel[0] - v0) / (200 * 0.002)
+    th, mu, g = np.radians(tilt), 0.4, 9.81
+    if np.tan(th) < mu:
+        assert abs(d.qvel[0]) < 2e-3 and abs(a) < 1e-2, (tilt, d.qvel[0], a)
+    else:
+        expect = g * (np.sin(th) - mu * np.cos(th))
+        assert abs(a - expect) <= 0.05 * expect, (tilt, a, expect)
+    assert abs(d.qpos[2] - 0.02) < 1e-3  # still resting on a face
