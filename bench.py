@@ -90,8 +90,8 @@ def cpu_baseline(seconds: float, threads: int, states, nsub: int):
     OpenMP over environments, on the same scene and the bench's own state mix: the
     sample starts from environment states taken from the GPU batch, draws random
     actions within ctrlrange each control step, and restarts an env from its initial
-    state once its cube lies on the ground (the reference would reset it on the
-    prop-ground contact, reorient.py:229-235)."""
+    state on the task's fall rule: a prop-ground contact at the new state
+    (reorient.py:229-235, the collision pass the reference's step ends with)."""
     import numpy as np
 
     from dexterity_amd import blob
@@ -106,13 +106,15 @@ def cpu_baseline(seconds: float, threads: int, states, nsub: int):
     n = q0.shape[0]
     qpos, qvel, ws = q0.copy(), v0.copy(), w0.copy()
     lo, hi = cm.actuator_ctrlrange.T
+    names = cm.names
+    ground, prop = names["geom"].index("ground"), names["body"].index("prop/")
     rng = np.random.RandomState(12345)
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         ctrl = rng.uniform(lo, hi, size=(n, cm.nu))
-        rc, qpos, qvel, ws = O.batch_step(om, qpos, qvel, ctrl, ws, xfrc, nsub=nsub, nthreads=threads)
-        down = qpos[:, 26] < 0.025  # cube centre below 2.5 cm: resting on the ground (half-size 2 cm)
+        rc, qpos, qvel, ws, down = O.batch_step_watch(om, qpos, qvel, ctrl, ws, xfrc, nsub, ground, prop,
+                                                      nthreads=threads)
         qpos[down], qvel[down], ws[down] = q0[down], v0[down], w0[down]
         steps += 1
     dt = time.perf_counter() - t0
@@ -122,7 +124,8 @@ def cpu_baseline(seconds: float, threads: int, states, nsub: int):
         "cores": threads,
         "kind": "port",
         "sample": f"fp64 C oracle (oracle/dx_oracle.c), reorient scene, {n} env states taken from the GPU batch "
-        f"x {steps} control steps (5 substeps each), random ctrl, fallen cubes restarted, OpenMP {threads} "
+        f"x {steps} control steps (5 substeps each) with the task's fall test (prop-ground contact), random ctrl, "
+        f"fallen cubes restarted, OpenMP {threads} "
         f"threads, {dt:.1f} s",
     }
 

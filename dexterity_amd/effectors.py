@@ -62,7 +62,15 @@ class MujocoEffector(Effector):
         return self._spec
 
     def set_control(self, physics, command) -> None:
+        """physics.bind(actuators).ctrl = command (mujoco_actuation.py:30-33), batched:
+        command is [B, len(actuators)].  An effector over every actuator in order (the
+        hand effector of every suite task) writes ctrl straight to the device; a subset
+        reads the other actuators' ctrl back first."""
         command = np.asarray(command, dtype=np.float32)
+        nu = physics.model.nu
+        if self._ids == list(range(nu)):
+            physics.set(_lib.CTRL, command.reshape(physics.nenv, nu))
+            return
         ctrl = physics.get(_lib.CTRL)
         ctrl[:, self._ids] = command.reshape(ctrl.shape[0], -1)
         physics.set(_lib.CTRL, ctrl)

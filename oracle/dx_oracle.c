@@ -1975,6 +1975,24 @@ int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double*
 int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                            const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads,
                            double* flops) {
+  return dxo_batch_step_watch(m, nenv, nsub, qpos, qvel, ctrl, qacc_warmstart, xfrc, nthreads, flops, -1, -1, NULL);
+}
+
+/* any contact at the current collision pass between geom wg and a geom of body wb with
+   dist <= 1e-8: mujoco_collisions.has_collision (utils/mujoco_collisions.py:95-119) as
+   ReOrient._is_prop_fallen calls it (reorient.py:229-235) */
+static int watch_contact(const dxo_model* m, const dxo_data* d, int wg, int wb) {
+  for (int i = 0; i < d->ncon; i++) {
+    const OContact* c = d->contact + i;
+    const int other = c->geom1 == wg ? c->geom2 : (c->geom2 == wg ? c->geom1 : -1);
+    if (other >= 0 && m->geom_bodyid[other] == wb && c->dist <= 1e-8) return 1;
+  }
+  return 0;
+}
+
+int dxo_batch_step_watch(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
+                         const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads,
+                         double* flops, int watch_geom, int watch_body, int* watch) {
   int err = 0;
   double fs[DXO_NSTAGE] = {0};
 #ifdef _OPENMP
@@ -1993,6 +2011,10 @@ int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos,
       memcpy(d->qacc_warmstart, qacc_warmstart + (size_t)e * m->nv, 8 * m->nv);
       if (xfrc) memcpy(d->xfrc_applied, xfrc, 48 * m->nbody);
       for (int s = 0; s < nsub; s++) err |= dxo_step(m, d) != 0;
+      if (watch) {  /* the new state's contacts (dm_control's step ends with mj_step1) */
+        dxo_kinematics(m, d);
+        watch[e] = watch_contact(m, d, watch_geom, watch_body);
+      }
       memcpy(qpos + (size_t)e * m->nq, d->qpos, 8 * m->nq);
       memcpy(qvel + (size_t)e * m->nv, d->qvel, 8 * m->nv);
       memcpy(qacc_warmstart + (size_t)e * m->nv, d->qacc_warmstart, 8 * m->nv);

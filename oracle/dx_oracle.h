@@ -100,6 +100,12 @@ int dxo_batch_step(const dxo_model* m, int nenv, int nsub, double* qpos, double*
 int dxo_batch_step_counted(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
                            const double* ctrl, double* qacc_warmstart, const double* xfrc,
                            int nthreads, double* flops);
+/* Same, and (watch != NULL) watch[e] = 1 when env e's state after the steps has a contact
+   between geom watch_geom and a geom of body watch_body with dist <= 1e-8 (the fall test
+   of reorient.py:229-235). */
+int dxo_batch_step_watch(const dxo_model* m, int nenv, int nsub, double* qpos, double* qvel,
+                         const double* ctrl, double* qacc_warmstart, const double* xfrc, int nthreads,
+                         double* flops, int watch_geom, int watch_body, int* watch);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,8 @@ def lib():
         L.dxo_batch_step.restype = ip
         L.dxo_batch_step_counted.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip, dp]
         L.dxo_batch_step_counted.restype = ip
+        L.dxo_batch_step_watch.argtypes = [vp, ip, ip, dp, dp, dp, dp, dp, ip, dp, ip, ip, vp]
+        L.dxo_batch_step_watch.restype = ip
         L.dxo_observe.argtypes = [vp, vp]
         L.dxo_observe.restype = ip
         L.dxo_object_velocity.argtypes = [vp, vp, ip, ip, dp]
@@ -213,3 +215,18 @@ def batch_step(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub:
     if flops is not None:
         flops.append(fl)
     return rc, arrs[0], arrs[1], arrs[3]
+
+
+def batch_step_watch(model: OracleModel, qpos, qvel, ctrl, qacc_warmstart, xfrc, nsub: int, watch_geom: int,
+                     watch_body: int, nthreads: int = 0):
+    """batch_step, plus per env whether the state after the steps has a contact between
+    geom watch_geom and a geom of body watch_body with dist <= 1e-8 (the prop-ground fall
+    test of reorient.py:229-235).  Returns (rc, qpos, qvel, qacc_warmstart, fell)."""
+    dp = ctypes.POINTER(ctypes.c_double)
+    arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (qpos, qvel, ctrl, qacc_warmstart)]
+    x = None if xfrc is None else np.ascontiguousarray(xfrc, dtype=np.float64)
+    fell = np.zeros(arrs[0].shape[0], dtype=np.int32)
+    rc = lib().dxo_batch_step_watch(model.ptr, arrs[0].shape[0], nsub, *(a.ctypes.data_as(dp) for a in arrs),
+                                    None if x is None else x.ctypes.data_as(dp), nthreads, None, int(watch_geom),
+                                    int(watch_body), fell.ctypes.data)
+    return rc, arrs[0], arrs[1], arrs[3], fell.astype(bool)

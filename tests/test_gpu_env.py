@@ -592,3 +592,21 @@ def test_sharded_job_two_processes(built):
         for k in ref:
             np.testing.assert_array_equal(ref[k][sl], got[r][k], err_msg=f"rank {r} {k}")
     whole.close()
+
+
+def test_effector_set_control_round_trip(built):
+    """hand_effector_test.py:12-20 / mujoco_actuation.py:30-33: set_control writes the
+    command into ctrl -- the hand effector over every actuator straight to the device, a
+    subset effector leaving the other actuators' ctrl as they were."""
+    from dexterity_amd import effectors, manipulation
+
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=4)
+    ph, nu = env.physics, env.physics.model.nu
+    cmd = np.random.RandomState(0).uniform(-1, 1, size=(4, nu)).astype(np.float32)
+    env.task.hand_effector.set_control(ph, cmd)
+    np.testing.assert_array_equal(ph.get(_lib.CTRL), cmd)
+    effectors.MujocoEffector([1, 3, 5]).set_control(ph, np.full((4, 3), 0.5, np.float32))
+    expect = cmd.copy()
+    expect[:, [1, 3, 5]] = 0.5
+    np.testing.assert_array_equal(ph.get(_lib.CTRL), expect)
+    env.close()

@@ -315,3 +315,23 @@ def test_oracle_inclined_plane_friction_kat(oracle_mod, tilt):
         expect = g * (np.sin(th) - mu * np.cos(th))
         assert abs(a - expect) <= 0.05 * expect, (tilt, a, expect)
     assert abs(d.qpos[2] - 0.02) < 1e-3  # still resting on a face
+
+
+def test_batch_step_watch_is_the_fall_test(oracle_mod, reorient_compiled):
+    """batch_step_watch's flag is ReOrient._is_prop_fallen (reorient.py:229-235): a
+    prop-ground contact (dist <= 1e-8) at the state after the steps -- set for a cube
+    resting on the ground, clear for one held above it (the CPU baseline's reset rule)."""
+    from dexterity_amd.physics import gravity_compensation
+
+    cm = reorient_compiled
+    om = oracle_mod.OracleModel(__import__("dexterity_amd.blob", fromlist=["pack"]).pack(cm.arrays))
+    q = np.tile(cm.qpos0, (2, 1))
+    q[0, 24:27] = (0.3, 0.3, 0.0195)  # on the ground, away from the hand
+    q[1, 24:27] = (0.0, -0.13, 0.16)   # the spawn point above the palm
+    z = np.zeros((2, cm.nv))
+    ctrl = np.zeros((2, cm.nu))
+    g = cm.names["geom"].index("ground")
+    b = cm.names["body"].index("prop/")
+    rc, _, _, _, fell = oracle_mod.batch_step_watch(om, q, z.copy(), ctrl, z.copy(),
+                                                    gravity_compensation(cm, "shadow_hand_e/"), 5, g, b)
+    assert rc == 0 and fell.tolist() == [True, False]
