@@ -249,18 +249,25 @@ enum {
   CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC, CNT_NP_TRIPS, CNT_BROAD_KEEP, CNT_MID_PAIRS,
   CNT_MID_KEEP  // event counters, not cycles
 };
+// The accumulators are this env's own global slots, updated by no-return atomics: a
+// read-modify-write would put a memory round trip on the wave's path at every mark
+// (and every in-loop count), charged to the stage after it.
+template <class P>
+__device__ __forceinline__ void stage_add(P p, unsigned long long v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 template <class Ctx>
 __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
   if (c.stage_acc && LANE == 0) {
     unsigned long long t = __builtin_amdgcn_s_memtime();
     unsigned long long* last = (unsigned long long*)(c.I + 10);
-    c.stage_acc[k] += t - *last;  // this env's own slots
+    stage_add(c.stage_acc + k, t - *last);
     *last = t;
   }
 }
 template <class Ctx>
 __device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
-  if (c.stage_acc && LANE == 0) c.stage_acc[k] += n;
+  if (c.stage_acc && LANE == 0) stage_add(c.stage_acc + k, (unsigned long long)n);
 }
 // misc int slots
 // I_OVF: capacity bits of the substep (1 candidates, 2 contacts, 4 Jacobian dofs, 8 rows);
@@ -812,20 +819,24 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float d
       if (i == j) e += dj1;
       C11[v] = e;
     }
+    // (clamped in-range addresses, selected after: no exec-mask branch per load)
     {  // C12: A[i][32 + j] = A[32 + j][i]
       const int r = 32 + j;
-      C12[v] = r < n ? A[ti(r) + i] : 0.f;
+      const float e = A[ti(min(r, n - 1)) + i];
+      C12[v] = r < n ? e : 0.f;
     }
     {  // C22: A[32 + i][32 + j]
       const int ri = 32 + i, rj = 32 + j;
       const bool in = ri < n && rj < n;
-      const int ra = max(ri, rj), rb = min(ri, rj);
-      float e = in ? A[ti(ra) + rb] : (i == j ? 1.f : 0.f);
+      const int ca = min(max(ri, rj), n - 1), cb = min(min(ri, rj), n - 1);
+      const float av = A[ti(ca) + cb];
+      float e = in ? av : (i == j ? 1.f : 0.f);
       if (i == j && in) e += dj2;
       C22[v] = e;
     }
   }
-  float b = l < n ? x[l] : 0.f;
+  const float bx = x[min(l, n - 1)];
+  float b = l < n ? bx : 0.f;
   SYNC();  // A may alias T
   float dinv = 0.f;  // lane k: 1 / L[k][k]
   // columns 0..31
@@ -884,7 +895,8 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float d
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int k = k0 + u;
-      lc[u] = i > k && i < n ? T[ti(i) + k] : 0.f;
+      const float t = T[ti(min(i, n - 1)) + min(k, n - 1)];
+      lc[u] = i > k && i < n ? t : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -903,7 +915,8 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float d
 #pragma unroll
     for (int u = 0; u < 8; u++) {
       const int k = k1 - u;
-      lc[u] = k >= 0 && i < k ? T[ti(k) + i] : 0.f;
+      const float t = T[ti(max(k, 0)) + min(i, max(k, 0))];
+      lc[u] = k >= 0 && i < k ? t : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < 8; u++) {
@@ -917,6 +930,80 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float d
   }
   SYNC();
   if (i < n) x[i] = xo;
+  SYNC();
+}
+
+// Solve for n <= 30 by the symmetric sweep operator on the matrix cores: the bordered
+// matrix [[A, b], [b^T, 0]] (b in row/column 31, identity padding between) sits in the
+// v_mfma_f32_32x32x2_f32 accumulator as in mfma_chol_solve32.  Sweeping the pivot pair
+// {k, k+1} of a symmetric S maps it to [[-P^-1, P^-1 U^T], [U P^-1, S' - U P^-1 U^T]]
+// (P the 2 x 2 pivot block, U the other rows of the pivot columns); once every pivot of
+// A is swept, column 31 holds A^-1 b.  One step = the pivot rows and columns zeroed, then
+// one rank-2 MFMA S -= V W V^T with W = P^-1 and V = U with -I in the pivot rows: that
+// writes U W into the pivot columns and -W into the pivot block without the cancellation
+// an in-place update would suffer when |P| >> |W|.  Only the entries read later are
+// zeroed: a pivot column below the pair (rows read as future pivot rows) and the pivot
+// rows (their column-31 entries are the answer).  The pivots are the Cholesky Schur
+// complements (Gauss-Jordan on an SPD matrix in pivot pairs): 15 dependent steps and no
+// triangular substitutions (mfma_chol_solve32's two 32-step readlane chains and its LDS
+// transpose).  A (+ dj on the diagonal) -> x = A^-1 x.  tests/test_sweep_solve.py
+// restates it in numpy.
+__device__ __forceinline__ void mfma_sweep_solve30(const float* A, int n, float dj, float* x) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  // Every lane loads in-range addresses (indices clamped to n - 1) and selects after:
+  // a guarded load compiles to an exec-mask branch with its own LDS wait, 32 in a row.
+  const int jc = min(j, n - 1);
+  const float bj = j < n ? x[jc] : 0.f;
+  float av[16], xv[16];
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int ic = min(8 * (v >> 2) + 4 * hi + (v & 3), n - 1);
+    av[v] = A[ti(max(ic, jc)) + min(ic, jc)];
+    xv[v] = x[ic];
+  }
+  dx_f16v C;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    const bool in = i < n && j < n;
+    float e = in ? av[v] : (i == j && i < 31 ? 1.f : 0.f);
+    if (i == j && in) e += dj;
+    if (i == 31) e = bj;              // row 31: b_j (0 at (31, 31))
+    if (j == 31 && i < n) e = xv[v];  // column 31: b_i
+    C[v] = e;
+  }
+#pragma unroll
+  for (int k = 0; k < 30; k += 2) {
+    if (k >= n) continue;  // identity padding (a uniform branch; break would block the unroll)
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // S[k][j], S[k+1][j]
+    const float p00 = rl(rk, k), p10 = rl(rk1, k), p11 = rl(rk1, k + 1);
+    const float id = 1.0f / (p00 * p11 - p10 * p10);
+    const float w00 = p11 * id, w01 = -p10 * id, w11 = p00 * id;
+    const bool pc = j == k || j == k + 1;  // a pivot column
+    const float v0 = pc ? (j == k ? -1.f : 0.f) : rk;
+    const float v1 = pc ? (j == k ? 0.f : -1.f) : rk1;
+    const float a = hi ? v1 : v0;                                             // A: V[j][hi]
+    const float b = hi ? fmaf(w01, v0, w11 * v1) : fmaf(w00, v0, w01 * v1);  // B: (W V^T)[hi][j]
+#pragma unroll
+    for (int v = 0; v < 16; v++)
+      if (8 * (v >> 2) + 4 + (v & 3) >= k + 2) C[v] = pc ? 0.f : C[v];
+    const bool ph = hi == (up ? 1 : 0);
+    C[vk] = ph ? 0.f : C[vk];
+    C[vk + 1] = ph ? 0.f : C[vk + 1];
+    C = __builtin_amdgcn_mfma_f32_32x32x2f32(-a, b, C, 0, 0, 0);
+  }
+  // column 31 -> x (lane 31 of each half writes its half's rows)
+  SYNC();
+  if (j == 31) {
+#pragma unroll
+    for (int v = 0; v < 16; v++) {
+      const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+      if (i < n) x[i] = C[v];
+    }
+  }
   SYNC();
 }
 
@@ -934,7 +1021,8 @@ __device__ __forceinline__ DiagAdd diag_add(const DXG float* dadd, float hs, int
 // x <- (A + diag(dd))^-1 x for a packed lower-triangle A (LDS), n <= 64;
 // T: ti(max(n, 32)) words of LDS scratch, may alias A.
 __device__ __forceinline__ void chol_solve(const float* A, int n, DiagAdd dd, float* x, float* T) {
-  if (n <= 32) mfma_chol_solve32(A, n, dd.d1, x, T);
+  if (DX_SWEEP && n <= 30) mfma_sweep_solve30(A, n, dd.d1, x);
+  else if (n <= 32) mfma_chol_solve32(A, n, dd.d1, x, T);
   else mfma_chol_solve64(A, n, dd.d1, dd.d2, x, T);
 }
 __device__ __forceinline__ void chol_solve(const float* A, int n, float* x, float* T) {

@@ -23,6 +23,9 @@
 #define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
 #define DX_LDL_SLOTS 16   // tree-sparse LDL^T items: at most 16 x 64 (dx_device.h tree_solve)
+#ifndef DX_SWEEP
+#define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)
+#endif
 #ifndef DX_NPG
 #define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
 #endif

@@ -1074,11 +1074,12 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
     Shape G;  // the pair's first geom on lanes 0-3 of the group, its second on lanes 4-7
     MprState M;
     bool cached = false;
+    int trips = 0;
     M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
     for (;;) {
       bool act = q < ng;
       if (__ballot(act) == 0) break;
-      stage_count(c, CNT_NP_TRIPS);
+      trips++;
       NpOut o;
       o.wr = false;
       o.rank = 0;
@@ -1148,6 +1149,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
       }
       next += __popcll(fin);
     }
+    stage_count(c, CNT_NP_TRIPS, trips);
   }
   SYNC();
   // candidate order: lane k ranks record k by its key, then moves it
@@ -1627,33 +1629,30 @@ __device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf,
 }
 
 // y = M x (lanes over rows).  For n <= 32 the row is gathered with 32 independent
-// LDS reads (one latency, not one per element); entries past n read zeros of the
-// packed triangle's padding only through x, which is 0 there.
+// LDS reads (one latency, not one per element).  Columns past n read a clamped,
+// in-range address and are zeroed after the load: a guarded load would be a branch
+// with its own LDS wait per column.
 __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y, int n) {
+  const int i = min(LANE, n - 1);
   if (n <= 32) {
-    const int i = min(LANE, n - 1);
     float s = 0;
 #pragma unroll
     for (int k = 0; k < 32; k++) {
-      int a = max(i, k), b = min(i, k);
-      float xk = k < n ? x[k] : 0.f;
-      float mk = k < n ? M[ti(a) + b] : 0.f;
-      s = fmaf(mk, xk, s);
+      const int kc = min(k, n - 1);
+      const float xv = x[kc], mv = M[ti(max(i, kc)) + min(i, kc)];
+      s = fmaf(k < n ? mv : 0.f, xv, s);
     }
     if (LANE < n) y[LANE] = s;
     return;
   }
   // n <= 64 (DX_MAX_NV): the same unrolled gather over 64 columns, every read
-  // independent of the running sum (the per-lane loops this replaced waited on LDS
-  // once per column)
-  const int i = min(LANE, n - 1);
+  // independent of the running sum
   float s = 0;
 #pragma unroll
   for (int k = 0; k < 64; k++) {
-    int a = max(i, k), b = min(i, k);
-    float xk = k < n ? x[k] : 0.f;
-    float mk = k < n ? M[ti(a) + b] : 0.f;
-    s = fmaf(mk, xk, s);
+    const int kc = min(k, n - 1);
+    const float xv = x[kc], mv = M[ti(max(i, kc)) + min(i, kc)];
+    s = fmaf(k < n ? mv : 0.f, xv, s);
   }
   if (LANE < n) y[LANE] = s;
 }
@@ -1675,10 +1674,11 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
     int nnz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
     float s = 0;
 #pragma unroll
-    for (int q = 0; q < DX_DOFMAX; q++) {
-      float v = q < nnz ? cj_val[(ci * 3 + k) * DX_DOFMAX + q] : 0.f;
-      float xv = q < nnz ? x[cj_idx[ci * DX_DOFMAX + q]] : 0.f;
-      s = fmaf(v, xv, s);
+    for (int q = 0; q < DX_DOFMAX; q++) {  // unguarded loads; slots past nnz are not summed
+      const float v = cj_val[(ci * 3 + k) * DX_DOFMAX + q];
+      const float xv = x[cj_idx[ci * DX_DOFMAX + q]];
+      const float t = fmaf(v, xv, s);
+      s = q < nnz ? t : s;
     }
     cq[t] = s;
   }
@@ -1824,15 +1824,19 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
         break;  // contact rows are last
       }
     }
-    uint64_t bit = 1ull << d;
+    // Branch-free over the contacts (a skipped contact's loads are made and discarded),
+    // so the unrolled iterations' LDS reads overlap instead of waiting one by one; the
+    // sum keeps the contact order.
+    const uint64_t bit = 1ull << d;
+#pragma unroll 4
     for (int ci = 0; ci < ncon; ci++) {
       const float* r = con + DX_CON_STRIDE * ci;
-      uint64_t sup = (uint64_t)(uint32_t)__float_as_int(r[18]) | ((uint64_t)(uint32_t)__float_as_int(r[19]) << 32);
-      if (!(sup & bit)) continue;
-      int q = __popcll(sup & (bit - 1));
-      if (q >= DX_DOFMAX) continue;
-      s += cj_val[(ci * 3 + 0) * DX_DOFMAX + q] * cw[3 * ci] + cj_val[(ci * 3 + 1) * DX_DOFMAX + q] * cw[3 * ci + 1] +
-           cj_val[(ci * 3 + 2) * DX_DOFMAX + q] * cw[3 * ci + 2];
+      const uint64_t sup = (uint64_t)(uint32_t)__float_as_int(r[18]) | ((uint64_t)(uint32_t)__float_as_int(r[19]) << 32);
+      const int q = __popcll(sup & (bit - 1));
+      const bool on = (sup & bit) && q < DX_DOFMAX;
+      const float* cv = cj_val + ci * 3 * DX_DOFMAX + min(q, DX_DOFMAX - 1);
+      const float t = cv[0] * cw[3 * ci] + cv[DX_DOFMAX] * cw[3 * ci + 1] + cv[2 * DX_DOFMAX] * cw[3 * ci + 2];
+      s = on ? s + t : s;
     }
     out[d] = s;
   }
@@ -1985,19 +1989,27 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   float D[DX_LS_SLOTS], fl[DX_LS_SLOTS], Rf[DX_LS_SLOTS], ja[DX_LS_SLOTS], jj[DX_LS_SLOTS];
 #pragma unroll
   for (int k = 0; k < DX_LS_SLOTS; k++) {
-    int r = LANE + DX_WAVE * k;
-    bool ok = k < ns && r < nefc;
-    bool fr = ok && r < c.nfric;
-    ty[k] = ok ? (meta[r] & 15) : DXR_CON;
-    D[k] = ok ? Dp[r] : 0.f;
-    fl[k] = fr ? flp[r] : 0.f;
-    Rf[k] = fr ? Rfp[r] : 0.f;
-    ja[k] = ok ? jarp[r] : 0.f;
-    jj[k] = ok ? jv[r] : 0.f;
+    if (k < ns) {  // uniform; the loads read a clamped row and select after (no per-lane branch)
+      const int r = LANE + DX_WAVE * k;
+      const int rc = max(min(r, nefc - 1), 0);
+      const bool ok = r < nefc;
+      const bool fr = ok && r < c.nfric;
+      const int mt = meta[rc];
+      const float d = Dp[rc], f = flp[rc], rf = Rfp[rc], a = jarp[rc], v = jv[rc];
+      ty[k] = ok ? (mt & 15) : DXR_CON;
+      D[k] = ok ? d : 0.f;
+      fl[k] = fr ? f : 0.f;
+      Rf[k] = fr ? rf : 0.f;
+      ja[k] = ok ? a : 0.f;
+      jj[k] = ok ? v : 0.f;
+    } else {
+      ty[k] = DXR_CON;
+      D[k] = fl[k] = Rf[k] = ja[k] = jj[k] = 0.f;
+    }
   }
   float lo = 0, hi = -1, alpha = 0, g0 = 0;
-  for (int it = 0; it < 40; it++) {
-    stage_count(c, CNT_LS_IT);
+  int it = 0;
+  for (; it < 40; it++) {
     float g = 0, h = 0;
 #pragma unroll
     for (int k = 0; k < DX_LS_SLOTS; k++) {
@@ -2019,6 +2031,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
     if (fabsf(next - alpha) <= 1e-7f * fabsf(alpha)) break;
     alpha = next;
   }
+  stage_count(c, CNT_LS_IT, min(it + 1, 40));
   if (slope0) *slope0 = g0;
   // rows whose cost zone differs between the current point and the new one
   int ch = 0;
