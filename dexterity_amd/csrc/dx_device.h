@@ -1108,10 +1108,13 @@ __device__ __forceinline__ void tree_solve(const Ctx& c, const float* A, float d
   if (l < n) x[l] = v;
   SYNC();
 }
-// M (+ diag) solve: the tree-sparse LDL^T when the model has its item table, else the
-// dense matrix-core Cholesky
+// M (+ diag) solve: n <= 30 by the MFMA sweep operator (15 dependent steps, no
+// substitutions: same-box 2.60 -> 2.67 M env-steps/s on Shadow reorient against the tree
+// LDL^T, whose six level barriers and two 30-step readlane chains cost more), larger n by
+// the tree-sparse LDL^T when the model has its item table, else the dense Cholesky.
 template <class Ctx>
 __device__ __forceinline__ void m_solve(const Ctx& c, const float* A, DiagAdd dd, float* x, float* T) {
-  if (c.mdl().ldl_nslot > 0) tree_solve(c, A, LANE < 32 ? dd.d1 : dd.d2, x, T);
+  if (DX_SWEEP && c.nv <= 30) mfma_sweep_solve30(A, c.nv, dd.d1, x);
+  else if (c.mdl().ldl_nslot > 0) tree_solve(c, A, LANE < 32 ? dd.d1 : dd.d2, x, T);
   else chol_solve(A, c.nv, dd, x, T);
 }

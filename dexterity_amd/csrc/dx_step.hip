@@ -1952,6 +1952,115 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   SYNC();
 }
 
+// Incremental Hessian for the sweep solve (nv <= 30, no tendon-limit rows).  H in LDS
+// holds M + sum_contacts J_c^T W_c J_c and is not touched by the sweep, so after the
+// first build only the contacts whose W changed in the last line search add their
+// change, (W_new - W_old) -- MuJoCo's Newton likewise updates its factor only for the
+// constraints whose state changed ([3P] mj_solNewton's incremental Hessian).  Lane ci
+// keeps contact ci's W (wo) across iterations.  The unit rows' diagonal (friction loss,
+// joint limits) is rebuilt every iteration into a register, the sweep's diagonal
+// addition for column LANE % 32.  Returns that addition.
+template <class Ctx>
+__device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, float (&wo)[5]) {
+  const DevModel& m = c.mdl();
+  const int nv = c.nv;
+  const int nefc = c.I[I_NEFC];
+  const int ncon = c.I[I_NCON];
+  float* H = c.f(c.L.H);
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* jar = c.f(c.L.efc_jar);
+  if (first) {
+    const float* M = c.f(c.L.M);
+    for (int k = LANE; k < ti(nv); k += DX_WAVE) H[k] = M[k];
+  }
+  // unit rows (friction, joint limits) -> this lane's diagonal addition
+  float s = 0.f;
+  {
+    const int d = LANE & 31;
+    if (d < nv) {
+      const int fr = m.dof_fricrow[d];
+      if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
+      for (int r = c.nfric; r < nefc; r++) {
+        const int mt = meta[r], type = mt & 15, id = mt >> 8;
+        if (type != DXR_LIMJ) break;  // (no tendon-limit rows on this path)
+        if (id != d) continue;
+        float f, hw;
+        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        s += hw;
+      }
+    }
+  }
+  const float* con = c.f(c.L.con);
+  const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
+  const float* cj_val = c.f(c.L.cj_val);
+  float w[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // w00, w01, w02, w11, w22
+  int nnz = 0;
+  if (LANE < ncon) {
+    const float* r = con + DX_CON_STRIDE * LANE;
+    const int row0 = __float_as_int(r[15]);
+    nnz = __float_as_int(r[14]) & 255;
+    if ((__float_as_int(r[14]) >> 8) == 1) {
+      if (row0 < nefc) {
+        float f, hw;
+        row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+        w[0] = hw;
+      }
+    } else {
+      for (int e = 0; e < 4; e++) {
+        const int row = row0 + e;
+        if (row >= nefc) break;
+        float f, hw;
+        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+        const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
+        w[0] += hw;
+        if (e < 2) { w[1] += hw * mu; w[3] += hw * mu * mu; }
+        else { w[2] += hw * mu; w[4] += hw * mu * mu; }
+      }
+    }
+  }
+  float dw[5];
+  bool ch = false;
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    dw[k] = w[k] - wo[k];
+    ch |= w[k] != wo[k];
+    wo[k] = w[k];
+  }
+  const int items = ch ? nnz * (nnz + 1) / 2 : 0;
+  const int incl = wave_incl_scan(items);
+  const int excl = incl - items;
+  const int total = __builtin_amdgcn_readlane(incl, 63);
+  if (first) SYNC();  // the M copy before the atomics
+  for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+    const int t = min(base + LANE, total - 1);
+    int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
+#pragma unroll
+    for (int st = 16; st >= 1; st >>= 1) {
+      const int mid = ci + st;
+      const int em = __shfl(excl, mid & 63, 64);
+      if (mid < ncon && em <= t) ci = mid;
+    }
+    const int u = t - __shfl(excl, ci, 64);
+    int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+    a += (a + 1) * (a + 2) / 2 <= u;
+    a -= a * (a + 1) / 2 > u;
+    const int b = u - a * (a + 1) / 2;
+    const float c00 = __shfl(dw[0], ci, 64), c01 = __shfl(dw[1], ci, 64), c02 = __shfl(dw[2], ci, 64);
+    const float c11 = __shfl(dw[3], ci, 64), c22 = __shfl(dw[4], ci, 64);
+    const float* jv = cj_val + ci * 3 * DX_DOFMAX;
+    const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
+    const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
+    const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
+                      c22 * a2 * b2;
+    if (base + LANE < total) atomicAdd(H + ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b], sum);
+  }
+  SYNC();
+  return s;
+}
+
 // zone of a row's cost at jar: 0 zero, 1 quadratic, 2 / 3 linear friction zones
 __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
   if (type == DXR_FRIC) return jar <= -Rf ? 3 : (jar >= Rf ? 2 : 1);
@@ -2181,6 +2290,8 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     solve_cg(c, scale, tol);
     return;
   }
+  const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
+  float wo[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
   for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
     jac_t_force(c, grad);  // grad <- J^T f
@@ -2192,12 +2303,20 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     gn = sqrtf(wave_sum(gn)) * scale;
     stage_mark(c, ST_NEWTON_GRAD);
     if (gn < tol) break;
-    build_hessian(c);
-    stage_mark(c, ST_NEWTON_HESS);
     float* H = c.f(c.L.H);
-    for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
-    SYNC();
-    chol_solve(H, nv, dir, H);
+    if (inc) {
+      const float hd = build_hessian_inc(c, it == 0, wo);
+      stage_mark(c, ST_NEWTON_HESS);
+      for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
+      SYNC();
+      mfma_sweep_solve30(H, nv, hd, dir);
+    } else {
+      build_hessian(c);
+      stage_mark(c, ST_NEWTON_HESS);
+      for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -grad[i];
+      SYNC();
+      chol_solve(H, nv, dir, H);
+    }
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float alpha = line_search(c, qacc, Ma, dir, &changed);
@@ -2212,15 +2331,20 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     }
     for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] += alpha * jvd[r];
     SYNC();
+    // Converged when (a) the full Newton step kept every row in its cost zone: the
+    // cost is quadratic on that zone set, so the step landed on its exact minimiser
+    // (decided before the cost evaluation, which this exit does not need); or (b) the
+    // improvement is below the tolerance or at fp32 noise level of the cost.
+    if (changed == 0 && fabsf(alpha - 1.0f) < 1e-3f) {
+      it++;
+      break;
+    }
     float nc = total_cost(c, qacc, Ma);
     stage_mark(c, ST_NEWTON_EVAL);
     float impr = scale * (cost - nc);
     float prev = cost;
     cost = nc;
-    // Converged when (a) the full Newton step kept every row in its cost zone: the
-    // cost is quadratic on that zone set, so the step landed on its exact minimiser;
-    // or (b) the improvement is below the tolerance or at fp32 noise level of the cost.
-    if ((changed == 0 && fabsf(alpha - 1.0f) < 1e-3f) || impr < tol || (prev - nc) <= 1e-9f * fabsf(prev)) {
+    if (impr < tol || (prev - nc) <= 1e-9f * fabsf(prev)) {
       it++;
       break;
     }
