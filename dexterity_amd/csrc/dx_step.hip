@@ -1725,13 +1725,14 @@ __device__ __forceinline__ float rows_cost(const Ctx& c, const float* jr, float 
 
 // cost at the current jar (efc_jar) + gauss; fills nothing else.  Returns total.
 template <class Ctx>
-__device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma) {
+__device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, const float* Ma, float* gauss = nullptr) {
   const DevModel& m = c.mdl();
   int nv = c.nv;
   const float* qs = c.f(c.L.qfrc_smooth);
   const float* a0 = c.f(c.L.qacc_smooth);
   float g = 0;
   for (int i = LANE; i < nv; i += DX_WAVE) g += 0.5f * (qacc[i] - a0[i]) * (Ma[i] - qs[i]);
+  if (gauss) *gauss = wave_sum(g);
   int nefc = c.I[I_NEFC];
   const int* meta = (const int*)c.f(c.L.efc_meta);
   const float* D = c.f(c.L.efc_D);
@@ -1748,7 +1749,7 @@ __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, con
 
 // jar = J qacc - aref, Ma = M qacc; returns cost
 template <class Ctx>
-__device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma) {
+__device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma, float* gauss = nullptr) {
   int nv = c.nv;
   mat_vec(c.f(c.L.M), qacc, Ma, nv);
   stage_mark(c, ST_MATVEC);
@@ -1759,7 +1760,7 @@ __device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, floa
   int nefc = c.I[I_NEFC];
   for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] -= aref[r];
   SYNC();
-  return total_cost(c, qacc, Ma);
+  return total_cost(c, qacc, Ma, gauss);
 }
 
 // out[d] = sum_r J[r][d] * w[r] computed as J^T applied to the per-row force of the
@@ -2071,9 +2072,17 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // cost).  Every row's (type, D, friction, jar, J dir) is loaded into registers once
 // -- lane-owned rows r = LANE + 64 k -- so the iterations touch no LDS.
 #define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
-template <class Ctx>
+// NEWTON (dir = -H^-1 grad): the slope at alpha = 0 is grad . dir and the curvature there
+// dir^T H dir = -grad . dir (H is the Hessian of the zone set at alpha = 0), so the first
+// 1-D Newton step from 0 lands at alpha = 1 -- the search starts there, with g0 = grad . dir
+// -- and at the end the new residuals are written from the registers and the cost at the
+// new point is returned in *cost_new: the rows' costs plus the Gauss term, continued along
+// the line as gauss + alpha qb + alpha^2 qa / 2 (M qacc_smooth = qfrc_smooth), so the
+// solver needs no separate cost pass.
+template <bool NEWTON = false, class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed,
-                                             float* slope0 = nullptr) {
+                                             float* slope0 = nullptr, const float* grad = nullptr,
+                                             float gauss = 0.f, float* cost_new = nullptr, float* gauss_new = nullptr) {
   const DevModel& m = c.mdl();
   int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
@@ -2083,10 +2092,15 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   jac_vec(c, dir, jv);  // includes SYNC
   stage_mark(c, ST_JACVEC);
   const float* qs = c.f(c.L.qfrc_smooth);
-  float qa = 0, qb = 0;
-  for (int i = LANE; i < nv; i += DX_WAVE) { qa += dir[i] * Mdir[i]; qb += dir[i] * (Ma[i] - qs[i]); }
+  float qa = 0, qb = 0, qg = 0;
+  for (int i = LANE; i < nv; i += DX_WAVE) {
+    qa += dir[i] * Mdir[i];
+    qb += dir[i] * (Ma[i] - qs[i]);
+    if (NEWTON) qg += dir[i] * grad[i];
+  }
   qa = wave_sum(qa);
   qb = wave_sum(qb);
+  if (NEWTON) qg = wave_sum(qg);
   int nefc = c.I[I_NEFC];
   const int ns = (nefc + DX_WAVE - 1) / DX_WAVE;  // uniform
   const int* meta = (const int*)c.f(c.L.efc_meta);
@@ -2118,6 +2132,11 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   }
   float lo = 0, hi = -1, alpha = 0, g0 = 0;
   int it = 0;
+  if (NEWTON) {
+    g0 = qg;
+    if (g0 < 0.f) { alpha = 1.f; it = 1; }  // else not a descent direction: alpha stays 0
+    else it = 40;
+  }
   for (; it < 40; it++) {
     float g = 0, h = 0;
 #pragma unroll
@@ -2142,6 +2161,23 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   }
   stage_count(c, CNT_LS_IT, min(it + 1, 40));
   if (slope0) *slope0 = g0;
+  if (NEWTON) {
+    float* jw = c.f(c.L.efc_jar);
+    float rc = 0.f;
+#pragma unroll
+    for (int k = 0; k < DX_LS_SLOTS; k++) {
+      if (k < ns) {
+        const float jn = ja[k] + alpha * jj[k];
+        float f, hw;
+        rc += row_cost(ty[k], D[k], fl[k], Rf[k], jn, f, hw);
+        const int r = LANE + DX_WAVE * k;
+        if (r < nefc) jw[r] = jn;
+      }
+    }
+    const float gn = gauss + alpha * qb + 0.5f * alpha * alpha * qa;
+    *gauss_new = gn;
+    *cost_new = gn + wave_sum(rc);
+  }
   // rows whose cost zone differs between the current point and the new one
   int ch = 0;
 #pragma unroll
@@ -2270,13 +2306,15 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   const float* aref = c.f(c.L.efc_aref);
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
-  float cw = eval_cost(c, qacc, Ma);
+  float gw = 0.f;
+  float cw = eval_cost(c, qacc, Ma, &gw);
   jac_vec(c, a0, jvs);
   for (int r = LANE; r < nefc; r += DX_WAVE) jvs[r] -= aref[r];
   SYNC();
   float cs = rows_cost(c, jvs, 0.f);
-  float cost = cw;
+  float cost = cw, gauss = gw;
   if (!(cw < cs)) {
+    gauss = 0.f;
     for (int i = LANE; i < nv; i += DX_WAVE) { qacc[i] = a0[i]; Ma[i] = qs[i]; }
     for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] = jvs[r];
     SYNC();
@@ -2319,17 +2357,21 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     }
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
-    float alpha = line_search(c, qacc, Ma, dir, &changed);
+    float nc = 0.f, gnew = 0.f;
+    float alpha = inc ? line_search<true>(c, qacc, Ma, dir, &changed, nullptr, grad, gauss, &nc, &gnew)
+                      : line_search(c, qacc, Ma, dir, &changed);
     stage_mark(c, ST_NEWTON_LS);
     // qacc += alpha dir; M qacc and J qacc - aref follow by linearity from the line
-    // search's M dir (v4) and J dir (efc_jv): no products recomputed
+    // search's M dir (v4) and J dir (efc_jv): no products recomputed (the Newton-mode
+    // search wrote the new residuals itself)
     const float* Mdir = c.f(c.L.v4);
     const float* jvd = c.f(c.L.efc_jv);
     for (int i = LANE; i < nv; i += DX_WAVE) {
       qacc[i] += alpha * dir[i];
       Ma[i] += alpha * Mdir[i];
     }
-    for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] += alpha * jvd[r];
+    if (!inc)
+      for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] += alpha * jvd[r];
     SYNC();
     // Converged when (a) the full Newton step kept every row in its cost zone: the
     // cost is quadratic on that zone set, so the step landed on its exact minimiser
@@ -2339,7 +2381,8 @@ __device__ __forceinline__ void solve(const Ctx& c) {
       it++;
       break;
     }
-    float nc = total_cost(c, qacc, Ma);
+    if (!inc) nc = total_cost(c, qacc, Ma);
+    gauss = gnew;
     stage_mark(c, ST_NEWTON_EVAL);
     float impr = scale * (cost - nc);
     float prev = cost;
