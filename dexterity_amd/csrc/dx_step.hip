@@ -1080,6 +1080,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
       bool act = q < ng;
       if (__ballot(act) == 0) break;
       trips++;
+
       NpOut o;
       o.wr = false;
       o.rank = 0;
@@ -1353,55 +1354,101 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     nrow += tot;
   }
   SYNC();
-  // 4. contacts: sparse frame jacobian, then pyramid rows
+  // 4. contacts: sparse frame jacobian, then pyramid rows.  Lane = contact (ncon <=
+  // DX_NCON_MAX <= 64) for the support masks and record fields; then the Jacobian entries
+  // flattened over (contact, support dof) items -- every item one lane, no serial walk
+  // over a contact's dofs -- and the frame velocities J qvel as jac_vec's gather.
+  static_assert(DX_NCON_MAX <= DX_WAVE, "one lane per contact");
   float* cdof = c.f(c.L.cdof);
   float* rcom = c.f(c.L.rcom);
   unsigned char* cj_idx = (unsigned char*)c.f(c.L.cj_idx);
   float* cj_val = c.f(c.L.cj_val);
   float* cq = c.f(c.L.cq);
-  for (int ci = LANE; ci < ncon; ci += DX_WAVE) {
-    float* r = con + DX_CON_STRIDE * ci;
-    const bool own = ci == LANE;
-    int gp = __float_as_int(r[13]);
-    uint64_t c1, c2;
-    int r1, r2;  // root trees of the two bodies: a dof of c1 ^ c2 is in c1 (tree r1) or c2 (tree r2)
-    if (own) {
-      c1 = cc1; c2 = cc2; r1 = cr1; r2 = cr2;
-    } else {
-      int b1 = m.geom_bodyid[m.gpair_geom[2 * gp]], b2 = m.geom_bodyid[m.gpair_geom[2 * gp + 1]];
-      c1 = m.body_chain[b1]; c2 = m.body_chain[b2];
-      r1 = m.body_rootidx[b1]; r2 = m.body_rootidx[b2];
-    }
-    uint64_t sup = c1 ^ c2;
-    int nnz = 0;
-    float vel[3] = {0, 0, 0};
-    while (sup && nnz < DX_DOFMAX) {
-      int d = __ffsll((long long)sup) - 1;
-      sup &= sup - 1;
-      float sgn = (c2 >> d) & 1ull ? 1.f : -1.f;
-      const float* rc = rcom + 3 * (((c1 >> d) & 1ull) ? r1 : r2);
-      const float* cd = cdof + 6 * d;
-      float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
-      float t[3];
-      cross3(t, cd, off);
-      float jp[3] = {cd[3] + t[0], cd[4] + t[1], cd[5] + t[2]};
-      cj_idx[ci * DX_DOFMAX + nnz] = (unsigned char)d;
-      for (int k = 0; k < 3; k++) {
-        float v = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
-        cj_val[(ci * 3 + k) * DX_DOFMAX + nnz] = v;
-        vel[k] += v * qvel[d];
-      }
-      nnz++;
-    }
-    if (sup) I[I_OVF] |= 4;
-    for (int k = 0; k < 3; k++) cq[3 * ci + k] = vel[k];  // frame velocities (J qvel)
-    int nr = (own ? ccd : m.gpair_condim[gp]) == 1 ? 1 : 4;
-    r[14] = __int_as_float(nnz | (nr << 8));
-    r[16] = own ? cfr0 : m.gpair_friction[5 * gp];
-    r[17] = own ? cfr1 : m.gpair_friction[5 * gp + 1];
-    uint64_t sp = c1 ^ c2;
+  int nnz = 0;
+  const uint64_t sp = cok ? cc1 ^ cc2 : 0ull;
+  if (cok) {
+    float* r = con + DX_CON_STRIDE * LANE;
+    const int np = __popcll(sp);
+    nnz = min(np, DX_DOFMAX);
+    if (np > DX_DOFMAX) I[I_OVF] |= 4;
+    r[14] = __int_as_float(nnz | ((ccd == 1 ? 1 : 4) << 8));
+    r[16] = cfr0;
+    r[17] = cfr1;
     r[18] = __int_as_float((int)(uint32_t)sp);
     r[19] = __int_as_float((int)(uint32_t)(sp >> 32));
+  }
+  {
+    const int incl = wave_incl_scan(nnz);
+    const int excl = incl - nnz;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    const unsigned splo = (unsigned)sp, sphi = (unsigned)(sp >> 32);
+    const unsigned c1lo = (unsigned)cc1, c1hi = (unsigned)(cc1 >> 32);
+    const unsigned c2lo = (unsigned)cc2, c2hi = (unsigned)(cc2 >> 32);
+    for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+      const int t = min(base + LANE, total - 1);
+      int ci = 0;  // last contact whose first item is <= t
+#pragma unroll
+      for (int st = 16; st >= 1; st >>= 1) {
+        const int mid = ci + st;
+        const int em = __shfl(excl, mid & 63, 64);
+        if (mid < ncon && em <= t) ci = mid;
+      }
+      int q = t - __shfl(excl, ci, 64);
+      const int slot = q;
+      // the q-th set bit of the contact's support mask: 32-bit half, then halving
+      // windows by popcount
+      const unsigned lo = (unsigned)__shfl((int)splo, ci, 64), hi = (unsigned)__shfl((int)sphi, ci, 64);
+      const int plo = __popc(lo);
+      unsigned w = q < plo ? lo : hi;
+      int d = q < plo ? 0 : 32;
+      q = q < plo ? q : q - plo;
+#pragma unroll
+      for (int h = 16; h >= 1; h >>= 1) {
+        const unsigned low = w & ((1u << h) - 1u);
+        const int pc = __popc(low);
+        const bool up = q >= pc;
+        q = up ? q - pc : q;
+        w = up ? (w >> h) : low;
+        d += up ? h : 0;
+      }
+      // (every shuffle unconditional: a shuffle under a divergent select would read
+      // inactive source lanes)
+      const unsigned a1l = (unsigned)__shfl((int)c1lo, ci, 64), a1h = (unsigned)__shfl((int)c1hi, ci, 64);
+      const unsigned a2l = (unsigned)__shfl((int)c2lo, ci, 64), a2h = (unsigned)__shfl((int)c2hi, ci, 64);
+      const int t1 = __shfl(cr1, ci, 64), t2 = __shfl(cr2, ci, 64);
+      const unsigned b1 = d < 32 ? a1l >> d : a1h >> (d - 32);
+      const unsigned b2 = d < 32 ? a2l >> d : a2h >> (d - 32);
+      const int rt = (b1 & 1u) ? t1 : t2;
+      const float sgn = (b2 & 1u) ? 1.f : -1.f;
+      const float* r = con + DX_CON_STRIDE * ci;
+      const float* rc = rcom + 3 * rt;
+      const float* cd = cdof + 6 * d;
+      const float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
+      float tq[3];
+      cross3(tq, cd, off);
+      const float jp[3] = {cd[3] + tq[0], cd[4] + tq[1], cd[5] + tq[2]};
+      if (base + LANE < total) {
+        cj_idx[ci * DX_DOFMAX + slot] = (unsigned char)d;
+#pragma unroll
+        for (int k = 0; k < 3; k++)
+          cj_val[(ci * 3 + k) * DX_DOFMAX + slot] = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
+      }
+    }
+  }
+  SYNC();
+  // frame velocities (J qvel), lane = (contact, frame axis)
+  for (int t = LANE; t < 3 * ncon; t += DX_WAVE) {
+    const int ci = t / 3, k = t - 3 * ci;
+    const int nz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
+    float v = 0;
+#pragma unroll
+    for (int q = 0; q < DX_DOFMAX; q++) {  // unguarded loads; slots past nnz are not summed
+      const float jv = cj_val[(ci * 3 + k) * DX_DOFMAX + q];
+      const float xv = qvel[cj_idx[ci * DX_DOFMAX + q]];
+      const float tt = v + jv * xv;
+      v = q < nz ? tt : v;
+    }
+    cq[t] = v;
   }
   SYNC();
   for (int base = 0; base < ncon; base += DX_WAVE) {
@@ -1657,14 +1704,13 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
   if (LANE < n) y[LANE] = s;
 }
 
+template <class Ctx>
+__device__ __forceinline__ void jac_rows(const Ctx& c, const float* x, float* out);
 // J x for every row -> out[r]; uses cq as contact-frame scratch.  The contact
 // frame rows are gathered with DX_DOFMAX independent reads per lane.
 template <class Ctx>
 __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out) {
-  const DevModel& m = c.mdl();
-  int nefc = c.I[I_NEFC];
   int ncon = c.I[I_NCON];
-  const int* meta = (const int*)c.f(c.L.efc_meta);
   const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
   float* cq = c.f(c.L.cq);
@@ -1683,6 +1729,16 @@ __device__ __forceinline__ void jac_vec(const Ctx& c, const float* x, float* out
     cq[t] = s;
   }
   SYNC();
+  jac_rows(c, x, out);
+}
+// the rows of J x from the contact-frame products in cq (jac_vec's second pass)
+template <class Ctx>
+__device__ __forceinline__ void jac_rows(const Ctx& c, const float* x, float* out) {
+  const DevModel& m = c.mdl();
+  const int nefc = c.I[I_NEFC];
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* cq = c.f(c.L.cq);
+  const float* con = c.f(c.L.con);
   for (int r = LANE; r < nefc; r += DX_WAVE) {
     int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
     float v;

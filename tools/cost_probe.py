@@ -6,6 +6,7 @@ warm-up, and estimates how much of the launch the wave slots sit idle: with S wa
 slots (8 per CU) and longest-first dispatch the makespan is bounded below by both
 sum(cost) / S and max(cost).
 """
+import ctypes
 import os
 import sys
 
@@ -19,10 +20,18 @@ def main(nenv=4096, steps=60):
     env = manipulation.load("reorient", "state_dense", seed=1, num_envs=nenv, device=0)
     env.reset()
     costs = []
+    L = _lib.load()
+    kms = []
     for i in range(steps):
+        if i >= 10:
+            _lib.check(L.dx_timing_enable(env.physics.ptr, 1))
+            _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int32())))
         env.step(env.sample_actions(i), device_action=True)
         if i >= 10:
             costs.append(env.physics.get(_lib.STEP_COST).ravel().astype(np.float64) * 1024)
+            kt, kn = ctypes.c_double(), ctypes.c_int32()
+            _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(kt), ctypes.byref(kn)))
+            kms.append(kt.value / max(kn.value, 1))
     c = np.array(costs)
     os.makedirs("gpurun_out", exist_ok=True)
     np.save("gpurun_out/costs.npy", c.astype(np.float32))
@@ -31,6 +40,10 @@ def main(nenv=4096, steps=60):
     print(f"cycles per env-step: mean {c.mean():.3e} p50 {np.median(c):.3e} p90 {np.percentile(c, 90):.3e} "
           f"p99 {np.percentile(c, 99):.3e} max {c.max():.3e}")
     print(f"per-step sum/slots {np.mean(c.sum(axis=1) / slots):.3e}  per-step max {np.mean(c.max(axis=1)):.3e}")
+    clk = float(os.environ.get("DX_CLOCK_MHZ", "2394")) * 1e6
+    km = float(np.mean(kms))
+    print(f"step kernel {km:.4f} ms = {km * 1e-3 * clk:.3e} cycles at {clk / 1e6:.0f} MHz; "
+          f"slot utilisation sum(cost)/(slots x kernel) = {np.mean(c.sum(axis=1)) / (slots * km * 1e-3 * clk):.3f}")
     print("per-env mean cost deciles:", np.round(np.percentile(per, np.arange(0, 101, 10)) / 1e6, 3))
     # how well the last step's cost predicts this step's (what longest-first relies on)
     cc = [np.corrcoef(c[t], c[t - 1])[0, 1] for t in range(1, len(c))]
