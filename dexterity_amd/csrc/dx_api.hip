@@ -688,9 +688,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, B0 + r4(ntri));
   L.cand_max = DX_CAND_MAX;
   L.cand = B0;
-  // + MPR portal points of the DX_NGRP narrowphase groups (36 words each), then the
+  // + MPR portal points of up to DX_NGRP_MAX narrowphase groups (36 words each), then the
   // candidates' pair records (float4 per candidate slot: cand_max - 2 * (cand_max / 3))
-  end = std::max(end, L.cand + L.cand_max + DX_NGRP * 36 + 4 * (L.cand_max - 2 * (L.cand_max / 3)));
+  end = std::max(end, L.cand + L.cand_max + DX_NGRP_MAX * 36 + 4 * (L.cand_max - 2 * (L.cand_max / 3)));
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_jar = take(L.nefc_max);

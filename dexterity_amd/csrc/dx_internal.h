@@ -26,10 +26,10 @@
 #ifndef DX_SWEEP
 #define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)
 #endif
-#ifndef DX_NPG
-#define DX_NPG 8          // lanes per narrowphase group (one candidate pair each)
-#endif
-#define DX_NGRP (DX_WAVE / DX_NPG)
+// narrowphase lane groups per wave: 8 of 8 lanes, or 16 of 4 lanes when a substep has
+// more than 8 candidates (dx_step.hip narrow_pass); the LDS layout reserves the portal
+// points of the larger count
+#define DX_NGRP_MAX 16
 #define DX_GOAL_RETRIES 64  // reach goal sampling: GoalInitializationError retries per goal (bounded)
 
 enum { DXG_PLANE = 0, DXG_SPHERE = 2, DXG_CAPSULE = 3, DXG_BOX = 6, DXG_MESH = 7 };

@@ -204,24 +204,30 @@ __device__ __forceinline__ void make_shape_rec(const Ctx& c, int g, float half_m
   s.margin = half_margin;
 }
 
-// Narrowphase runs DX_NGRP candidate pairs per wave, one per DX_NPG-lane group (part of a DPP
+// Narrowphase runs DX_WAVE / NPG candidate pairs per wave, one per NPG-lane group (part of a DPP
 // row).  Every lane of a group runs the same MPR control flow for its pair; the
 // groups diverge only through the exec mask.
-// DX_NPG (dx_internal.h) lanes per group: 8 (two groups per DPP row) or 16.
-#define SL (LANE & (DX_NPG - 1))
-#define GBASE (LANE & (DX_WAVE - DX_NPG))  // first lane of this lane's group
+// NPG lanes per group: 8 (two groups per DPP row) or 4 (see narrow_pass).
+// The group size is a template parameter (NPG = 8: eight pairs per wave; NPG = 4:
+// sixteen, for substeps with more than eight candidates, see collision()).
+template <int NPG> __device__ __forceinline__ int sl_() { return LANE & (NPG - 1); }
+template <int NPG> __device__ __forceinline__ int gbase_() { return LANE & (DX_WAVE - NPG); }  // first lane of the group
+#define SL sl_<NPG>()
+#define GBASE gbase_<NPG>()
+template <int NPG>
 __device__ __forceinline__ float row_max_f(float m) {
   m = fmaxf(m, dpp_f<0xB1, 0xF>(m));                      // quad_perm [1,0,3,2]
-  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));                      // quad_perm [2,3,0,1]
-  m = fmaxf(m, dpp_f<0x141, 0xF>(m));                     // row_half_mirror (8 lanes)
-  if (DX_NPG == 16) m = fmaxf(m, dpp_f<0x140, 0xF>(m));   // row_mirror (16 lanes)
+  if (NPG >= 4) m = fmaxf(m, dpp_f<0x4E, 0xF>(m));        // quad_perm [2,3,0,1]
+  if (NPG >= 8) m = fmaxf(m, dpp_f<0x141, 0xF>(m));       // row_half_mirror (8 lanes)
+  if (NPG == 16) m = fmaxf(m, dpp_f<0x140, 0xF>(m));      // row_mirror (16 lanes)
   return m;
 }
+template <int NPG>
 __device__ __forceinline__ int row_min_i(int m) {
   m = min(m, dpp_i<0xB1, 0xF>(m));
-  m = min(m, dpp_i<0x4E, 0xF>(m));
-  m = min(m, dpp_i<0x141, 0xF>(m));
-  if (DX_NPG == 16) m = min(m, dpp_i<0x140, 0xF>(m));
+  if (NPG >= 4) m = min(m, dpp_i<0x4E, 0xF>(m));
+  if (NPG >= 8) m = min(m, dpp_i<0x141, 0xF>(m));
+  if (NPG == 16) m = min(m, dpp_i<0x140, 0xF>(m));
   return m;
 }
 
@@ -265,11 +271,12 @@ __device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i,
 // cell's list is sorted by vertex index, a whole hull is scanned in index order, so
 // this is the vertex the oracle's serial scan returns); its coordinates come from the
 // lane that scanned it, found by ballot and read through ds_bpermute.
+template <int NPG>
 __device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
-  float vmax = row_max_f(h.d);
-  int bi = row_min_i(h.d == vmax ? h.i : 0x7fffffff);
+  float vmax = row_max_f<NPG>(h.d);
+  int bi = row_min_i<NPG>(h.d == vmax ? h.i : 0x7fffffff);
   const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
-  const unsigned grp = (unsigned)(own >> GBASE) & ((1u << DX_NPG) - 1u);
+  const unsigned grp = (unsigned)(own >> GBASE) & ((1u << NPG) - 1u);
   int src = GBASE | (grp ? __builtin_ctz(grp) : 0);
   lp[0] = __shfl(h.x, src, 64);
   lp[1] = __shfl(h.y, src, 64);
@@ -298,7 +305,6 @@ __device__ __forceinline__ int hull_cell(const float* ld, int n) {
 // is not binned / a zero direction -- two 16-B loads per lane, one memory round trip;
 // then, rarely, an overflow run: the rest of a cell whose slot 15 is a header, or the
 // rest of a whole-hull scan.
-constexpr int DX_SLK = 16 / DX_NPG;  // block slots per lane
 struct HullScan {
   HullBest h;
   const DXG float4* ov;  // overflow run (a valid address even when empty)
@@ -318,11 +324,13 @@ __device__ __forceinline__ void hull_block(const Shape& s, const float* ld, cons
     }
   }
 }
-__device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[DX_SLK],
+template <int NPG>
+__device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[16 / NPG],
                                                 const DXG float4* blk, int n1, bool cell, HullScan& H) {
+  constexpr int DX_SLK = 16 / NPG;  // block slots per lane
 #pragma unroll
   for (int u = 0; u < DX_SLK; u++) {
-    const int sl = u * DX_NPG + SL;
+    const int sl = u * NPG + SL;
     const int idx = cell ? __float_as_int(v[u].w) : sl;
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < n1 && idx >= 0);
   }
@@ -332,9 +340,9 @@ __device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld,
   H.cell = cell;
   H.ov = blk;
   H.nov = 0;
-  const bool hdr = cell && SL == DX_NPG - 1 && __float_as_int(v[DX_SLK - 1].w) == -2;
+  const bool hdr = cell && SL == NPG - 1 && __float_as_int(v[DX_SLK - 1].w) == -2;
   if (__any(hdr)) {
-    const int src = GBASE | (DX_NPG - 1);
+    const int src = GBASE | (NPG - 1);
     const int tag = __shfl(__float_as_int(v[DX_SLK - 1].w), src, 64);
     const int off = __shfl(__float_as_int(v[DX_SLK - 1].x), src, 64);
     const int cnt = __shfl(__float_as_int(v[DX_SLK - 1].y), src, 64);
@@ -348,10 +356,11 @@ __device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld,
     H.nov = s.nvert - 16;
   }
 }
-__device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)[DX_SLK], int base, HullScan& H) {
+template <int NPG>
+__device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)[16 / NPG], int base, HullScan& H) {
 #pragma unroll
-  for (int u = 0; u < DX_SLK; u++) {
-    const int sl = base + u * DX_NPG + SL;
+  for (int u = 0; u < 16 / NPG; u++) {
+    const int sl = base + u * NPG + SL;
     const int idx = H.cell ? __float_as_int(v[u].w) : 16 + sl;
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < H.nov && idx >= 0);
   }
@@ -364,12 +373,19 @@ __device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)
 // computes one cube-map cell, one local direction, one reduction (over its quad: two DPP
 // steps) and one world transform, and keeps one Shape.  The vertex arithmetic and the
 // first-maximiser rule are those of the oracle's serial scan.
-constexpr int DX_SLH = 16 / (DX_NPG / 2);  // block slots per lane of a half group
-static_assert(DX_NPG == 8, "the split support pairs the two quads of an 8-lane group");
-__device__ __forceinline__ bool half_b() { return (SL & 4) != 0; }  // this lane holds B
+// (NPG = 4: two lanes per half, eight slots each, halves swapped by quad_perm [2,3,0,1])
+template <int NPG> __device__ __forceinline__ bool half_b() { return (SL & (NPG / 2)) != 0; }  // this lane holds B
+// the other half's value: lane i <-> 7 - i (NPG 8) or i ^ 2 (NPG 4)
+template <int NPG> __device__ __forceinline__ float half_swap(float v) {
+  static_assert(NPG == 8 || NPG == 4, "groups of 8 or 4 lanes");
+  return NPG == 8 ? dpp_f<0x141, 0xF>(v) : dpp_f<0x4E, 0xF>(v);
+}
+template <int NPG>
 __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, float* outA, float* outB) {
-  const bool hb = half_b();
-  const int q = SL & 3;
+  constexpr int H = NPG / 2;          // lanes per half
+  constexpr int DX_SLH = 16 / H;      // block slots per lane of a half group
+  const bool hb = half_b<NPG>();
+  const int q = SL & (H - 1);
   const float sg = hb ? -1.f : 1.f;
   const float d[3] = {sg * dir[0], sg * dir[1], sg * dir[2]};
   float ld[3];
@@ -387,21 +403,21 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
     float4 v[DX_SLH];
 #pragma unroll
     for (int u = 0; u < DX_SLH; u++) {
-      const int sl = 4 * u + q;
+      const int sl = H * u + q;
       v[u] = blk[sl < n1 ? sl : 0];
     }
 #pragma unroll
     for (int u = 0; u < DX_SLH; u++) {
-      const int sl = 4 * u + q;
+      const int sl = H * u + q;
       const int idx = cell ? __float_as_int(v[u].w) : sl;
       hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, mesh && sl < n1 && idx >= 0);
     }
     // overflow run: slot 15 of a cell (its quad's last lane, last load) may be a header
     const DXG float4* ov = blk;
     int nov = 0;
-    const bool hdr = mesh && cell && q == 3 && __float_as_int(v[DX_SLH - 1].w) == -2;
+    const bool hdr = mesh && cell && q == H - 1 && __float_as_int(v[DX_SLH - 1].w) == -2;
     if (__any(hdr)) {
-      const int src = (LANE & ~3) | 3;
+      const int src = (LANE & ~(H - 1)) | (H - 1);
       const int tag = __shfl(__float_as_int(v[DX_SLH - 1].w), src, 64);
       const int off = __shfl(__float_as_int(v[DX_SLH - 1].x), src, 64);
       const int cnt = __shfl(__float_as_int(v[DX_SLH - 1].y), src, 64);
@@ -417,25 +433,25 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
     for (int base = 0; __any(base < nov); base += 16) {
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
-        const int sl = base + 4 * u + q;
+        const int sl = base + H * u + q;
         v[u] = ov[sl < nov ? sl : 0];
       }
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
-        const int sl = base + 4 * u + q;
+        const int sl = base + H * u + q;
         const int idx = cell ? __float_as_int(v[u].w) : 16 + sl;
         hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < nov && idx >= 0);
       }
     }
-    // quad reduction: the lowest vertex index among the maxima, coordinates from its lane
+    // half reduction: the lowest vertex index among the maxima, coordinates from its lane
     float vmax = fmaxf(h.d, dpp_f<0xB1, 0xF>(h.d));
-    vmax = fmaxf(vmax, dpp_f<0x4E, 0xF>(vmax));
+    if (H == 4) vmax = fmaxf(vmax, dpp_f<0x4E, 0xF>(vmax));
     int bi = h.d == vmax ? h.i : 0x7fffffff;
     bi = min(bi, dpp_i<0xB1, 0xF>(bi));
-    bi = min(bi, dpp_i<0x4E, 0xF>(bi));
+    if (H == 4) bi = min(bi, dpp_i<0x4E, 0xF>(bi));
     const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
-    const unsigned qb = (unsigned)(own >> (LANE & ~3)) & 15u;
-    const int src = (LANE & ~3) | (qb ? __builtin_ctz(qb) : 0);
+    const unsigned qb = (unsigned)(own >> (LANE & ~(H - 1))) & ((1u << H) - 1u);
+    const int src = (LANE & ~(H - 1)) | (qb ? __builtin_ctz(qb) : 0);
     const float hx = __shfl(h.x, src, 64), hy = __shfl(h.y, src, 64), hz = __shfl(h.z, src, 64);
     if (mesh) { lp[0] = hx; lp[1] = hy; lp[2] = hz; }
   }
@@ -445,14 +461,16 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
   support_world(S, lp, d, out);
 #pragma unroll
   for (int k = 0; k < 3; k++) {
-    const float o = dpp_f<0x141, 0xF>(out[k]);  // row_half_mirror: the other half's point
+    const float o = half_swap<NPG>(out[k]);  // the other half's point
     outA[k] = hb ? o : out[k];
     outB[k] = hb ? out[k] : o;
   }
 }
 
 // Support of one shape along dir (group-cooperative for hulls).
+template <int NPG>
 __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, float* out) {
+  constexpr int DX_SLK = 16 / NPG;
   float ld[3], lp[3];
   mattvec3(ld, s.mat, dir);
   if (s.type == DXG_MESH) {
@@ -465,19 +483,19 @@ __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, fl
     float4 v[DX_SLK];
 #pragma unroll
     for (int u = 0; u < DX_SLK; u++) {
-      const int sl = u * DX_NPG + SL;
+      const int sl = u * NPG + SL;
       v[u] = blk[sl < n1 ? sl : 0];
     }
-    hull_take_block(s, ld, v, blk, n1, cell, S);
+    hull_take_block<NPG>(s, ld, v, blk, n1, cell, S);
     for (int base = 0; __any(base < S.nov); base += 16) {
 #pragma unroll
       for (int u = 0; u < DX_SLK; u++) {
-        const int sl = base + u * DX_NPG + SL;
+        const int sl = base + u * NPG + SL;
         v[u] = S.ov[sl < S.nov ? sl : 0];
       }
-      if (base < S.nov) hull_take_run(ld, v, base, S);
+      if (base < S.nov) hull_take_run<NPG>(ld, v, base, S);
     }
-    hull_reduce(S.h, lp);
+    hull_reduce<NPG>(S.h, lp);
   } else {
     support_prim(s, ld, lp);
   }
@@ -522,11 +540,12 @@ struct MprState {
 // cached: a separating direction of this pair from an earlier collision pass (world
 // frame), tried first (phase -1): if the supports along it do not reach the origin the
 // pair is separated -- the verdict MPR's own tests give -- in one support pass.
+template <int NPG>
 __device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const float* cached) {
   MPoint P0;
-  const bool hb = half_b();
+  const bool hb = half_b<NPG>();
   for (int k = 0; k < 3; k++) {
-    const float o = dpp_f<0x141, 0xF>(G.center[k]);  // the other half's shape centre
+    const float o = half_swap<NPG>(G.center[k]);  // the other half's shape centre
     P0.a[k] = hb ? o : G.center[k];
     P0.b[k] = hb ? G.center[k] : o;
   }
@@ -549,6 +568,7 @@ __device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const floa
 // portal slot chosen per group.  Each phase performs exactly the arithmetic of libccd's
 // structure (the oracle's dxo_mpr), so the results are unchanged; only the separated,
 // degenerate and final exits branch.
+template <int NPG>
 __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& depth, float* normal,
                                         float* pos, NpStats& st) {
   const float tol = 1e-6f;
@@ -558,7 +578,7 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
   for (int k = 0; k < 3; k++) { v0[k] = P[k]; v1[k] = P[9 + k]; v2[k] = P[18 + k]; v3[k] = P[27 + k]; }
   MPoint p;
   float* dir = S.dir;
-  support_pair(G, dir, p.a, p.b);
+  support_pair<NPG>(G, dir, p.a, p.b);
   sub3(p.v, p.a, p.b);
   st.support++;
   const int ph = S.phase;
@@ -763,7 +783,7 @@ __device__ __forceinline__ bool pair_is_prim(const DevModel& m, int gp) {
 }
 // Primitive narrowphase of one geom pair by one lane group; returns the group's
 // contact count (group-uniform, at most 4).
-template <class Ctx>
+template <int NPG, class Ctx>
 __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, NpStats& st) {
   const DevModel& m = c.mdl();
   int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
@@ -787,32 +807,44 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
       float ext = 0;
       for (int k = 0; k < 3; k++) ext += fabsf(bm[k] * n[0] + bm[3 + k] * n[1] + bm[6 + k] * n[2]) * sz[k];
       if (cdist > margin + ext) return 0;
-      // corners i = 0..7 on group lanes 0..7; keep the first 4 (in corner order) within the margin
-      bool hit = false;
-      float v[3] = {0, 0, 0}, dist = 0;
-      if (SL < 8) {
-        int i = SL;
+      // keep the first 4 corners (in corner order) within the margin: the group's lanes
+      // test corners SL, SL + NPG, ...; lane k < 4 then emits the k-th such corner
+      auto corner = [&](int i, float* v) {
         float s0 = (i & 1) ? sz[0] : -sz[0], s1 = (i & 2) ? sz[1] : -sz[1], s2 = (i & 4) ? sz[2] : -sz[2];
         for (int k = 0; k < 3; k++) v[k] = bp[k] + bm[3 * k] * s0 + bm[3 * k + 1] * s1 + bm[3 * k + 2] * s2;
         float r[3];
         sub3(r, v, pp);
-        dist = dot3(r, n);
-        hit = dist <= margin;
+        return dot3(r, n);
+      };
+      unsigned cm = 0;  // corners within the margin, bit i = corner i
+#pragma unroll
+      for (int r8 = 0; r8 < 8 / NPG; r8++) {
+        float v[3];
+        const bool hit = corner(SL + NPG * r8, v) <= margin;
+        cm |= (unsigned)((__ballot(hit) >> GBASE) & ((1ull << NPG) - 1ull)) << (NPG * r8);
       }
-      unsigned gm = (unsigned)((__ballot(hit) >> GBASE) & ((1ull << DX_NPG) - 1ull));
-      int rank = __popc(gm & ((1u << SL) - 1u));
-      o.wr = hit && rank < 4;
-      o.rank = rank;
+      const int nh = __popc(cm);
+      int ik = 0, seen = 0;  // the SL-th set corner
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const bool on = (cm >> b) & 1u;
+        ik = (on && seen == SL) ? b : ik;
+        seen += on;
+      }
+      float v[3];
+      const float dist = corner(ik, v);
+      o.wr = SL < min(4, nh);
+      o.rank = SL;
       o.dist = dist;
       for (int k = 0; k < 3; k++) o.pos[k] = v[k] - 0.5f * dist * n[k];
-      return min(4, __popc(gm));
+      return min(4, nh);
     }
     st.plane_convex++;
     Shape s;
     make_shape(c, g2, 0, s);
     float nd[3] = {-n[0], -n[1], -n[2]};
     float sp[3];
-    support_grp(s, nd, sp);
+    support_grp<NPG>(s, nd, sp);
     float r[3];
     sub3(r, sp, pp);
     float dist = dot3(r, n);
@@ -861,6 +893,112 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
   return 0;
 }
 
+// 3. narrowphase.  The wave's DX_WAVE / NPG lane groups walk the candidate list in one
+// loop, each taking the next unassigned candidate when its pair is done, so a group
+// never waits for another group's pair.  Contacts are written unordered together with
+// their key (candidate, rank); collision() puts them into candidate order, which gives
+// the list of the serial loop.  Returns the contact count (before the DX_NCON_MAX cap).
+template <int NPG, class Ctx>
+__device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcand, const float4* gcrec, float* con) {
+  int ncon = 0;
+  NpStats st = {0, 0, 0, 0, 0, 0, 0};
+  {
+    const int grp = LANE / NPG;
+    int q = grp, next = DX_WAVE / NPG;
+    bool fresh = true;
+    int gp = 0;
+    float margin = 0;
+    Shape G;  // the pair's first geom on the group's first half of lanes, its second on the other
+    MprState M;
+    bool cached = false;
+    int trips = 0;
+    M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
+    for (;;) {
+      bool act = q < ng;
+      if (__ballot(act) == 0) break;
+      trips++;
+
+      NpOut o;
+      o.wr = false;
+      o.rank = 0;
+      int cnt = 0;
+      bool done = false;
+      if (act) {
+        bool stepping = !fresh;
+        if (fresh) {
+          gp = gcand[q];
+          const float4 pr = gcrec[q];
+          if (__float_as_int(pr.w)) {
+            cnt = narrowphase_prim<NPG>(c, gp, o, st);
+            done = true;
+          } else {
+            st.mpr++;
+            margin = pr.z;
+            make_shape_rec(c, __float_as_int(half_b<NPG>() ? pr.y : pr.x), 0.5f * margin, G);
+            float4 ce = c.sep ? c.sep[gp & (DX_SEP_SLOTS - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            cached = __float_as_int(ce.w) == gp + 1;
+            const float cd[3] = {ce.x, ce.y, ce.z};
+            mpr_init<NPG>(G, M, cached ? cd : nullptr);
+            fresh = false;
+            stepping = true;
+          }
+        }
+        if (stepping) {
+          float depth, nrm[3], pos[3];
+          int r = mpr_step<NPG>(G, M, depth, nrm, pos, st);
+          if (r && c.sep && SL == 0) {
+            // remember a separating direction (unless it is the cached one, still
+            // separating: phase -1); forget it once the pair touches
+            const int so = 16 * (gp & (DX_SEP_SLOTS - 1));
+            if (r == 1 && M.phase != -1)
+              st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1)));
+            else if (cached) st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(0.f, 0.f, 0.f, 0.f));
+          }
+          if (r) {
+            done = true;
+            if (r == 2) {
+              st.hit++;
+              cnt = 1;
+              o.wr = SL == 0;
+              o.dist = margin - depth;
+              for (int k = 0; k < 3; k++) { o.n[k] = nrm[k]; o.pos[k] = pos[k]; }
+            }
+          }
+        }
+      }
+      if (__ballot(cnt > 0)) {  // most loop trips produce no contact
+        // contacts of the groups before this one (cnt is uniform within a group)
+        const int cinc = wave_incl_scan(SL == 0 ? cnt : 0);
+        const int pre = __shfl(cinc, GBASE, 64) - cnt;
+        int slot = ncon + pre + o.rank;
+        if (o.wr && slot < DX_NCON_MAX) {
+          write_contact(con, slot, o.pos, o.n, o.dist, gp);
+          con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
+        }
+        ncon += __builtin_amdgcn_readlane(cinc, 63);
+      }
+      // a group that finished its pair takes the next unassigned candidate (in group
+      // order), so a long MPR on one group no longer holds back the others' queues;
+      // the contact keys still sort the list into candidate order below
+      const uint64_t fin = __ballot(done && SL == 0);
+      if (done) {
+        q = next + __popcll(fin & ((1ull << GBASE) - 1ull));
+        fresh = true;
+      }
+      next += __popcll(fin);
+    }
+    stage_count(c, CNT_NP_TRIPS, trips);
+  }
+  SYNC();
+  if (c.stage_acc) {
+    bool lead = SL == 0;
+    int v[7] = {st.plane_box, st.plane_convex, st.capsule, st.mpr, st.support, st.hit, st.maxit};
+#pragma unroll
+    for (int k = 0; k < 7; k++) stage_count(c, CNT_PLANE_BOX + k, wave_sum_i(lead ? v[k] : 0));
+  }
+  return ncon;
+}
+
 // broadphase (body spheres, lanes over body pairs) -> flattened mid-phase (geom
 // spheres, lanes over every geom pair of the surviving body pairs) -> narrowphase
 // (whole wave per pair).  Writes contact records into LDS.
@@ -884,7 +1022,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int half = cmax / 3;
   int* pref = cand + half;
   int nbc = 0, ngp = 0;
-  int* sl = (int*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP * MP_WORDS);  // the pair-record area, unused yet
+  int* sl = (int*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP_MAX * MP_WORDS);  // the pair-record area, unused yet
   const int slcap = 4 * (cmax - 2 * half);
   int nsl = 0;
   auto flush = [&]() {
@@ -988,7 +1126,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   int gmax = cmax - 2 * half;
   // pair records of the surviving candidates, after the four groups' portal points
   // (dx_api.hip layout reserves 4 * gmax words there)
-  float4* gcrec = (float4*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP * MP_WORDS);
+  float4* gcrec = (float4*)(c.f(c.L.cand + c.L.cand_max) + DX_NGRP_MAX * MP_WORDS);
   int ng = 0;
   int total = nbc > 0 ? pref[nbc] : 0;
   for (int base = 0; base < total; base += DX_WAVE) {
@@ -1057,101 +1195,12 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   stage_count(c, CNT_MID_KEEP, ng);
   SYNC();
   stage_mark(c, ST_MID);
-  // 3. narrowphase.  DX_NGRP lane groups walk the candidate list in this one loop,
-  // each taking the next unassigned candidate when its pair is done, so a group
-  // never waits for another group's pair.  Contacts are written unordered together with
-  // their key (candidate, rank) and put into candidate order below, which gives the
-  // list of the serial loop.
+  // 3. narrowphase (narrow_pass): eight pairs per wave, or sixteen (four-lane groups)
+  // when the substep has more than eight candidates -- the contact-rich states whose
+  // serial chains of pairs per group bound the heaviest environments' substeps
   float* con = c.f(c.L.con);
-  int ncon = 0;
-  NpStats st = {0, 0, 0, 0, 0, 0, 0};
-  {
-    const int grp = LANE / DX_NPG;
-    int q = grp, next = DX_NGRP;
-    bool fresh = true;
-    int gp = 0;
-    float margin = 0;
-    Shape G;  // the pair's first geom on lanes 0-3 of the group, its second on lanes 4-7
-    MprState M;
-    bool cached = false;
-    int trips = 0;
-    M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
-    for (;;) {
-      bool act = q < ng;
-      if (__ballot(act) == 0) break;
-      trips++;
-
-      NpOut o;
-      o.wr = false;
-      o.rank = 0;
-      int cnt = 0;
-      bool done = false;
-      if (act) {
-        bool stepping = !fresh;
-        if (fresh) {
-          gp = gcand[q];
-          const float4 pr = gcrec[q];
-          if (__float_as_int(pr.w)) {
-            cnt = narrowphase_prim(c, gp, o, st);
-            done = true;
-          } else {
-            st.mpr++;
-            margin = pr.z;
-            make_shape_rec(c, __float_as_int(half_b() ? pr.y : pr.x), 0.5f * margin, G);
-            float4 ce = c.sep ? c.sep[gp & (DX_SEP_SLOTS - 1)] : make_float4(0.f, 0.f, 0.f, 0.f);
-            cached = __float_as_int(ce.w) == gp + 1;
-            const float cd[3] = {ce.x, ce.y, ce.z};
-            mpr_init(G, M, cached ? cd : nullptr);
-            fresh = false;
-            stepping = true;
-          }
-        }
-        if (stepping) {
-          float depth, nrm[3], pos[3];
-          int r = mpr_step(G, M, depth, nrm, pos, st);
-          if (r && c.sep && SL == 0) {
-            // remember a separating direction (unless it is the cached one, still
-            // separating: phase -1); forget it once the pair touches
-            const int so = 16 * (gp & (DX_SEP_SLOTS - 1));
-            if (r == 1 && M.phase != -1)
-              st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1)));
-            else if (cached) st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(0.f, 0.f, 0.f, 0.f));
-          }
-          if (r) {
-            done = true;
-            if (r == 2) {
-              st.hit++;
-              cnt = 1;
-              o.wr = SL == 0;
-              o.dist = margin - depth;
-              for (int k = 0; k < 3; k++) { o.n[k] = nrm[k]; o.pos[k] = pos[k]; }
-            }
-          }
-        }
-      }
-      if (__ballot(cnt > 0)) {  // most loop trips produce no contact
-        // contacts of the groups before this one (cnt is uniform within a group)
-        const int cinc = wave_incl_scan(SL == 0 ? cnt : 0);
-        const int pre = __shfl(cinc, GBASE, 64) - cnt;
-        int slot = ncon + pre + o.rank;
-        if (o.wr && slot < DX_NCON_MAX) {
-          write_contact(con, slot, o.pos, o.n, o.dist, gp);
-          con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
-        }
-        ncon += __builtin_amdgcn_readlane(cinc, 63);
-      }
-      // a group that finished its pair takes the next unassigned candidate (in group
-      // order), so a long MPR on one group no longer holds back the others' queues;
-      // the contact keys still sort the list into candidate order below
-      const uint64_t fin = __ballot(done && SL == 0);
-      if (done) {
-        q = next + __popcll(fin & ((1ull << GBASE) - 1ull));
-        fresh = true;
-      }
-      next += __popcll(fin);
-    }
-    stage_count(c, CNT_NP_TRIPS, trips);
-  }
+  const int ncon_raw = ng > DX_WAVE / 8 ? narrow_pass<4>(c, ng, gcand, gcrec, con) : narrow_pass<8>(c, ng, gcand, gcrec, con);
+  int ncon = ncon_raw;
   SYNC();
   // candidate order: lane k ranks record k by its key, then moves it
   {
@@ -1167,12 +1216,6 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
 #pragma unroll
       for (int e = 0; e < 14; e++) con[DX_CON_STRIDE * rank + e] = rec[e];
     }
-  }
-  if (c.stage_acc) {
-    bool lead = SL == 0;
-    int v[7] = {st.plane_box, st.plane_convex, st.capsule, st.mpr, st.support, st.hit, st.maxit};
-#pragma unroll
-    for (int k = 0; k < 7; k++) stage_count(c, CNT_PLANE_BOX + k, wave_sum_i(lead ? v[k] : 0));
   }
   stage_mark(c, ST_NP_MPR);
   if (LANE == 0 && !watch_only) I[I_NRAW] = max(I[I_NRAW], ncon);
