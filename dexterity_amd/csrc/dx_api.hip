@@ -914,6 +914,7 @@ struct dx_batch {
   DevBatch db;
   int spec;  // specialized step kernel (dx_specs.inc) or -1 for the generic one
   bool queue;  // mode-0 steps through the substep queue
+  bool qhead_zero = false;  // the last kernel on the stream zeroed the queue heads
   int* watch_list = nullptr;  // device copy of DevBatch::watch_pairs
   int slots;   // persistent workgroups of a queued launch
   float* xfrc;
@@ -1007,7 +1008,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   }
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
-  if (B.order && dx_launch_order(nenv, b->stream, B.cost, (int*)B.order) != hipSuccess) {  // a permutation
+  if (B.order && dx_launch_order(nenv, b->stream, B.cost, (int*)B.order, nullptr) != hipSuccess) {  // a permutation
     fail(DX_EHIP, "order kernel launch failed");
     dx_batch_destroy(b);
     return nullptr;
@@ -1178,7 +1179,8 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
       HIPCHK(hipMemsetAsync(B.progress, 0, (size_t)b->nenv * 4, b->stream));
       B.epoch = 1;
     }
-    HIPCHK(hipMemsetAsync(B.qhead, 0, DX_QUEUES * DX_QHEAD_STRIDE * 4, b->stream));
+    if (!b->qhead_zero) HIPCHK(hipMemsetAsync(B.qhead, 0, DX_QUEUES * DX_QHEAD_STRIDE * 4, b->stream));
+    b->qhead_zero = false;
   }
   hipEvent_t t0;
   timing_begin(b, &t0);
@@ -1190,7 +1192,12 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
     HIPCHK(dx_launch_sensor(b->nenv, ((size_t)b->model->lds.total + 6 * DX_MAX_NV) * 4, b->stream, b->dm_dev, b->db,
                             b->model->lds, b->sensor));
   // next launch: heaviest environments first (costs just measured)
-  if (mode == 0 && b->db.order) HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order));
+  // next launch: heaviest environments first (costs just measured); the same kernel
+  // zeroes the queue heads the next queued launch claims from
+  if (mode == 0 && b->db.order) {
+    HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order, b->db.qhead));
+    b->qhead_zero = true;
+  }
   return 0;
 }
 

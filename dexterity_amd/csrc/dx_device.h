@@ -724,6 +724,7 @@ __device__ __forceinline__ float wl(float v, float s, int k) {  // v with lane k
   return __int_as_float(dx_writelane_i32(__float_as_int(s), k, __float_as_int(v)));
 }
 typedef float dx_f16v __attribute__((ext_vector_type(16)));
+typedef float dx_f2v __attribute__((ext_vector_type(2)));
 // v with its lower (up = false) or upper (up = true) half-wave copied into both halves
 __device__ __forceinline__ float half_dup(float v, bool up) {
   auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
@@ -987,9 +988,29 @@ __device__ __forceinline__ void mfma_sweep_solve30(const float* A, int n, float 
     const float v1 = pc ? (j == k ? 0.f : -1.f) : rk1;
     const float a = hi ? v1 : v0;                                             // A: V[j][hi]
     const float b = hi ? fmaf(w01, v0, w11 * v1) : fmaf(w00, v0, w01 * v1);  // B: (W V^T)[hi][j]
+#if DX_SWEEP_PK
+    // two accumulator entries per packed multiply (v_pk_mul_f32) by 0 on the pivot
+    // columns' lanes, 1 elsewhere: half the instructions of one select per entry
+    const dx_f2v mk = {pc ? 0.f : 1.f, pc ? 0.f : 1.f};
+#pragma unroll
+    for (int v = 0; v < 16; v += 2) {
+      const bool z0 = 8 * (v >> 2) + 4 + (v & 3) >= k + 2, z1 = 8 * ((v + 1) >> 2) + 4 + ((v + 1) & 3) >= k + 2;
+      if (z0 && z1) {
+        dx_f2v t = {C[v], C[v + 1]};
+        t = t * mk;
+        C[v] = t.x;
+        C[v + 1] = t.y;
+      } else if (z0) {
+        C[v] = pc ? 0.f : C[v];
+      } else if (z1) {
+        C[v + 1] = pc ? 0.f : C[v + 1];
+      }
+    }
+#else
 #pragma unroll
     for (int v = 0; v < 16; v++)
       if (8 * (v >> 2) + 4 + (v & 3) >= k + 2) C[v] = pc ? 0.f : C[v];
+#endif
     const bool ph = hi == (up ? 1 : 0);
     C[vk] = ph ? 0.f : C[vk];
     C[vk + 1] = ph ? 0.f : C[vk + 1];

@@ -22,7 +22,13 @@
 #define DX_QUEUES 8         // substep queues: one per XCD (MI355X: 8 XCDs)
 #define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
+#ifndef DX_SEP_WT
+#define DX_SEP_WT 0       // 1: cache entries stored write-through (sc1), the round-2 form
+#endif
 #define DX_LDL_SLOTS 16   // tree-sparse LDL^T items: at most 16 x 64 (dx_device.h tree_solve)
+#ifndef DX_SWEEP_PK
+#define DX_SWEEP_PK 0     // sweep: pivot-column zeroing by packed multiplies (A/B switch)
+#endif
 #ifndef DX_SWEEP
 #define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)
 #endif
@@ -260,24 +266,46 @@ __device__ __forceinline__ uint32_t dx_mt_next(uint32_t* s, int nenv, int env) {
   return dx_mt_temper(y);
 }
 // RandomState.random_sample: 53-bit double from two outputs
+__device__ __forceinline__ double dx_mt_double2(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
+}
 __device__ __forceinline__ double dx_mt_double(uint32_t* s, int nenv, int env) {
-  const uint32_t a = dx_mt_next(s, nenv, env) >> 5, b = dx_mt_next(s, nenv, env) >> 6;
-  return ((double)a * 67108864.0 + (double)b) / 9007199254740992.0;
+  const uint32_t a = dx_mt_next(s, nenv, env), b = dx_mt_next(s, nenv, env);
+  return dx_mt_double2(a, b);
+}
+// The next N outputs at once: one load of the position, then the N state words as
+// independent loads (one memory round trip instead of two per output), unless the
+// block crosses a twist -- then one output at a time.
+template <int N>
+__device__ __forceinline__ void dx_mt_take(uint32_t* s, int nenv, int env, uint32_t (&out)[N]) {
+  const uint32_t pos = s[(size_t)624 * nenv + env];
+  if (pos + N <= 624) {
+#pragma unroll
+    for (int k = 0; k < N; k++) out[k] = dx_mt_temper(s[(size_t)(pos + k) * nenv + env]);
+    s[(size_t)624 * nenv + env] = pos + N;
+  } else {
+    for (int k = 0; k < N; k++) out[k] = dx_mt_next(s, nenv, env);
+  }
 }
 // [3P] dm_control composer.variation.rotations.UniformQuaternion:
 // u1, u2, u3 = random_state.uniform([0, 0, 0], [1, 2 pi, 2 pi]);
 // q = [sqrt(1-u1) sin u2, sqrt(1-u1) cos u2, sqrt(u1) sin u3, sqrt(u1) cos u3]
 // (computed in double, then rounded to the fp32 state)
-__device__ __forceinline__ void dx_mt_uniform_quat(uint32_t* s, int nenv, int env, float* q) {
+__device__ __forceinline__ void dx_mt_quat_from(const uint32_t* w, float* q) {
   const double twopi = 6.283185307179586;
-  const double u1 = dx_mt_double(s, nenv, env);
-  const double u2 = twopi * dx_mt_double(s, nenv, env);
-  const double u3 = twopi * dx_mt_double(s, nenv, env);
+  const double u1 = dx_mt_double2(w[0], w[1]);
+  const double u2 = twopi * dx_mt_double2(w[2], w[3]);
+  const double u3 = twopi * dx_mt_double2(w[4], w[5]);
   const double a = sqrt(1.0 - u1), b = sqrt(u1);
-  q[0] = (float)(a * sin(u2));  // products only: no contraction to worry about
+  q[0] = (float)(a * sin(u2));
   q[1] = (float)(a * cos(u2));
   q[2] = (float)(b * sin(u3));
   q[3] = (float)(b * cos(u3));
+}
+__device__ __forceinline__ void dx_mt_uniform_quat(uint32_t* s, int nenv, int env, float* q) {
+  uint32_t w[6];
+  dx_mt_take<6>(s, nenv, env, w);
+  dx_mt_quat_from(w, q);
 }
 
 // Counter-based RNG: splitmix64 over (seed, env, episode, draw).
@@ -298,7 +326,7 @@ int dx_spec_find(const DevModel& d, const Lds& L);
 int dx_step_occupancy(int spec, size_t lds);
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
-hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order);
+hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order, unsigned* qhead);
 
 // dx_sensor.hip: joint torque sensors from the step kernel's stash (host side)
 hipError_t dx_launch_sensor(int nenv, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,

@@ -948,11 +948,18 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
           int r = mpr_step<NPG>(G, M, depth, nrm, pos, st);
           if (r && c.sep && SL == 0) {
             // remember a separating direction (unless it is the cached one, still
-            // separating: phase -1); forget it once the pair touches
-            const int so = 16 * (gp & (DX_SEP_SLOTS - 1));
-            if (r == 1 && M.phase != -1)
-              st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1)));
-            else if (cached) st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, so, make_float4(0.f, 0.f, 0.f, 0.f));
+            // separating: phase -1); forget it once the pair touches.  Plain stores: the
+            // entry only picks the first direction MPR tries, never its verdict, so a
+            // task on another XCD that reads an older entry (its L2 has not seen this
+            // one) computes the same contacts; written through (DX_SEP_WT) every 16-B
+            // entry cost a partial-line HBM write and the next task's read a miss.
+            const bool keep = r == 1 && M.phase != -1;
+            if (keep || cached) {
+              const float4 ent = keep ? make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1))
+                                      : make_float4(0.f, 0.f, 0.f, 0.f);
+              if (DX_SEP_WT) st_sc1_f4(c.sep, 16 * DX_SEP_SLOTS, 16 * (gp & (DX_SEP_SLOTS - 1)), ent);
+              else c.sep[gp & (DX_SEP_SLOTS - 1)] = ent;
+            }
           }
           if (r) {
             done = true;
@@ -3290,10 +3297,12 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       env_store_hand(c, rec, B.hand_stride, time,
                      cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull));
     }
-    // publish: the bytes the env's next task reads (hand-off record, separating-
-    // direction cache) were stored write-through (sc1), so a drained vmcnt suffices
-    // and no release fence (a write-back of the whole XCD L2) is needed.  Profiling
-    // runs also carry stage_acc across tasks with plain stores: those keep the release.
+    // publish: the bytes the env's next task must read (the hand-off record) were
+    // stored write-through (sc1), so a drained vmcnt suffices and no release fence (a
+    // write-back of the whole XCD L2) is needed.  The separating-direction cache is
+    // stored plainly: a stale entry on another XCD changes no result (narrow_pass).
+    // Profiling runs also carry stage_acc across tasks with plain stores: those keep
+    // the release.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (B.stage_acc) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -3413,24 +3422,32 @@ int dx_spec_find(const DevModel& d, const Lds& L) {
 // last step's cost (descending, 256 buckets of 16 K shader cycles), one workgroup.
 // The order within a bucket depends on atomic timing, which only changes which CU
 // runs an environment, never its results.
-__global__ void __launch_bounds__(1024) dx_order_kernel(int nenv, const unsigned* cost, int* order) {
+// The same kernel zeroes the substep-queue heads for the next launch (qhead != nullptr):
+// no separate memset node per step.
+__global__ void __launch_bounds__(1024) dx_order_kernel(int nenv, const unsigned* cost, int* order, unsigned* qhead) {
   __shared__ int hist[256];
   __shared__ int base[256];
   const int t = threadIdx.x;
   if (t < 256) hist[t] = 0;
+  if (qhead && t < DX_QUEUES) qhead[t * DX_QHEAD_STRIDE] = 0u;
   __syncthreads();
   for (int e = t; e < nenv; e += 1024) atomicAdd(&hist[255 - (int)min(cost[e] >> 4, 255u)], 1);
   __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int k = 0; k < 256; k++) { base[k] = acc; acc += hist[k]; }
+  if (t < 64) {  // exclusive prefix of the 256 buckets: four per lane, then a wave scan
+    const int h0 = hist[4 * t], h1 = hist[4 * t + 1], h2 = hist[4 * t + 2], h3 = hist[4 * t + 3];
+    const int tot = h0 + h1 + h2 + h3;
+    const int ex = wave_incl_scan(tot) - tot;
+    base[4 * t] = ex;
+    base[4 * t + 1] = ex + h0;
+    base[4 * t + 2] = ex + h0 + h1;
+    base[4 * t + 3] = ex + h0 + h1 + h2;
   }
   __syncthreads();
   for (int e = t; e < nenv; e += 1024) order[atomicAdd(&base[255 - (int)min(cost[e] >> 4, 255u)], 1)] = e;
 }
 
-hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order) {
-  hipLaunchKernelGGL(dx_order_kernel, dim3(1), dim3(1024), 0, stream, nenv, cost, order);
+hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order, unsigned* qhead) {
+  hipLaunchKernelGGL(dx_order_kernel, dim3(1), dim3(1024), 0, stream, nenv, cost, order, qhead);
   return hipGetLastError();
 }
 

@@ -95,11 +95,13 @@ extern "C" __global__ void dx_task_pre_kernel(TaskParams P, TaskState S, DevBatc
       float* g = S.goal + P.goal_dim * env;
       dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);
       if (P.prop_qadr >= 0) {
+        uint32_t w[12];  // position (3 doubles) then the quaternion (3 doubles), one fetch
+        dx_mt_take<12>(S.mt_env, P.nenv, env, w);
         for (int k = 0; k < 3; k++)
           // random_uniform: low + (high - low) * u, rounded as numpy does (no fma)
           q[P.prop_qadr + k] = (float)__dadd_rn(P.bbox_lo_d[k], __dmul_rn(P.bbox_hi_d[k] - P.bbox_lo_d[k],
-                                                                          dx_mt_double(S.mt_env, P.nenv, env)));
-        dx_mt_uniform_quat(S.mt_env, P.nenv, env, q + P.prop_qadr + 3);
+                                                                          dx_mt_double2(w[2 * k], w[2 * k + 1])));
+        dx_mt_quat_from(w + 6, q + P.prop_qadr + 3);
       }
     } else {
       // reach.py:155-168: fingertip goal (physics rollouts) and collision-free joint
