@@ -27,7 +27,7 @@
 #endif
 #define DX_LDL_SLOTS 16   // tree-sparse LDL^T items: at most 16 x 64 (dx_device.h tree_solve)
 #ifndef DX_SWEEP_PK
-#define DX_SWEEP_PK 0     // sweep: pivot-column zeroing by packed multiplies (A/B switch)
+#define DX_SWEEP_PK 1     // sweep: pivot-column zeroing by packed multiplies (0: one select per entry)
 #endif
 #ifndef DX_SWEEP
 #define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)

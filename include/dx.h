@@ -182,7 +182,7 @@ int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
  * LAST is re-initialised by its next step and returns FIRST). */
 typedef struct dx_env dx_env;
 enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
-/* Reorient params (float[26], or float[32]), reorient.py:40-78 / task.py:120-135:
+/* Reorient params (float[26], or float[38] with the fp64 bbox), reorient.py:40-78 / task.py:120-135:
  *  0 n_sub_steps  1 hand_nq  2 hand_nv  3 prop_qposadr  4 prop_dofadr
  *  5 first fingertip site  6 n fingertips  7 successes_needed
  *  8 steps_before_changing_goal  9 fall_termination  10 success_threshold
