@@ -183,8 +183,9 @@ def main():
     collator = distributed.OutputCollator(env, comm) if comm else None
 
     def one_step(i):
-        a = env.sample_actions(i)
-        env.step(a, device_action=True)
+        # the random agent (manipulation_test.py:44-45), its actions drawn inside the step
+        # kernel: a control step is two launches (step kernel + overflow tier / order)
+        env.step_random(i)
         if collator:
             collator.gather()  # enqueued on the env stream behind the step: no host sync
 
@@ -211,24 +212,24 @@ def main():
     qerr = env.physics.debug_get("queue_timeouts")
     refuse = "substep queue timed out during the timed region" if int(qerr[0]) != 0 else ""
     # health of the timed region (include/dx.h dx_health): a diverged env, or a capacity
-    # overflow that truncates work (candidate lists, Jacobian dofs, constraint rows),
-    # voids the number.  Contacts beyond the 32 kept per env-substep (MuJoCo keeps up to
-    # nconmax = 200) occur at ~3.4e-6 of env-substeps on this workload (34 in 1.0e7,
-    # profiles/r3a_ncon_hist.json); they are counted and reported, and a rate 30x that
-    # voids the number too.
+    # overflow that truncates work (contact pool, candidate lists, Jacobian dofs,
+    # constraint rows), voids the number.  Physics steps with more than the 32 contacts
+    # the step kernel keeps in LDS (~3.4e-6 of env-substeps on this workload,
+    # profiles/r3a_ncon_hist.json) are not truncated: the overflow tier runs them with
+    # the 256-contact pool, inside the timed region ("contact_deferred").
     nsub = env.task.config.n_sub_steps
     health = env.physics.health()
     health.pop("ncon_hist")
     env_substeps = B * args.steps * nsub
-    bad = {k: v for k, v in health.items() if k in ("diverged", "candidate_overflow", "jacobian_dof_overflow",
-                                                    "row_overflow") and v}
-    if bad or health["contact_overflow"] > 1e-4 * env_substeps:
+    bad = {k: v for k, v in health.items() if k in ("diverged", "contact_overflow", "candidate_overflow",
+                                                    "jacobian_dof_overflow", "row_overflow") and v}
+    if bad:
         refuse = refuse or f"health counters of the timed region {health}"
     # every rank learns whether any rank refuses (no rank is left waiting in a collective)
     if (comm.max(1.0 if refuse else 0.0) if comm else (1.0 if refuse else 0.0)) > 0:
         raise SystemExit(f"rank {rank}: {refuse or 'another rank refused'}; refusing to report")
     health["env_substeps"] = env_substeps
-    health["contact_overflow_rate"] = health["contact_overflow"] / env_substeps
+    health["contact_deferred_rate"] = health["contact_deferred"] / env_substeps
     if comm:
         elapsed = comm.max(elapsed)
     total_env_steps = world * B * args.steps

@@ -20,7 +20,7 @@ SENSOR_TORQUE, DIVERGED = 15, 16
 INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST, DIVERGED)
 HEALTH_WORDS, NCON_HIST = 16, 65
 HEALTH = ("contact_overflow", "candidate_overflow", "jacobian_dof_overflow", "row_overflow", "diverged",
-          "ncon_max")
+          "ncon_max", "contact_deferred")
 
 EXPORTS = (
     "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_model_lds_bytes", "dx_field_width",
@@ -37,6 +37,7 @@ EXPORTS = (
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
     "dx_env_set_time_limit", "dx_set_outputs", "dx_env_create_shard",
     "dx_health", "dx_health_clear", "dx_ncon_histogram", "dx_env_set_goal_time_limit",
+    "dx_env_step_random",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -132,6 +133,7 @@ def load(path: str = LIB_PATH):
     L.dx_env_output.argtypes = [vp, ctypes.c_int, ctypes.POINTER(vp)]
     L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
     L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]
+    L.dx_env_step_random.argtypes = [vp, ctypes.c_uint64, i32]
     L.dx_env_pack_outputs.argtypes = [vp, vp]
     L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]

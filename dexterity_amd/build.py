@@ -64,6 +64,8 @@ def _units() -> list:
     scene specialization (-DDX_SPEC_ONLY), so the kernels compile in parallel."""
     units = [(os.path.splitext(s)[0], s, ()) for s in SOURCES]
     units += [(f"dx_step_{n}", "dx_step.hip", (f"-DDX_SPEC_ONLY={n}",)) for n in _spec_names()]
+    # the overflow tier: the step kernel's physics with the DX_NCON_HI contact pool
+    units.append(("dx_step_hi", "dx_step.hip", ("-DDX_TIER_HI", "-DDX_NCON_MAX=DX_NCON_HI")))
     return units
 
 

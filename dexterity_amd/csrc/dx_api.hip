@@ -79,7 +79,8 @@ struct dx_model {
   std::map<int, std::vector<void*>> dev_allocs;
   std::map<int, DevModel> dev_models;
   std::map<int, const DevModel*> dev_model_ptrs;  // device copy of dev_models[device]
-  Lds lds;
+  Lds lds;     // the step kernel's per-env LDS layout (contact pool DX_NCON_MAX)
+  Lds lds_hi;  // the overflow tier's (DX_NCON_HI)
   int ncon_max, nefc_max;
 };
 
@@ -648,7 +649,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   //   H  Newton Hessian / Euler transpose over A          solve, euler
   // The union keeps one environment in < 20 KB for the Shadow scene, so eight
   // 64-lane workgroups (two waves per SIMD) fit in a CU's 160 KB.
-  Lds& L = m->lds;
+  auto layout = [&](int cap, Lds& L) {
   int off = 0;
   auto take = [&](int n) { int o = off; off += (n + 3) & ~3; return o; };
   auto r4 = [](int n) { return (n + 3) & ~3; };
@@ -659,7 +660,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   L.v1 = take(nv); L.v2 = take(nv); L.v3 = take(nv); L.v4 = take(nv); L.v5 = take(nv);
   L.M = take(ntri);
   L.ten_len = take(std::max(d.ntendon, 1));  // read by the tendon-limit rows: persistent
-  L.con = take(DX_NCON_MAX * DX_CON_STRIDE);
+  L.con = take((cap + DX_NCON_SPARE) * DX_CON_STRIDE);
   // limit rows: a joint / tendon whose range is wider than twice its margin can have only
   // one side within the margin at a time (q - lo < margin and hi - q < margin need
   // hi - lo < 2 margin), so it holds one row, else two
@@ -670,7 +671,7 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
     auto& tr = m->hf["tendon_range"]; auto& tm = m->hf["tendon_margin"];
     for (int t : limt) nlimrow += (tr[2 * t + 1] - tr[2 * t]) > 2.0f * tm[t] + 1e-4f ? 1 : 2;
   }
-  L.nefc_max = d.nfric + nlimrow + 4 * DX_NCON_MAX;
+  L.nefc_max = d.nfric + nlimrow + 4 * cap;
   L.efc_fl = take(std::max(d.nfric, 1)); L.efc_Rf = take(std::max(d.nfric, 1));
   L.tri = 0;  // (was the wave Cholesky's index table; n > 32 now factors on the matrix cores)
   const int U0 = off;
@@ -694,11 +695,11 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   off = std::max(B0, U0 + r4(ntri));
   L.efc_meta = take(L.nefc_max); L.efc_D = take(L.nefc_max); L.efc_aref = take(L.nefc_max);
   L.efc_jar = take(L.nefc_max);
-  L.cj_idx = take((DX_NCON_MAX * DX_DOFMAX + 3) / 4);  // uint8 dof ids
-  L.cj_val = take(DX_NCON_MAX * 3 * DX_DOFMAX);
+  L.cj_idx = take((cap * DX_DOFMAX + 3) / 4);  // uint8 dof ids
+  L.cj_val = take(cap * 3 * DX_DOFMAX);
   // contact-frame scratch: J x in jac_vec, the frame forces in jac_t_force (and the
   // sensor stash right after the last one); never live at the same time
-  L.cq = take(3 * DX_NCON_MAX);
+  L.cq = take(3 * cap);
   L.cw = L.cq;
   // The solver's J dir (efc_jv) and CG's M^-1 grad: written only from the solve on, when
   // the kinematic block is dead, so they go past the Newton Hessian when it has room
@@ -711,14 +712,20 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   end = std::max(end, off);
   L.H = U0;
   L.total = (end + 3) & ~3;  // the kernels zero it with 16-byte stores
-  m->ncon_max = DX_NCON_MAX;
-  m->nefc_max = L.nefc_max;
-  if (L.nefc_max > 5 * 64) {  // line-search register slots (dx_step.hip DX_LS_SLOTS)
-    fail(DX_ELIMIT, "constraint row capacity exceeds 320");
+  };
+  // the step kernel's layout (pool DX_NCON_MAX) and the overflow tier's (DX_NCON_HI)
+  layout(DX_NCON_MAX, m->lds);
+  layout(DX_NCON_HI, m->lds_hi);
+  m->ncon_max = DX_NCON_HI;
+  m->nefc_max = m->lds_hi.nefc_max;
+  // line-search register slots (dx_step.hip DX_LS_SLOTS: 5 in the step kernel, 20 in the
+  // overflow tier)
+  if (m->lds.nefc_max > 5 * 64 || m->lds_hi.nefc_max > 20 * 64) {
+    fail(DX_ELIMIT, "constraint row capacity exceeds the line search's register slots");
     delete m;
     return nullptr;
   }
-  if (L.total * 4 > 160 * 1024) {
+  if (m->lds.total * 4 > 160 * 1024 || m->lds_hi.total * 4 > 160 * 1024) {
     fail(DX_ELIMIT, "per-env LDS footprint exceeds 160 KiB");
     delete m;
     return nullptr;
@@ -978,23 +985,29 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
   rc |= balloc(b, (void**)&B.health, DX_HEALTH_WORDS * 4);
   rc |= balloc(b, (void**)&B.bad, E * 4);
+  rc |= balloc(b, (void**)&B.nstep, E * 4);
+  // the overflow tier's deferral list (models that can have contacts)
+  if (!d.disable_contact && d.ngpair > 0) rc |= balloc(b, (void**)&B.defer, (E + 2) * 4);
   if (!getenv("DX_NO_LPT_ORDER")) {
     void* po = nullptr;
     rc |= balloc(b, (void**)&B.cost, E * 4);
     rc |= balloc(b, &po, E * 4);
     B.order = (const int*)po;
+    rc |= balloc(b, (void**)&B.ohist, 2 * 256 * 4);
+    rc |= balloc(b, (void**)&B.okey, E * 4);
   }
   rc |= balloc(b, (void**)&b->xfrc, 6 * d.nbody * 4);
   // substep queue state (DX_NO_QUEUE=1: one workgroup per env for the whole step)
   b->queue = !getenv("DX_NO_QUEUE");
   rc |= balloc(b, (void**)&B.qhead, DX_QUEUES * DX_QHEAD_STRIDE * 4);
   rc |= balloc(b, (void**)&B.progress, E * 4);
-  rc |= balloc(b, (void**)&B.qerr, 4);
-  B.hand_stride = (d.nq + 2 * d.nv + 2 + 31) / 32 * 32;
+  rc |= balloc(b, (void**)&B.qerr, 8);  // [0] queue timeout, [1] the overflow kernel's finished workgroups
+  B.hand_stride = (d.nq + 2 * d.nv + 4 + 31) / 32 * 32;
   rc |= balloc(b, (void**)&B.hand, E * B.hand_stride * 4);
   B.epoch = 0;
   // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
+  B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
@@ -1166,11 +1179,18 @@ extern "C" int dx_set_watch(dx_batch* b, int32_t geom, int32_t body) {
 static void timing_begin(dx_batch* b, hipEvent_t* start);
 static void timing_end(dx_batch* b, hipEvent_t start);
 
+#define DX_HI_GRID 32  // workgroups of the overflow tier (each loops over the deferred steps)
 static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
   if (const char* pad = getenv("DX_LDS_PAD")) lds += (size_t)atol(pad);  // occupancy experiment
-  const bool queued = mode == 0 && b->queue && nsub < 32;
+  // (progress tags 30 and 31 are markers: dx_step.hip DX_QUEUE_NSUB)
+  const bool queued = mode == 0 && b->queue && nsub <= 29;
+  // a mode-0 step builds the next launch's longest-first order, placed by the overflow
+  // tier's launch (or, without one, by the order kernel)
+  DevBatch& Bo = b->db;
+  Bo.onext = (mode == 0 && Bo.order && Bo.defer) ? 1 : 0;
+  if (Bo.onext) Bo.opar ^= 1;
   const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots) : b->nenv;
   if (queued) {
     // substep queue: a new progress epoch and zeroed task counters
@@ -1187,37 +1207,37 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
   HIPCHK(e);
+  // the overflow tier: physics steps whose contacts did not fit the step kernel's pool
+  // (nothing to do unless some env deferred one), the next launch's longest-first order,
+  // and the queue heads zeroed for the next launch
+  if (b->db.defer && mode != 2) {
+    HIPCHK(dx_launch_step_hi(DX_HI_GRID, (size_t)b->model->lds_hi.total * 4, b->stream, b->dm_dev, b->db,
+                             b->model->lds_hi, nsub));
+    b->qhead_zero = true;
+  }
   // torque sensors from the last substep's stash (mode 0 step, mode 1 forward)
   if (b->db.sen_stash && mode != 2)
     HIPCHK(dx_launch_sensor(b->nenv, ((size_t)b->model->lds.total + 6 * DX_MAX_NV) * 4, b->stream, b->dm_dev, b->db,
                             b->model->lds, b->sensor));
-  // next launch: heaviest environments first (costs just measured)
-  // next launch: heaviest environments first (costs just measured); the same kernel
-  // zeroes the queue heads the next queued launch claims from
-  if (mode == 0 && b->db.order) {
+  // next launch: heaviest environments first (costs just measured) -- for a model without
+  // an overflow tier (contacts disabled), by the order kernel, which also zeroes the queue
+  // heads the next queued launch claims from
+  if (mode == 0 && b->db.order && !b->db.defer) {
     HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order, b->db.qhead));
     b->qhead_zero = true;
   }
   return 0;
 }
 
-// DX_DIVERGED of a physics-level call reports that call only (a dx_env's task kernel
-// consumes and clears the flags itself)
-static int clear_bad(dx_batch* b) {
-  HIPCHK(hipSetDevice(b->device));
-  HIPCHK(hipMemsetAsync(b->db.bad, 0, (size_t)b->nenv * 4, b->stream));
-  return 0;
-}
-
+// (DX_DIVERGED of a call reports that call only: the step kernel clears an env's flag in
+// its first physics-step task)
 extern "C" int dx_step(dx_batch* b, int32_t nsubstep) {
   if (!b || nsubstep < 1) return fail(DX_EINVAL, "bad batch or nsubstep");
-  if (int rc = clear_bad(b)) return rc;
   return launch_step(b, nsubstep, 0);
 }
 
 extern "C" int dx_forward(dx_batch* b) {
   if (!b) return fail(DX_EINVAL, "null batch");
-  if (int rc = clear_bad(b)) return rc;
   return launch_step(b, 1, 1);
 }
 
@@ -1411,7 +1431,7 @@ extern "C" int dx_sensor_enable(dx_batch* b, int enable) {
   DevBatch& B = b->db;
   if (enable) {
     if (!b->sen_stash) {
-      const size_t E = b->nenv, words = (size_t)b->dm.nq + 2 * b->dm.nv + 1 + 8 * DX_NCON_MAX;
+      const size_t E = b->nenv, words = (size_t)b->dm.nq + 2 * b->dm.nv + 1 + 8 * DX_NCON_HI;
       if (int rc = balloc(b, (void**)&b->sen_stash, E * words * 4)) return rc;
       if (int rc = balloc(b, (void**)&b->sensor, E * 3 * b->dm.nbody * 4)) return rc;
     }
@@ -1432,7 +1452,7 @@ extern "C" int dx_debug_enable(dx_batch* b, int enable) {
     rc |= balloc(b, (void**)&B.dbg_qacc_smooth, E * nv * 4);
     rc |= balloc(b, (void**)&B.dbg_qfrc_smooth, E * nv * 4);
     rc |= balloc(b, (void**)&B.dbg_M, E * nv * nv * 4);
-    rc |= balloc(b, (void**)&B.dbg_con, E * DX_NCON_MAX * 16 * 4);
+    rc |= balloc(b, (void**)&B.dbg_con, E * DX_NCON_HI * 16 * 4);
     rc |= balloc(b, (void**)&B.dbg_nefc, E * 2 * 4);
     if (rc) return rc;
     b->debug = true;
@@ -1473,7 +1493,7 @@ extern "C" int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nf
   if (s == "qacc_smooth") { src = B.dbg_qacc_smooth; n = E * nv; }
   else if (s == "qfrc_smooth") { src = B.dbg_qfrc_smooth; n = E * nv; }
   else if (s == "M") { src = B.dbg_M; n = E * nv * nv; }
-  else if (s == "contact") { src = B.dbg_con; n = E * DX_NCON_MAX * 16; }
+  else if (s == "contact") { src = B.dbg_con; n = E * DX_NCON_HI * 16; }
   else if (s == "efc_count") { src = B.dbg_nefc; n = E * 2; }
   else return fail(DX_EINVAL, "unknown debug field");
   if (nfloats < n) return fail(DX_EINVAL, "destination too small");
@@ -1658,9 +1678,41 @@ extern "C" void dx_env_destroy(dx_env* e) {
 extern "C" dx_batch* dx_env_batch(dx_env* e) { return e ? e->batch : nullptr; }
 extern "C" int dx_env_obs_dim(const dx_env* e) { return e ? e->P.obs_dim : fail(DX_EINVAL, "null env"); }
 
-static int env_run(dx_env* e, const float* action) {
+extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
+                                                    int step, int env0, float* out);
+
+// One control step.  Reorient runs its task logic fused into the step kernel (task_pre
+// in each env's first physics-step task, task_post in its last; dx_task.h), so a control
+// step is the step kernel plus the overflow tier's launch.  Reach keeps the task kernels
+// around its sampling pass (DX_NO_FUSE=1 selects them for reorient too).
+// random: actions drawn in the kernel by the random agent (seed, step) instead of read.
+static int env_run(dx_env* e, const float* action, bool random = false, uint64_t seed = 0, int step = 0) {
   dx_batch* b = e->batch;
   HIPCHK(hipSetDevice(b->device));
+  if (e->P.kind == DX_KIND_REORIENT && !getenv("DX_NO_FUSE") && b->db.defer) {
+    DevBatch& B = b->db;
+    const int* skip = B.skip;
+    B.fuse = 1;
+    B.skip = nullptr;
+    B.action = action;
+    B.act_random = random ? 1 : 0;
+    B.act_seed = seed;
+    B.act_step = step;
+    const int rc = launch_step(b, e->nsub, 0);
+    B.fuse = 0;
+    B.skip = skip;
+    B.action = nullptr;
+    B.act_random = 0;
+    return rc;
+  }
+  if (random) {  // the random agent into the action buffer, then the step
+    void* buf = nullptr;
+    if (int rc = dx_env_action_buffer(e, &buf)) return rc;
+    hipLaunchKernelGGL(dx_sample_actions_kernel, dim3((e->P.nenv * e->P.nu + 255) / 256), dim3(256), 0, b->stream,
+                       e->P.nenv, e->P.nu, b->dm.actuator_ctrlrange, seed, step, e->P.env0, (float*)buf);
+    HIPCHK(hipGetLastError());
+    action = (const float*)buf;
+  }
   int nb = (e->P.nenv + 63) / 64;
   hipLaunchKernelGGL(dx_task_pre_kernel, dim3(nb), dim3(64), 0, b->stream, e->P, e->S, b->db,
                      b->dm.qpos0, action);
@@ -1710,6 +1762,11 @@ extern "C" int dx_env_step(dx_env* e, const float* action) {
   return env_run(e, action);
 }
 
+extern "C" int dx_env_step_random(dx_env* e, uint64_t seed, int32_t step) {
+  if (!e) return fail(DX_EINVAL, "null env");
+  return env_run(e, nullptr, true, seed, step);
+}
+
 extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
   if (!e || !devptr) return fail(DX_EINVAL, "null argument");
   switch (which) {
@@ -1727,9 +1784,6 @@ extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {
   }
   return fail(DX_EINVAL, "unknown output");
 }
-
-extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
-                                                    int step, int env0, float* out);
 
 extern "C" int dx_env_action_buffer(dx_env* e, void** devptr) {
   if (!e || !devptr) return fail(DX_EINVAL, "null argument");

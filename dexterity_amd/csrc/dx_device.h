@@ -215,6 +215,8 @@ struct CtxT {
   int* I;  // misc ints
   unsigned long long* stage_acc;
   float4* sep = nullptr;  // this env's separating-direction cache (DX_SEP_SLOTS), or null
+  int np_wide = DX_WAVE / 8;  // narrowphase: 4-lane groups above this many candidates
+  bool defer = false;         // a full contact pool defers the physics step (I_DEFER)
   __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
       : m(m_), S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
@@ -231,6 +233,8 @@ struct CtxT<SpecRT> {
   int* I;
   unsigned long long* stage_acc;
   float4* sep = nullptr;
+  int np_wide = DX_WAVE / 8;
+  bool defer = false;
   __device__ CtxT(const DevModel& m_, const Lds& L_, float* S_, int* I_, unsigned long long* acc)
       : m(m_), L(L_),
 #define DX_X(n) n(m_.n),
@@ -272,7 +276,12 @@ __device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
 // misc int slots
 // I_OVF: capacity bits of the substep (1 candidates, 2 contacts, 4 Jacobian dofs, 8 rows);
 // I_NRAW: most contacts any collision pass of the substep found (before the DX_NCON_MAX cap)
-enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NRAW, I_NINT };
+// I_DEFER: the substep's contacts exceed this tier's pool; it is redone by the overflow tier
+enum { I_NCON = 0, I_NEFC, I_NCAND, I_NBC, I_OVF, I_NITER, I_WATCH, I_NLIM, I_NRAW, I_DEFER, I_NINT };
+// (words 10-11: the stage clock; carried between an env's physics-step tasks:)
+// I_NSTEP: physics steps since the env's last mj_resetData (the fp64 time's addition count);
+// I_FLAGS: bit 0 -- a physics step of this control step diverged and reset the env
+enum { I_NSTEP = 12, I_FLAGS = 13 };
 
 // ------------------------------------------------------------------------ //
 // position stage

@@ -8,9 +8,20 @@
 #include <stdint.h>
 
 #define DX_WAVE 64
+// Contact pool, two tiers.  The step kernel keeps DX_NCON_MAX = 32 contacts per env and
+// physics step in LDS; a physics step that finds more is not truncated but deferred, from
+// its unchanged state, to the overflow tier (dx_step.hip compiled with -DDX_TIER_HI, pool
+// DX_NCON_HI = 256, above the reference scenes' nconmax 200, shadow_hand_series_e.xml:8).
+// A pool that still overflows keeps its first contacts in candidate (generation) order.
+#define DX_NCON_HI 256
 #ifndef DX_NCON_MAX
-#define DX_NCON_MAX 32    // contacts kept per env per substep (MuJoCo pool: nconmax)
+#define DX_NCON_MAX 32    // contacts kept per env per substep by this translation unit
 #endif
+#define DX_NCON_SPARE 4   // extra record slots: the crossing candidate's contacts in a pool cut
+// contact chunks of DX_WAVE (lane = contact) the constraint / Hessian passes walk
+#define DX_NCH ((DX_NCON_MAX + DX_WAVE - 1) / DX_WAVE)
+// first step of the shuffle search over a chunk's contacts (5 steps for <= 32 contacts)
+#define DX_SEARCH0 (DX_NCON_MAX > 32 ? 32 : 16)
 #ifndef DX_CAND_MAX
 #define DX_CAND_MAX 768   // collision candidate-list words per env (dx_api.hip LDS layout)
 #endif
@@ -141,8 +152,8 @@ struct DevBatch {
   int nqueue;
   int* qerr;
   // the state an env's task hands to its next substep's task: [nenv][hand_stride]
-  // floats = qpos | qvel | warm start | time | cost so far, each record on whole
-  // 128-B lines (hand_stride a multiple of 32), so a hand-off writes back and reads
+  // floats = qpos | qvel | warm start | time | cost so far | nstep | flags, each record on
+  // whole 128-B lines (hand_stride a multiple of 32), so a hand-off writes back and reads
   // only its own lines
   float* hand;
   int hand_stride;
@@ -156,7 +167,33 @@ struct DevBatch {
   unsigned* health;
   unsigned* ncon_hist;
   int* bad;
+  int* nstep;  // [nenv] physics steps since the env's last mj_resetData (fp64 time = nstep additions of h)
+  // narrowphase group size: sixteen 4-lane groups when a substep has more than np_wide
+  // candidates, else eight 8-lane groups (DX_WAVE / 8; DX_NP_WIDE overrides it, the
+  // group-size invisibility test forces either layout)
+  int np_wide;
+  // physics steps deferred to the overflow tier (dx_step.hip dx_step_hi_kernel): [0] the
+  // count, [1] the overflow kernel's finished workgroups, [2 ..] entries env | substep
+  // << 24 | forward-only << 30, appended by the step kernel, emptied by the overflow
+  // kernel's last workgroup
+  unsigned* defer;
+  // Task logic fused into the step kernel (dx_task.h; DevBatch::tp / ts): task_pre in the
+  // env's first physics-step task, with ctrl = the action (`action`, [nenv][nu], or drawn
+  // in the kernel by the random agent when act_random: dx_urand(act_seed, env0 + env,
+  // act_step)), task_post in its last.  0: the task kernels of dx_task.hip run instead.
+  int fuse;
+  const float* action;
+  int act_random, act_step;
+  uint64_t act_seed;
+  // Longest-first dispatch order for the next launch, built without a kernel of its own:
+  // an env's last task of a launch that sets onext counts its cost bucket in
+  // ohist[opar][256] (descending cost) and keeps its rank in okey[env] (bucket << 16 |
+  // rank); the overflow tier's launch then places every env at its bucket's prefix +
+  // rank in `order` and its last workgroup zeroes ohist[opar] and the queue heads.
+  unsigned *ohist, *okey;
+  int opar, onext;
 };
+#define DX_DEFER_FWD (1u << 30)
 #define DX_HEALTH_WORDS 16
 #define DX_NCON_HIST 65   // bins 0..63, and >= 64
 #define DX_MAXVAL 1e10f   // mjMAXVAL: |qacc| beyond this is a diverged state (mj_checkAcc)
@@ -327,6 +364,9 @@ int dx_step_occupancy(int spec, size_t lds);
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);
 hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, int* order, unsigned* qhead);
+// the overflow tier (dx_step.hip, DX_TIER_HI): the physics steps deferred by the last launch
+hipError_t dx_launch_step_hi(int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
+                             const Lds& L, int nsub);
 
 // dx_sensor.hip: joint torque sensors from the step kernel's stash (host side)
 hipError_t dx_launch_sensor(int nenv, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,

@@ -17,8 +17,8 @@
 #include "dx_device.h"
 
 // Stash layout per env (floats): qpos [nq] | qvel [nv] | qacc [nv] | ncon (int bits) |
-// DX_NCON_MAX x {b1, b2 (int bits), pos[3], force[3] (world, acting on b2)}.
-__host__ __device__ inline int dx_sensor_stash_words(int nq, int nv) { return nq + 2 * nv + 1 + 8 * DX_NCON_MAX; }
+// DX_NCON_HI x {b1, b2 (int bits), pos[3], force[3] (world, acting on b2)}.
+__host__ __device__ inline int dx_sensor_stash_words(int nq, int nv) { return nq + 2 * nv + 1 + 8 * DX_NCON_HI; }
 
 extern "C" __global__ void __launch_bounds__(64) dx_sensor_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L,
                                                                   float* out) {

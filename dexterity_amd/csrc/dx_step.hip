@@ -18,6 +18,7 @@
 // are listed in oracle/dx_oracle.c (the fp64 CPU oracle these kernels are
 // parity-tested against) and DESIGN.md §3.
 #include "dx_device.h"
+#include "dx_task.h"
 
 // 16-byte write-through (sc1) store into a per-env block whose base is wave-uniform:
 // the substep queue hands these bytes to the env's next task without a release fence
@@ -538,8 +539,17 @@ struct MprState {
   int phase, it;
 };
 // cached: a separating direction of this pair from an earlier collision pass (world
-// frame), tried first (phase -1): if the supports along it do not reach the origin the
-// pair is separated -- the verdict MPR's own tests give -- in one support pass.
+// frame), tried first (phase -1).  The cache may only save work, never change a result:
+// its entries are stored plainly and shared by two pairs per slot, so which entry a task
+// sees depends on the narrowphase layout and on which XCD ran the env's last substep.
+// The cached test therefore returns "separated" only when the Minkowski difference lies
+// at least DX_SEP_CLEAR beyond the origin along the cached direction: every point MPR
+// can put into a portal is a point of A - B, so MPR's own verdict is then "separated"
+// too, unless fp32 rounding in its portal tests exceeded DX_SEP_CLEAR (coordinates
+// ~0.3 m: ~1e-7).  Anything closer falls through to MPR from its standard start, with
+// the very direction an uncached pair starts from (kept in the P1 slot, unused until
+// phase 0 writes it) -- so the pair's arithmetic is then exactly the uncached one.
+#define DX_SEP_CLEAR 1e-5f
 template <int NPG>
 __device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const float* cached) {
   MPoint P0;
@@ -557,6 +567,7 @@ __device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const floa
   S.phase = 0;
   S.it = 0;
   if (cached) {
+    S.P[9] = S.dir[0]; S.P[10] = S.dir[1]; S.P[11] = S.dir[2];  // the uncached start
     S.dir[0] = cached[0]; S.dir[1] = cached[1]; S.dir[2] = cached[2];
     S.phase = -1;
   }
@@ -588,7 +599,9 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
   const bool stop =
       fminf(dt - dot3(v1, dir), fminf(dt - dot3(v2, dir), dt - dot3(v3, dir))) <= tol || S.it > maxit;
   // exits: separated (phases -1..3) and converged penetration (phase 4)
-  if ((ph <= 1 && behind) || (ph == 2 && (S.it > 1000 || behind)) || (ph == 3 && (stop || dt < 0))) return 1;
+  if ((ph == -1 && dt < -DX_SEP_CLEAR) || (ph >= 0 && ph <= 1 && behind) || (ph == 2 && (S.it > 1000 || behind)) ||
+      (ph == 3 && (stop || dt < 0)))
+    return 1;
   if (ph == 4 && stop) {
     float cl[3];
     float d2 = tri_origin_dist2(v1, v2, v3, cl);
@@ -636,7 +649,6 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
   sub3(eb, b, cc);
   float X[3];
   cross3(X, ea, eb);
-  if (ph == -1) { X[0] = -v0[0]; X[1] = -v0[1]; X[2] = -v0[2]; }
   if (ph == 0 && fzero(dot3(X, X))) {  // p on the line through the origin and v0
     dir[0] = X[0]; dir[1] = X[1]; dir[2] = X[2];
     if (fzero(p.v[0]) && fzero(p.v[1]) && fzero(p.v[2])) {
@@ -651,6 +663,7 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
     return 2;
   }
   normalize3(X);
+  if (ph == -1) { X[0] = v1[0]; X[1] = v1[1]; X[2] = v1[2]; }  // not clear: MPR's own start (mpr_init)
   // phase 1: orient the portal so that the origin is on dir's side (swap P1, P2)
   const bool swap = ph == 1 && dot3(X, v0) > 0;
   if (swap) {
@@ -899,7 +912,8 @@ __device__ __forceinline__ int narrowphase_prim(const Ctx& c, int gp, NpOut& o, 
 // their key (candidate, rank); collision() puts them into candidate order, which gives
 // the list of the serial loop.  Returns the contact count (before the DX_NCON_MAX cap).
 template <int NPG, class Ctx>
-__device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcand, const float4* gcrec, float* con) {
+__device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcand, const float4* gcrec, float* con,
+                                           int* cntq) {
   int ncon = 0;
   NpStats st = {0, 0, 0, 0, 0, 0, 0};
   {
@@ -948,11 +962,12 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
           int r = mpr_step<NPG>(G, M, depth, nrm, pos, st);
           if (r && c.sep && SL == 0) {
             // remember a separating direction (unless it is the cached one, still
-            // separating: phase -1); forget it once the pair touches.  Plain stores: the
-            // entry only picks the first direction MPR tries, never its verdict, so a
-            // task on another XCD that reads an older entry (its L2 has not seen this
-            // one) computes the same contacts; written through (DX_SEP_WT) every 16-B
-            // entry cost a partial-line HBM write and the next task's read a miss.
+            // separating: phase -1); forget it once the pair touches.  Plain stores: an
+            // entry decides a verdict only where MPR's own verdict is the same (mpr_init,
+            // DX_SEP_CLEAR), so a task on another XCD that reads an older entry (its L2
+            // has not seen this one), or a layout that gives the slot to the other pair
+            // sharing it, computes the same contacts; written through (DX_SEP_WT) every
+            // 16-B entry cost a partial-line HBM write and the next task's read a miss.
             const bool keep = r == 1 && M.phase != -1;
             if (keep || cached) {
               const float4 ent = keep ? make_float4(M.dir[0], M.dir[1], M.dir[2], __int_as_float(gp + 1))
@@ -978,7 +993,7 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
         const int cinc = wave_incl_scan(SL == 0 ? cnt : 0);
         const int pre = __shfl(cinc, GBASE, 64) - cnt;
         int slot = ncon + pre + o.rank;
-        if (o.wr && slot < DX_NCON_MAX) {
+        if (o.wr && slot < DX_NCON_MAX + DX_NCON_SPARE) {
           write_contact(con, slot, o.pos, o.n, o.dist, gp);
           con[DX_CON_STRIDE * slot + 14] = __int_as_float(4 * q + o.rank);  // sort key
         }
@@ -988,6 +1003,7 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
       // order), so a long MPR on one group no longer holds back the others' queues;
       // the contact keys still sort the list into candidate order below
       const uint64_t fin = __ballot(done && SL == 0);
+      if (done && SL == 0) cntq[q] = cnt;  // contacts of candidate q (the pool cut, collision())
       if (done) {
         q = next + __popcll(fin & ((1ull << GBASE) - 1ull));
         fresh = true;
@@ -1206,26 +1222,83 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
   // when the substep has more than eight candidates -- the contact-rich states whose
   // serial chains of pairs per group bound the heaviest environments' substeps
   float* con = c.f(c.L.con);
-  const int ncon_raw = ng > DX_WAVE / 8 ? narrow_pass<4>(c, ng, gcand, gcrec, con) : narrow_pass<8>(c, ng, gcand, gcrec, con);
+  int* cntq = cand;  // the body-pair list is dead now: contacts per narrowphase candidate
+  const int ncon_raw = ng > c.np_wide ? narrow_pass<4>(c, ng, gcand, gcrec, con, cntq)
+                                      : narrow_pass<8>(c, ng, gcand, gcrec, con, cntq);
   int ncon = ncon_raw;
   SYNC();
-  // candidate order: lane k ranks record k by its key, then moves it
-  {
-    int nk = min(ncon, DX_NCON_MAX);
-    int key = LANE < nk ? __float_as_int(con[DX_CON_STRIDE * LANE + 14]) : 0x7fffffff;
-    int rank = 0;
-    for (int j = 0; j < nk; j++) rank += __builtin_amdgcn_readlane(key, j) < key;
-    float rec[14];
+  if (ncon_raw > DX_NCON_MAX && !watch_only) {
+    if (c.defer) {
+      // the step kernel's pool is full: this physics step runs in the overflow tier
+      // (dx_step_hi, DX_NCON_HI contacts) from the unchanged state (env_substep)
+      if (LANE == 0) { I[I_DEFER] = 1; I[I_NRAW] = max(I[I_NRAW], ncon_raw); }
+      SYNC();
+      return;
+    }
+    // The pool keeps the first DX_NCON_MAX contacts in candidate (generation) order, as
+    // MuJoCo fills its contact buffer: the records above were kept in completion order,
+    // so the candidates up to the one whose contacts cross the cap run again with every
+    // contact kept (DX_NCON_SPARE extra record slots hold the crossing candidate's), and
+    // the sort and the cap below drop the rest.  (The verdicts and contacts of a rerun
+    // pair are the first run's: the separating-direction cache never decides one.)
+    int v[4], sum = 0;
 #pragma unroll
-    for (int e = 0; e < 14; e++) rec[e] = LANE < nk ? con[DX_CON_STRIDE * LANE + e] : 0.f;
+    for (int k = 0; k < 4; k++) {  // ng <= 256 candidates: four per lane
+      const int q = 4 * LANE + k;
+      v[k] = q < ng ? cntq[q] : 0;
+      sum += v[k];
+    }
+    const int ex = wave_incl_scan(sum) - sum;
+    int qcut = 1 << 30, run = ex;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      run += v[k];
+      qcut = (run > DX_NCON_MAX && qcut == (1 << 30)) ? 4 * LANE + k : qcut;
+    }
+    qcut = wave_min_i(qcut);
     SYNC();
-    if (LANE < nk) {
+    ncon = qcut + 1 > c.np_wide ? narrow_pass<4>(c, qcut + 1, gcand, gcrec, con, cntq)
+                                : narrow_pass<8>(c, qcut + 1, gcand, gcrec, con, cntq);
+    SYNC();
+  }
+  // candidate order: lane k ranks record k (and k + 64, ...) by its key, then moves it
+  {
+    constexpr int NS = (DX_NCON_MAX + DX_NCON_SPARE + DX_WAVE - 1) / DX_WAVE;
+    const int nk = min(ncon, DX_NCON_MAX + DX_NCON_SPARE);
+    int key[NS], rank[NS];
+    float rec[NS][14];
 #pragma unroll
-      for (int e = 0; e < 14; e++) con[DX_CON_STRIDE * rank + e] = rec[e];
+    for (int k = 0; k < NS; k++) {
+      const int i = LANE + DX_WAVE * k;
+      key[k] = i < nk ? __float_as_int(con[DX_CON_STRIDE * i + 14]) : 0x7fffffff;
+      rank[k] = 0;
+    }
+#pragma unroll
+    for (int cc = 0; cc < NS; cc++) {
+      const int nj = min(nk - DX_WAVE * cc, DX_WAVE);
+      for (int j = 0; j < nj; j++) {
+        const int kj = __builtin_amdgcn_readlane(key[cc], j);
+#pragma unroll
+        for (int k = 0; k < NS; k++) rank[k] += kj < key[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      const int i = LANE + DX_WAVE * k;
+#pragma unroll
+      for (int e = 0; e < 14; e++) rec[k][e] = i < nk ? con[DX_CON_STRIDE * i + e] : 0.f;
+    }
+    SYNC();
+#pragma unroll
+    for (int k = 0; k < NS; k++) {
+      if (LANE + DX_WAVE * k < nk) {
+#pragma unroll
+        for (int e = 0; e < 14; e++) con[DX_CON_STRIDE * rank[k] + e] = rec[k][e];
+      }
     }
   }
   stage_mark(c, ST_NP_MPR);
-  if (LANE == 0 && !watch_only) I[I_NRAW] = max(I[I_NRAW], ncon);
+  if (LANE == 0 && !watch_only) I[I_NRAW] = max(I[I_NRAW], ncon_raw);
   if (ncon > DX_NCON_MAX) {
     if (LANE == 0) I[I_OVF] |= 2;
     ncon = DX_NCON_MAX;
@@ -1291,19 +1364,20 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   // instead of a chain of them per section after each barrier.
   // level 1
   const int ncon = I[I_NCON];
-  const bool fok = LANE < nfric, lok = LANE < c.nlimj, cok = LANE < ncon;
+  const bool fok = LANE < nfric, lok = LANE < c.nlimj;
+  bool cok = LANE < ncon;
   const int fd = fok ? m.fric_dof[LANE] : 0;
   const int lj = lok ? m.limj_jnt[LANE] : 0;
   // (contact tables only for lanes holding a contact: a scene without contact pairs
   // has empty gpair tables)
-  const int cgp = cok ? __float_as_int(con[DX_CON_STRIDE * LANE + 13]) : 0;
-  const int cg1 = cok ? m.gpair_geom[2 * cgp] : 0, cg2 = cok ? m.gpair_geom[2 * cgp + 1] : 0;
-  const int ccd = cok ? m.gpair_condim[cgp] : 1;
-  const float cfr0 = cok ? m.gpair_friction[5 * cgp] : 0.f, cfr1 = cok ? m.gpair_friction[5 * cgp + 1] : 0.f;
-  const float csr[2] = {cok ? m.gpair_solref[2 * cgp] : 0.f, cok ? m.gpair_solref[2 * cgp + 1] : 0.f};
+  int cgp = cok ? __float_as_int(con[DX_CON_STRIDE * LANE + 13]) : 0;
+  int cg1 = cok ? m.gpair_geom[2 * cgp] : 0, cg2 = cok ? m.gpair_geom[2 * cgp + 1] : 0;
+  int ccd = cok ? m.gpair_condim[cgp] : 1;
+  float cfr0 = cok ? m.gpair_friction[5 * cgp] : 0.f, cfr1 = cok ? m.gpair_friction[5 * cgp + 1] : 0.f;
+  float csr[2] = {cok ? m.gpair_solref[2 * cgp] : 0.f, cok ? m.gpair_solref[2 * cgp + 1] : 0.f};
   float csi[5];
   for (int e = 0; e < 5; e++) csi[e] = cok ? m.gpair_solimp[5 * cgp + e] : 0.f;
-  const float cmg = cok ? m.gpair_margin[cgp] : 0.f;
+  float cmg = cok ? m.gpair_margin[cgp] : 0.f;
   // level 2
   const float ffl = m.dof_frictionloss[fd], fiw = m.dof_invweight0[fd];
   const float fsr[2] = {m.dof_solref[2 * fd], m.dof_solref[2 * fd + 1]};
@@ -1314,12 +1388,12 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
   const float lsr[2] = {m.jnt_solref[2 * lj], m.jnt_solref[2 * lj + 1]};
   float lsi[5];
   for (int e = 0; e < 5; e++) lsi[e] = m.jnt_solimp[5 * lj + e];
-  const int cb1 = cok ? m.geom_bodyid[cg1] : 0, cb2 = cok ? m.geom_bodyid[cg2] : 0;
+  int cb1 = cok ? m.geom_bodyid[cg1] : 0, cb2 = cok ? m.geom_bodyid[cg2] : 0;
   // level 3
   const float liw = m.dof_invweight0[ldof];
-  const uint64_t cc1 = m.body_chain[cb1], cc2 = m.body_chain[cb2];
-  const float ctran = m.body_invweight0[2 * cb1] + m.body_invweight0[2 * cb2];
-  const int cr1 = m.body_rootidx[cb1], cr2 = m.body_rootidx[cb2];
+  uint64_t cc1 = m.body_chain[cb1], cc2 = m.body_chain[cb2];
+  float ctran = m.body_invweight0[2 * cb1] + m.body_invweight0[2 * cb2];
+  int cr1 = m.body_rootidx[cb1], cr2 = m.body_rootidx[cb2];
   // 1. dof friction rows: fixed positions [0, nfric)
   for (int k = LANE; k < nfric; k += DX_WAVE) {
     const bool own = k == LANE;
@@ -1404,152 +1478,166 @@ __device__ __forceinline__ void make_constraint(const Ctx& c) {
     nrow += tot;
   }
   SYNC();
-  // 4. contacts: sparse frame jacobian, then pyramid rows.  Lane = contact (ncon <=
-  // DX_NCON_MAX <= 64) for the support masks and record fields; then the Jacobian entries
-  // flattened over (contact, support dof) items -- every item one lane, no serial walk
-  // over a contact's dofs -- and the frame velocities J qvel as jac_vec's gather.
-  static_assert(DX_NCON_MAX <= DX_WAVE, "one lane per contact");
+  // 4. contacts: sparse frame jacobian, then pyramid rows, in chunks of DX_WAVE contacts
+  // (one chunk for DX_NCON_MAX <= 64 -- the step kernel; the overflow tier's larger pool
+  // takes several).  Lane = contact of the chunk for the support masks and record fields
+  // (chunk 0's tables were loaded above); then the Jacobian entries flattened over
+  // (contact, support dof) items -- every item one lane, no serial walk over a contact's
+  // dofs -- and the frame velocities J qvel as jac_vec's gather.
   float* cdof = c.f(c.L.cdof);
   float* rcom = c.f(c.L.rcom);
   unsigned char* cj_idx = (unsigned char*)c.f(c.L.cj_idx);
   float* cj_val = c.f(c.L.cj_val);
   float* cq = c.f(c.L.cq);
-  int nnz = 0;
-  const uint64_t sp = cok ? cc1 ^ cc2 : 0ull;
-  if (cok) {
-    float* r = con + DX_CON_STRIDE * LANE;
-    const int np = __popcll(sp);
-    nnz = min(np, DX_DOFMAX);
-    if (np > DX_DOFMAX) I[I_OVF] |= 4;
-    r[14] = __int_as_float(nnz | ((ccd == 1 ? 1 : 4) << 8));
-    r[16] = cfr0;
-    r[17] = cfr1;
-    r[18] = __int_as_float((int)(uint32_t)sp);
-    r[19] = __int_as_float((int)(uint32_t)(sp >> 32));
-  }
-  {
-    const int incl = wave_incl_scan(nnz);
-    const int excl = incl - nnz;
-    const int total = __builtin_amdgcn_readlane(incl, 63);
-    const unsigned splo = (unsigned)sp, sphi = (unsigned)(sp >> 32);
-    const unsigned c1lo = (unsigned)cc1, c1hi = (unsigned)(cc1 >> 32);
-    const unsigned c2lo = (unsigned)cc2, c2hi = (unsigned)(cc2 >> 32);
-    for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
-      const int t = min(base + LANE, total - 1);
-      int ci = 0;  // last contact whose first item is <= t
-#pragma unroll
-      for (int st = 16; st >= 1; st >>= 1) {
-        const int mid = ci + st;
-        const int em = __shfl(excl, mid & 63, 64);
-        if (mid < ncon && em <= t) ci = mid;
-      }
-      int q = t - __shfl(excl, ci, 64);
-      const int slot = q;
-      // the q-th set bit of the contact's support mask: 32-bit half, then halving
-      // windows by popcount
-      const unsigned lo = (unsigned)__shfl((int)splo, ci, 64), hi = (unsigned)__shfl((int)sphi, ci, 64);
-      const int plo = __popc(lo);
-      unsigned w = q < plo ? lo : hi;
-      int d = q < plo ? 0 : 32;
-      q = q < plo ? q : q - plo;
-#pragma unroll
-      for (int h = 16; h >= 1; h >>= 1) {
-        const unsigned low = w & ((1u << h) - 1u);
-        const int pc = __popc(low);
-        const bool up = q >= pc;
-        q = up ? q - pc : q;
-        w = up ? (w >> h) : low;
-        d += up ? h : 0;
-      }
-      // (every shuffle unconditional: a shuffle under a divergent select would read
-      // inactive source lanes)
-      const unsigned a1l = (unsigned)__shfl((int)c1lo, ci, 64), a1h = (unsigned)__shfl((int)c1hi, ci, 64);
-      const unsigned a2l = (unsigned)__shfl((int)c2lo, ci, 64), a2h = (unsigned)__shfl((int)c2hi, ci, 64);
-      const int t1 = __shfl(cr1, ci, 64), t2 = __shfl(cr2, ci, 64);
-      const unsigned b1 = d < 32 ? a1l >> d : a1h >> (d - 32);
-      const unsigned b2 = d < 32 ? a2l >> d : a2h >> (d - 32);
-      const int rt = (b1 & 1u) ? t1 : t2;
-      const float sgn = (b2 & 1u) ? 1.f : -1.f;
-      const float* r = con + DX_CON_STRIDE * ci;
-      const float* rc = rcom + 3 * rt;
-      const float* cd = cdof + 6 * d;
-      const float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
-      float tq[3];
-      cross3(tq, cd, off);
-      const float jp[3] = {cd[3] + tq[0], cd[4] + tq[1], cd[5] + tq[2]};
-      if (base + LANE < total) {
-        cj_idx[ci * DX_DOFMAX + slot] = (unsigned char)d;
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-          cj_val[(ci * 3 + k) * DX_DOFMAX + slot] = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
-      }
+  constexpr int NCH = DX_NCH;
+#pragma unroll 1
+  for (int ch = 0; ch < NCH; ch++) {
+    const int cb = ch * DX_WAVE;
+    if (cb >= ncon) break;  // uniform
+    const int nc = min(ncon - cb, DX_WAVE);  // contacts in this chunk
+    if (ch > 0) {  // (overflow tier only) this chunk's tables
+      const int ci = cb + LANE;
+      cok = ci < ncon;
+      cgp = cok ? __float_as_int(con[DX_CON_STRIDE * ci + 13]) : 0;
+      cg1 = cok ? m.gpair_geom[2 * cgp] : 0;
+      cg2 = cok ? m.gpair_geom[2 * cgp + 1] : 0;
+      ccd = cok ? m.gpair_condim[cgp] : 1;
+      cfr0 = cok ? m.gpair_friction[5 * cgp] : 0.f;
+      cfr1 = cok ? m.gpair_friction[5 * cgp + 1] : 0.f;
+      csr[0] = cok ? m.gpair_solref[2 * cgp] : 0.f;
+      csr[1] = cok ? m.gpair_solref[2 * cgp + 1] : 0.f;
+      for (int e = 0; e < 5; e++) csi[e] = cok ? m.gpair_solimp[5 * cgp + e] : 0.f;
+      cmg = cok ? m.gpair_margin[cgp] : 0.f;
+      cb1 = cok ? m.geom_bodyid[cg1] : 0;
+      cb2 = cok ? m.geom_bodyid[cg2] : 0;
+      cc1 = m.body_chain[cb1];
+      cc2 = m.body_chain[cb2];
+      ctran = m.body_invweight0[2 * cb1] + m.body_invweight0[2 * cb2];
+      cr1 = m.body_rootidx[cb1];
+      cr2 = m.body_rootidx[cb2];
     }
-  }
-  SYNC();
-  // frame velocities (J qvel), lane = (contact, frame axis)
-  for (int t = LANE; t < 3 * ncon; t += DX_WAVE) {
-    const int ci = t / 3, k = t - 3 * ci;
-    const int nz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
-    float v = 0;
+    int nnz = 0;
+    const uint64_t sp = cok ? cc1 ^ cc2 : 0ull;
+    if (cok) {
+      float* r = con + DX_CON_STRIDE * (cb + LANE);
+      const int np = __popcll(sp);
+      nnz = min(np, DX_DOFMAX);
+      if (np > DX_DOFMAX) I[I_OVF] |= 4;
+      r[14] = __int_as_float(nnz | ((ccd == 1 ? 1 : 4) << 8));
+      r[16] = cfr0;
+      r[17] = cfr1;
+      r[18] = __int_as_float((int)(uint32_t)sp);
+      r[19] = __int_as_float((int)(uint32_t)(sp >> 32));
+    }
+    {
+      const int incl = wave_incl_scan(nnz);
+      const int excl = incl - nnz;
+      const int total = __builtin_amdgcn_readlane(incl, 63);
+      const unsigned splo = (unsigned)sp, sphi = (unsigned)(sp >> 32);
+      const unsigned c1lo = (unsigned)cc1, c1hi = (unsigned)(cc1 >> 32);
+      const unsigned c2lo = (unsigned)cc2, c2hi = (unsigned)(cc2 >> 32);
+      for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+        const int t = min(base + LANE, total - 1);
+        int ci = 0;  // last contact (of the chunk) whose first item is <= t
 #pragma unroll
-    for (int q = 0; q < DX_DOFMAX; q++) {  // unguarded loads; slots past nnz are not summed
-      const float jv = cj_val[(ci * 3 + k) * DX_DOFMAX + q];
-      const float xv = qvel[cj_idx[ci * DX_DOFMAX + q]];
-      const float tt = v + jv * xv;
-      v = q < nz ? tt : v;
-    }
-    cq[t] = v;
-  }
-  SYNC();
-  for (int base = 0; base < ncon; base += DX_WAVE) {
-    int ci = base + LANE;
-    int nr = 0;
-    int gp = 0;
-    float* r = nullptr;
-    if (ci < ncon) {
-      r = con + DX_CON_STRIDE * ci;
-      gp = __float_as_int(r[13]);
-      nr = __float_as_int(r[14]) >> 8;
-    }
-    int inc = wave_incl_scan(nr);
-    int off = inc - nr;
-    int tot = __builtin_amdgcn_readlane(inc, 63);
-    if (nr) {
-      const bool own = base == 0;  // first pass: the preloaded tables
-      float tran, mg, fr[2], sr[2], si[5];
-      if (own) {
-        tran = ctran; mg = cmg; fr[0] = cfr0; fr[1] = cfr1;
-        sr[0] = csr[0]; sr[1] = csr[1];
-        for (int e = 0; e < 5; e++) si[e] = csi[e];
-      } else {
-        int g1 = m.gpair_geom[2 * gp], g2 = m.gpair_geom[2 * gp + 1];
-        int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
-        tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
-        mg = m.gpair_margin[gp];
-        fr[0] = m.gpair_friction[5 * gp]; fr[1] = m.gpair_friction[5 * gp + 1];
-        sr[0] = m.gpair_solref[2 * gp]; sr[1] = m.gpair_solref[2 * gp + 1];
-        for (int e = 0; e < 5; e++) si[e] = m.gpair_solimp[5 * gp + e];
-      }
-      r[15] = __int_as_float(nrow + off);
-      if (nr == 1) {
-        int row = nrow + off;
-        if (row < c.L.nefc_max) {
-          meta[row] = DXR_CONFL | (ci << 8);
-          row_params(c, row, r[12], mg, 0, tran, sr, si, cq[3 * ci], 1.0f, false);
+        for (int st = DX_SEARCH0; st >= 1; st >>= 1) {
+          const int mid = ci + st;
+          const int em = __shfl(excl, mid & 63, 64);
+          if (mid < nc && em <= t) ci = mid;
         }
-      } else {
-        float rs = 2 * fr[0] * fr[0] / m.impratio;
-        for (int e = 0; e < 4; e++) {
-          int row = nrow + off + e;
-          if (row >= c.L.nefc_max) break;
-          int k = 1 + (e >> 1);
-          float mu = fr[k - 1] * ((e & 1) ? -1.f : 1.f);
-          meta[row] = DXR_CON | (e << 4) | (ci << 8);
-          row_params(c, row, r[12], mg, 0, tran, sr, si, cq[3 * ci] + mu * cq[3 * ci + k], rs, false);
+        int q = t - __shfl(excl, ci, 64);
+        const int slot = q;
+        // the q-th set bit of the contact's support mask: 32-bit half, then halving
+        // windows by popcount
+        const unsigned lo = (unsigned)__shfl((int)splo, ci, 64), hi = (unsigned)__shfl((int)sphi, ci, 64);
+        const int plo = __popc(lo);
+        unsigned w = q < plo ? lo : hi;
+        int d = q < plo ? 0 : 32;
+        q = q < plo ? q : q - plo;
+#pragma unroll
+        for (int h = 16; h >= 1; h >>= 1) {
+          const unsigned low = w & ((1u << h) - 1u);
+          const int pc = __popc(low);
+          const bool up = q >= pc;
+          q = up ? q - pc : q;
+          w = up ? (w >> h) : low;
+          d += up ? h : 0;
+        }
+        // (every shuffle unconditional: a shuffle under a divergent select would read
+        // inactive source lanes)
+        const unsigned a1l = (unsigned)__shfl((int)c1lo, ci, 64), a1h = (unsigned)__shfl((int)c1hi, ci, 64);
+        const unsigned a2l = (unsigned)__shfl((int)c2lo, ci, 64), a2h = (unsigned)__shfl((int)c2hi, ci, 64);
+        const int t1 = __shfl(cr1, ci, 64), t2 = __shfl(cr2, ci, 64);
+        const unsigned b1 = d < 32 ? a1l >> d : a1h >> (d - 32);
+        const unsigned b2 = d < 32 ? a2l >> d : a2h >> (d - 32);
+        const int rt = (b1 & 1u) ? t1 : t2;
+        const float sgn = (b2 & 1u) ? 1.f : -1.f;
+        const int cg = cb + ci;
+        const float* r = con + DX_CON_STRIDE * cg;
+        const float* rc = rcom + 3 * rt;
+        const float* cd = cdof + 6 * d;
+        const float off[3] = {r[0] - rc[0], r[1] - rc[1], r[2] - rc[2]};
+        float tq[3];
+        cross3(tq, cd, off);
+        const float jp[3] = {cd[3] + tq[0], cd[4] + tq[1], cd[5] + tq[2]};
+        if (base + LANE < total) {
+          cj_idx[cg * DX_DOFMAX + slot] = (unsigned char)d;
+#pragma unroll
+          for (int k = 0; k < 3; k++)
+            cj_val[(cg * 3 + k) * DX_DOFMAX + slot] = sgn * (r[3 + 3 * k] * jp[0] + r[4 + 3 * k] * jp[1] + r[5 + 3 * k] * jp[2]);
         }
       }
     }
-    nrow += tot;
+    SYNC();
+    // frame velocities (J qvel), lane = (contact, frame axis)
+    for (int t = 3 * cb + LANE; t < 3 * (cb + nc); t += DX_WAVE) {
+      const int ci = t / 3, k = t - 3 * ci;
+      const int nz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
+      float v = 0;
+#pragma unroll
+      for (int q = 0; q < DX_DOFMAX; q++) {  // unguarded loads; slots past nnz are not summed
+        const float jv = cj_val[(ci * 3 + k) * DX_DOFMAX + q];
+        const float xv = qvel[cj_idx[ci * DX_DOFMAX + q]];
+        const float tt = v + jv * xv;
+        v = q < nz ? tt : v;
+      }
+      cq[t] = v;
+    }
+    SYNC();
+    // pyramid rows, lane = contact of the chunk (its tables loaded above)
+    {
+      const int ci = cb + LANE;
+      int nr = 0;
+      float* r = nullptr;
+      if (LANE < nc) {
+        r = con + DX_CON_STRIDE * ci;
+        nr = __float_as_int(r[14]) >> 8;
+      }
+      int inc = wave_incl_scan(nr);
+      int off = inc - nr;
+      int tot = __builtin_amdgcn_readlane(inc, 63);
+      if (nr) {
+        r[15] = __int_as_float(nrow + off);
+        if (nr == 1) {
+          int row = nrow + off;
+          if (row < c.L.nefc_max) {
+            meta[row] = DXR_CONFL | (ci << 8);
+            row_params(c, row, r[12], cmg, 0, ctran, csr, csi, cq[3 * ci], 1.0f, false);
+          }
+        } else {
+          float rs = 2 * cfr0 * cfr0 / m.impratio;
+          for (int e = 0; e < 4; e++) {
+            int row = nrow + off + e;
+            if (row >= c.L.nefc_max) break;
+            int k = 1 + (e >> 1);
+            float mu = (k == 1 ? cfr0 : cfr1) * ((e & 1) ? -1.f : 1.f);
+            meta[row] = DXR_CON | (e << 4) | (ci << 8);
+            row_params(c, row, r[12], cmg, 0, ctran, csr, csi, cq[3 * ci] + mu * cq[3 * ci + k], rs, false);
+          }
+        }
+      }
+      nrow += tot;
+    }
   }
   if (nrow > c.L.nefc_max) {
     if (LANE == 0) I[I_OVF] |= 8;
@@ -2004,57 +2092,64 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   const float* con = c.f(c.L.con);
   const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
-  float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w22 = 0.f;
-  int nnz = 0, items = 0;
-  if (LANE < ncon) {
-    const float* r = con + DX_CON_STRIDE * LANE;
-    const int row0 = __float_as_int(r[15]);
-    nnz = __float_as_int(r[14]) & 255;
-    if ((__float_as_int(r[14]) >> 8) == 1) {
-      if (row0 < nefc) {
-        float f, hw;
-        row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
-        w00 = hw;
+#pragma unroll 1
+  for (int ch = 0; ch < DX_NCH; ch++) {  // contact chunks (lane = contact)
+    const int cb = ch * DX_WAVE;
+    if (cb >= ncon) break;  // uniform
+    const int nc = min(ncon - cb, DX_WAVE);
+    float w00 = 0.f, w01 = 0.f, w02 = 0.f, w11 = 0.f, w22 = 0.f;
+    int nnz = 0, items = 0;
+    if (LANE < nc) {
+      const float* r = con + DX_CON_STRIDE * (cb + LANE);
+      const int row0 = __float_as_int(r[15]);
+      nnz = __float_as_int(r[14]) & 255;
+      if ((__float_as_int(r[14]) >> 8) == 1) {
+        if (row0 < nefc) {
+          float f, hw;
+          row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+          w00 = hw;
+        }
+      } else {
+        for (int e = 0; e < 4; e++) {
+          const int row = row0 + e;
+          if (row >= nefc) break;
+          float f, hw;
+          row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+          const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
+          w00 += hw;
+          if (e < 2) { w01 += hw * mu; w11 += hw * mu * mu; }
+          else { w02 += hw * mu; w22 += hw * mu * mu; }
+        }
       }
-    } else {
-      for (int e = 0; e < 4; e++) {
-        const int row = row0 + e;
-        if (row >= nefc) break;
-        float f, hw;
-        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
-        const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
-        w00 += hw;
-        if (e < 2) { w01 += hw * mu; w11 += hw * mu * mu; }
-        else { w02 += hw * mu; w22 += hw * mu * mu; }
-      }
+      items = (w00 == 0.f && w11 == 0.f && w22 == 0.f) ? 0 : nnz * (nnz + 1) / 2;
     }
-    items = (w00 == 0.f && w11 == 0.f && w22 == 0.f) ? 0 : nnz * (nnz + 1) / 2;
-  }
-  const int incl = wave_incl_scan(items);
-  const int excl = incl - items;
-  const int total = __builtin_amdgcn_readlane(incl, 63);
-  for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
-    const int t = min(base + LANE, total - 1);
-    int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
+    const int incl = wave_incl_scan(items);
+    const int excl = incl - items;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+      const int t = min(base + LANE, total - 1);
+      int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
 #pragma unroll
-    for (int st = 16; st >= 1; st >>= 1) {
-      const int mid = ci + st;
-      const int em = __shfl(excl, mid & 63, 64);
-      if (mid < ncon && em <= t) ci = mid;
+      for (int st = DX_SEARCH0; st >= 1; st >>= 1) {
+        const int mid = ci + st;
+        const int em = __shfl(excl, mid & 63, 64);
+        if (mid < nc && em <= t) ci = mid;
+      }
+      const int u = t - __shfl(excl, ci, 64);
+      int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+      a += (a + 1) * (a + 2) / 2 <= u;
+      a -= a * (a + 1) / 2 > u;
+      const int b = u - a * (a + 1) / 2;
+      const float c00 = __shfl(w00, ci, 64), c01 = __shfl(w01, ci, 64), c02 = __shfl(w02, ci, 64);
+      const float c11 = __shfl(w11, ci, 64), c22 = __shfl(w22, ci, 64);
+      const int cg = cb + ci;
+      const float* jv = cj_val + cg * 3 * DX_DOFMAX;
+      const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
+      const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
+      const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
+                        c22 * a2 * b2;
+      if (base + LANE < total) atomicAdd(H + ti(cj_idx[cg * DX_DOFMAX + a]) + cj_idx[cg * DX_DOFMAX + b], sum);
     }
-    const int u = t - __shfl(excl, ci, 64);
-    int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
-    a += (a + 1) * (a + 2) / 2 <= u;
-    a -= a * (a + 1) / 2 > u;
-    const int b = u - a * (a + 1) / 2;
-    const float c00 = __shfl(w00, ci, 64), c01 = __shfl(w01, ci, 64), c02 = __shfl(w02, ci, 64);
-    const float c11 = __shfl(w11, ci, 64), c22 = __shfl(w22, ci, 64);
-    const float* jv = cj_val + ci * 3 * DX_DOFMAX;
-    const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
-    const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
-    const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
-                      c22 * a2 * b2;
-    if (base + LANE < total) atomicAdd(H + ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b], sum);
   }
   SYNC();
 }
@@ -2068,7 +2163,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
 // joint limits) is rebuilt every iteration into a register, the sweep's diagonal
 // addition for column LANE % 32.  Returns that addition.
 template <class Ctx>
-__device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, float (&wo)[5]) {
+__device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, float (&wo)[DX_NCH][5]) {
   const DevModel& m = c.mdl();
   const int nv = c.nv;
   const int nefc = c.I[I_NEFC];
@@ -2103,66 +2198,74 @@ __device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, flo
   const float* con = c.f(c.L.con);
   const unsigned char* cj_idx = (const unsigned char*)c.f(c.L.cj_idx);
   const float* cj_val = c.f(c.L.cj_val);
-  float w[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // w00, w01, w02, w11, w22
-  int nnz = 0;
-  if (LANE < ncon) {
-    const float* r = con + DX_CON_STRIDE * LANE;
-    const int row0 = __float_as_int(r[15]);
-    nnz = __float_as_int(r[14]) & 255;
-    if ((__float_as_int(r[14]) >> 8) == 1) {
-      if (row0 < nefc) {
-        float f, hw;
-        row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
-        w[0] = hw;
-      }
-    } else {
-      for (int e = 0; e < 4; e++) {
-        const int row = row0 + e;
-        if (row >= nefc) break;
-        float f, hw;
-        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
-        const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
-        w[0] += hw;
-        if (e < 2) { w[1] += hw * mu; w[3] += hw * mu * mu; }
-        else { w[2] += hw * mu; w[4] += hw * mu * mu; }
+  constexpr int NCH = DX_NCH;  // contact chunks (lane = contact)
+#pragma unroll
+  for (int ch = 0; ch < NCH; ch++) {
+    const int cb = ch * DX_WAVE;
+    if (cb >= ncon) break;  // uniform
+    const int nc = min(ncon - cb, DX_WAVE);
+    float w[5] = {0.f, 0.f, 0.f, 0.f, 0.f};  // w00, w01, w02, w11, w22
+    int nnz = 0;
+    if (LANE < nc) {
+      const float* r = con + DX_CON_STRIDE * (cb + LANE);
+      const int row0 = __float_as_int(r[15]);
+      nnz = __float_as_int(r[14]) & 255;
+      if ((__float_as_int(r[14]) >> 8) == 1) {
+        if (row0 < nefc) {
+          float f, hw;
+          row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+          w[0] = hw;
+        }
+      } else {
+        for (int e = 0; e < 4; e++) {
+          const int row = row0 + e;
+          if (row >= nefc) break;
+          float f, hw;
+          row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+          const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
+          w[0] += hw;
+          if (e < 2) { w[1] += hw * mu; w[3] += hw * mu * mu; }
+          else { w[2] += hw * mu; w[4] += hw * mu * mu; }
+        }
       }
     }
-  }
-  float dw[5];
-  bool ch = false;
+    float dw[5];
+    bool chg = false;
 #pragma unroll
-  for (int k = 0; k < 5; k++) {
-    dw[k] = w[k] - wo[k];
-    ch |= w[k] != wo[k];
-    wo[k] = w[k];
-  }
-  const int items = ch ? nnz * (nnz + 1) / 2 : 0;
-  const int incl = wave_incl_scan(items);
-  const int excl = incl - items;
-  const int total = __builtin_amdgcn_readlane(incl, 63);
-  if (first) SYNC();  // the M copy before the atomics
-  for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
-    const int t = min(base + LANE, total - 1);
-    int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
-#pragma unroll
-    for (int st = 16; st >= 1; st >>= 1) {
-      const int mid = ci + st;
-      const int em = __shfl(excl, mid & 63, 64);
-      if (mid < ncon && em <= t) ci = mid;
+    for (int k = 0; k < 5; k++) {
+      dw[k] = w[k] - wo[ch][k];
+      chg |= w[k] != wo[ch][k];
+      wo[ch][k] = w[k];
     }
-    const int u = t - __shfl(excl, ci, 64);
-    int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
-    a += (a + 1) * (a + 2) / 2 <= u;
-    a -= a * (a + 1) / 2 > u;
-    const int b = u - a * (a + 1) / 2;
-    const float c00 = __shfl(dw[0], ci, 64), c01 = __shfl(dw[1], ci, 64), c02 = __shfl(dw[2], ci, 64);
-    const float c11 = __shfl(dw[3], ci, 64), c22 = __shfl(dw[4], ci, 64);
-    const float* jv = cj_val + ci * 3 * DX_DOFMAX;
-    const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
-    const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
-    const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
-                      c22 * a2 * b2;
-    if (base + LANE < total) atomicAdd(H + ti(cj_idx[ci * DX_DOFMAX + a]) + cj_idx[ci * DX_DOFMAX + b], sum);
+    const int items = chg ? nnz * (nnz + 1) / 2 : 0;
+    const int incl = wave_incl_scan(items);
+    const int excl = incl - items;
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (first && ch == 0) SYNC();  // the M copy before the atomics
+    for (int base = 0; base < total; base += DX_WAVE) {  // uniform trip count: the shuffles see every lane
+      const int t = min(base + LANE, total - 1);
+      int ci = 0;  // last contact whose first item is <= t (contacts without items tie and lose)
+#pragma unroll
+      for (int st = DX_SEARCH0; st >= 1; st >>= 1) {
+        const int mid = ci + st;
+        const int em = __shfl(excl, mid & 63, 64);
+        if (mid < nc && em <= t) ci = mid;
+      }
+      const int u = t - __shfl(excl, ci, 64);
+      int a = (int)((sqrtf(8.0f * (float)u + 1.0f) - 1.0f) * 0.5f);
+      a += (a + 1) * (a + 2) / 2 <= u;
+      a -= a * (a + 1) / 2 > u;
+      const int b = u - a * (a + 1) / 2;
+      const float c00 = __shfl(dw[0], ci, 64), c01 = __shfl(dw[1], ci, 64), c02 = __shfl(dw[2], ci, 64);
+      const float c11 = __shfl(dw[3], ci, 64), c22 = __shfl(dw[4], ci, 64);
+      const int cg = cb + ci;
+      const float* jv = cj_val + cg * 3 * DX_DOFMAX;
+      const float a0 = jv[a], a1 = jv[DX_DOFMAX + a], a2 = jv[2 * DX_DOFMAX + a];
+      const float b0 = jv[b], b1 = jv[DX_DOFMAX + b], b2 = jv[2 * DX_DOFMAX + b];
+      const float sum = c00 * a0 * b0 + c01 * (a0 * b1 + a1 * b0) + c02 * (a0 * b2 + a2 * b0) + c11 * a1 * b1 +
+                        c22 * a2 * b2;
+      if (base + LANE < total) atomicAdd(H + ti(cj_idx[cg * DX_DOFMAX + a]) + cj_idx[cg * DX_DOFMAX + b], sum);
+    }
   }
   SYNC();
   return s;
@@ -2177,7 +2280,9 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // Exact line search along dir (1-D Newton with bracketing on the piecewise-quadratic
 // cost).  Every row's (type, D, friction, jar, J dir) is loaded into registers once
 // -- lane-owned rows r = LANE + 64 k -- so the iterations touch no LDS.
-#define DX_LS_SLOTS 5  // nefc_max <= 320 (checked at model load)
+#ifndef DX_LS_SLOTS
+#define DX_LS_SLOTS (DX_NCON_MAX > 64 ? 20 : 5)  // nefc_max <= 320 / 1280 (checked at model load)
+#endif
 // NEWTON (dir = -H^-1 grad): the slope at alpha = 0 is grad . dir and the curvature there
 // dir^T H dir = -grad . dir (H is the Hessian of the zone set at alpha = 0), so the first
 // 1-D Newton step from 0 lands at alpha = 1 -- the search starts there, with g0 = grad . dir
@@ -2435,7 +2540,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     return;
   }
   const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
-  float wo[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float wo[DX_NCH][5] = {};
   for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
     jac_t_force(c, grad);  // grad <- J^T f
@@ -2535,6 +2640,7 @@ __device__ __forceinline__ void forward(const Ctx& c, const float* xfrc) {
   m_solve(c, M, DiagAdd{0.f, 0.f}, a0, H);
   stage_mark(c, ST_SMOOTH);
   collision(c, 0, -1, -1);
+  if (c.I[I_DEFER]) return;  // the pool is full: the overflow tier redoes this physics step
   make_constraint(c);
   stage_mark(c, ST_CON);
   solve(c);
@@ -2592,7 +2698,10 @@ __device__ __forceinline__ void euler(const Ctx& c, float* time) {
       qpos[qa] += h * qvel[da];
     }
   }
-  if (LANE == 0) *time += h;
+  if (LANE == 0) {
+    *time += h;
+    c.I[I_NSTEP] += 1;
+  }
   SYNC();
   stage_mark(c, ST_EULER);
 }
@@ -2881,6 +2990,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
         if (need & 2) {
           for (int i = LANE; i < c.nv; i += DX_WAVE) { c.f(c.L.qvel)[i] = 0.f; ws[i] = 0.f; }
           time = 0.f;
+          if (LANE == 0) c.I[I_NSTEP] = 0;
           SYNC();
         }
       }
@@ -2907,6 +3017,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       }
       SYNC();
       const float t0 = time;
+      const int n0 = c.I[I_NSTEP];
       for (int s = 0; s < 2; s++) {  // JointStaticIsolator: two physics steps
         forward(c, B.xfrc);
         for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
@@ -2920,6 +3031,8 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       if (T.goal_qpos && LANE < nq) T.goal_qpos[(size_t)env * nq + LANE] = qpos[LANE];
       if (!contact_now(c)) { ok = true; break; }
       time = t0;
+      SYNC();
+      if (LANE == 0) c.I[I_NSTEP] = n0;
     }
     if (LANE < 3 * P.ntips) T.goal[(size_t)env * P.goal_dim + LANE] = gc;
     if (LANE == 0) {
@@ -2930,7 +3043,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       T.exceeded[env] = 0;
       T.registered[env] = 0;
       T.solve_start[env] = time;
-      T.solve_n[env] = (int)rintf(time / c.mdl().timestep);  // fp64 start: dx_task_post_kernel
+      T.solve_n[env] = c.I[I_NSTEP];  // the fp64 start (task_post): the goal's physics step
     }
     if (LANE < nq) qpos[LANE] = q_init;
     if (LANE < nu) ctrl[LANE] = c_init;
@@ -2967,7 +3080,8 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
 // rec: the env's hand-off record (substeps after the first of a queued step), or null
 // for the batch arrays.
 template <class Ctx>
-__device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env, const float* rec = nullptr) {
+__device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env, const float* rec = nullptr,
+                                           bool resume = false) {
   const Lds& L = c.L;
   float* smem = c.S;
   // Zero the whole per-env LDS block: the Cholesky solve reads a few words past its
@@ -2992,6 +3106,10 @@ __device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env, c
       ws[i] = rec[c.nq + c.nv + i];
     }
     time = rec[c.nq + 2 * c.nv];
+    if (LANE == 0) {
+      I[I_NSTEP] = __float_as_int(rec[c.nq + 2 * c.nv + 2]);
+      I[I_FLAGS] = __float_as_int(rec[c.nq + 2 * c.nv + 3]);
+    }
   } else {
     for (int i = LANE; i < c.nq; i += DX_WAVE) qpos[i] = B.qpos[(size_t)env * c.nq + i];
     for (int i = LANE; i < c.nv; i += DX_WAVE) {
@@ -2999,6 +3117,12 @@ __device__ __forceinline__ float env_begin(Ctx& c, const DevBatch& B, int env, c
       ws[i] = B.qacc_ws[(size_t)env * c.nv + i];
     }
     time = B.time[env];
+    if (LANE == 0) {
+      I[I_NSTEP] = B.nstep ? B.nstep[env] : 0;
+      // (the overflow tier resuming a deferred control step: its earlier physics steps'
+      // divergence flag, which health_check stored write-through)
+      I[I_FLAGS] = resume && B.bad ? (B.bad[env] & 1) : 0;
+    }
   }
   for (int i = LANE; i < c.nu; i += DX_WAVE) ctrl[i] = B.ctrl[(size_t)env * c.nu + i];
   if (LANE < I_NINT) I[LANE] = 0;
@@ -3016,7 +3140,10 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
     B.qvel[(size_t)env * c.nv + i] = qvel[i];
     B.qacc_ws[(size_t)env * c.nv + i] = ws[i];
   }
-  if (LANE == 0) B.time[env] = time;
+  if (LANE == 0) {
+    B.time[env] = time;
+    if (B.nstep) B.nstep[env] = c.I[I_NSTEP];
+  }
 }
 
 // The hand-off record (DevBatch::hand) of a task whose env has substeps left: lane t
@@ -3026,17 +3153,18 @@ __device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int str
   const float* qpos = c.f(c.L.qpos);
   const float* qvel = c.f(c.L.qvel);
   const float* ws = c.f(c.L.v5);
-  const int nw = c.nq + 2 * c.nv + 2;
+  const int nw = c.nq + 2 * c.nv + 4;
   time = rl(time, 0);  // euler advances time in lane 0 only
+  const int nstep = c.I[I_NSTEP], flags = c.I[I_FLAGS];
   for (int t = LANE; 4 * t < nw; t += DX_WAVE) {
     float w[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int m = 4 * t + u;
+      const int m = 4 * t + u, k = m - (c.nq + 2 * c.nv);
       w[u] = m < c.nq ? qpos[m]
            : m < c.nq + c.nv ? qvel[m - c.nq]
            : m < c.nq + 2 * c.nv ? ws[m - c.nq - c.nv]
-           : m == c.nq + 2 * c.nv ? time : __uint_as_float(cost);
+           : k == 0 ? time : k == 1 ? __uint_as_float(cost) : k == 2 ? __int_as_float(nstep) : __int_as_float(flags);
     }
     st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
   }
@@ -3050,7 +3178,7 @@ template <class Ctx>
 __device__ __forceinline__ void sensor_stash(const Ctx& c, const DevBatch& B, int env) {
   const DevModel& m = c.mdl();
   const int nq = c.nq, nv = c.nv;
-  float* o = B.sen_stash + (size_t)env * (nq + 2 * nv + 1 + 8 * DX_NCON_MAX);
+  float* o = B.sen_stash + (size_t)env * (nq + 2 * nv + 1 + 8 * DX_NCON_HI);
   for (int i = LANE; i < nq; i += DX_WAVE) o[i] = c.f(c.L.qpos)[i];
   for (int i = LANE; i < nv; i += DX_WAVE) {
     o[nq + i] = c.f(c.L.qvel)[i];
@@ -3079,7 +3207,7 @@ __device__ __forceinline__ void sensor_stash(const Ctx& c, const DevBatch& B, in
 // start, ctrl and time), the env is flagged (B.bad, which the task turns into dm_control's
 // divergent-physics step: LAST, reward 0, discount 0) and counted.
 template <class Ctx>
-__device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, int env, float& time) {
+__device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, int env, float& time, bool reset = true) {
   const DevModel& m = c.mdl();
   int* I = c.I;
   const int ovf = I[I_OVF], nraw = I[I_NRAW];
@@ -3096,12 +3224,14 @@ __device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, in
     if (ovf & 4) atomicAdd(B.health + 2, 1u);
     if (ovf & 8) atomicAdd(B.health + 3, 1u);
     if (bad) atomicAdd(B.health + 4, 1u);
-    if (nraw > DX_NCON_MAX / 2) atomicMax(B.health + 5, (unsigned)nraw);
+    if (nraw > 16) atomicMax(B.health + 5, (unsigned)nraw);
     if (B.ncon_hist) atomicAdd(B.ncon_hist + min(nraw, DX_NCON_HIST - 1), 1u);
   }
   SYNC();
   if (LANE == 0) { I[I_OVF] = 0; I[I_NRAW] = 0; }
-  if (bad) {
+  if (bad && !reset) {  // mj_forward: flagged and counted ([3P] mj_checkAcc runs in mj_step only)
+    if (LANE == 0 && B.bad && env >= 0) TaskStore<true>::st(B.bad, env, 1);
+  } else if (bad) {
     float* q = c.f(c.L.qpos);
     for (int i = LANE; i < c.nq; i += DX_WAVE) q[i] = m.qpos0[i];
     for (int i = LANE; i < c.nv; i += DX_WAVE) {
@@ -3111,10 +3241,15 @@ __device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, in
     }
     for (int i = LANE; i < c.nu; i += DX_WAVE) {
       c.f(c.L.ctrl)[i] = 0.f;
-      if (env >= 0) B.ctrl[(size_t)env * c.nu + i] = 0.f;  // later substeps (queued tasks) reload it
+      // later substeps (queued tasks, maybe on another XCD) reload it: write-through
+      if (env >= 0) TaskStore<true>::st(B.ctrl, (size_t)env * c.nu + i, 0.f);
     }
     time = 0.f;
-    if (LANE == 0 && B.bad && env >= 0) B.bad[env] = 1;
+    if (LANE == 0) {
+      c.I[I_NSTEP] = 0;
+      c.I[I_FLAGS] |= 1;
+      if (B.bad && env >= 0) TaskStore<true>::st(B.bad, env, 1);  // (read after the launch)
+    }
   }
   SYNC();
 }
@@ -3123,6 +3258,7 @@ __device__ __forceinline__ void health_check(const Ctx& c, const DevBatch& B, in
 template <class Ctx>
 __device__ __forceinline__ void env_substep(const Ctx& c, const DevBatch& B, float& time, int env, bool last) {
   forward(c, B.xfrc);
+  if (c.I[I_DEFER]) return;  // (the state in LDS is still the one this physics step started from)
   if (last && B.sen_stash) sensor_stash(c, B, env);
   float* ws = c.f(c.L.v5);
   for (int i = LANE; i < c.nv; i += DX_WAVE) ws[i] = c.f(c.L.qacc)[i];
@@ -3148,7 +3284,7 @@ __device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int 
       B.dbg_M[(size_t)env * c.nv * c.nv + k] = c.f(L.M)[i >= j ? ti(i) + j : ti(j) + i];
     }
     int n = I[I_NCON];
-    for (int k = LANE; k < DX_NCON_MAX * 16; k += DX_WAVE) {
+    for (int k = LANE; k < DX_NCON_HI * 16; k += DX_WAVE) {
       int ci = k / 16, e = k % 16;
       float v = 0;
       if (ci < n) {
@@ -3159,7 +3295,7 @@ __device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int 
           v = e == 13 ? (float)m.gpair_geom[2 * gp] : e == 14 ? (float)m.gpair_geom[2 * gp + 1] : (float)m.gpair_condim[gp];
         }
       }
-      B.dbg_con[(size_t)env * DX_NCON_MAX * 16 + k] = v;
+      B.dbg_con[(size_t)env * DX_NCON_HI * 16 + k] = v;
     }
     if (LANE == 0) { B.dbg_nefc[2 * env] = I[I_NEFC]; B.dbg_nefc[2 * env + 1] = I[I_OVF]; }
   }
@@ -3176,6 +3312,72 @@ __device__ __forceinline__ void env_finish(const Ctx& c, const DevBatch& B, int 
   env_store_state(c, B, env, time);
 }
 
+// The next launch's longest-first order (DevBatch::ohist / okey): the env's cost bucket
+// (descending cost) counted, its rank within the bucket kept.  Called once per env and
+// launch, when its control step ends (or goes to the overflow tier: the top bucket).
+__device__ __forceinline__ void order_key(const DevBatch& B, int env, unsigned cost) {
+  if (B.onext && LANE == 0) {
+    const unsigned b = 255u - min(cost >> 4, 255u);
+    const unsigned r = atomicAdd(B.ohist + 256 * B.opar + b, 1u);
+    B.okey[env] = b << 16 | r;
+  }
+}
+
+// A physics step whose contacts overflow the step kernel's pool (I_DEFER) is handed,
+// from the state it started from, to the overflow tier: the state goes to the batch
+// arrays, the env to the deferral list (substep s; forward-only for a dx_forward), its
+// cost to the top bucket of the next launch's longest-first order, and the count of
+// deferrals to the health counters.  Nothing of the env is written after this.
+template <class Ctx>
+__device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int env, int s, bool fwd, float time) {
+  env_store_state(c, B, env, rl(time, 0));
+  if (LANE == 0) {
+    const unsigned k = atomicAdd(B.defer, 1u);
+    B.defer[2 + k] = (unsigned)env | ((unsigned)s << 24) | (fwd ? DX_DEFER_FWD : 0u);
+    if (B.cost) B.cost[env] = 0xffffffffu;
+    if (B.health) {
+      atomicAdd(B.health + 6, 1u);
+      atomicMax(B.health + 5, (unsigned)c.I[I_NRAW]);
+    }
+  }
+  if (!fwd) order_key(B, env, 0xffffffffu);
+}
+
+// Fused task_pre (DevBatch::fuse) in the env's first physics-step task: before_step /
+// initialize_episode by lane 0, then ctrl = the action (zero after a reset), every lane,
+// write-through -- the env's later tasks may run on other XCDs.  Returns 1 when the env
+// was (re)initialised (FIRST: observed only).  The workgroup fence makes lane 0's batch
+// stores (a reset's state) visible to the env_begin that follows.
+template <class Ctx>
+__device__ __forceinline__ int fused_pre(const Ctx& c, const DevBatch& B, int env) {
+  const TaskParams& P = *(const TaskParams*)(const DXG TaskParams*)B.tp;
+  const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
+  int skip = 0;
+  if (LANE == 0) skip = task_pre<true>(P, S, B, c.mdl().qpos0, env);
+  skip = __shfl(skip, 0, 64);
+  for (int i = LANE; i < c.nu; i += DX_WAVE) {
+    const size_t k = (size_t)env * c.nu + i;
+    const float a = skip ? 0.f
+                  : B.act_random ? random_action(c.mdl().actuator_ctrlrange, B.act_seed, P.env0 + env, B.act_step, i)
+                  : B.action ? B.action[k] : B.ctrl[k];
+    TaskStore<true>::st(B.ctrl, k, a);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return skip;
+}
+
+// Fused task_post in the env's last task, after env_finish wrote its outputs: after_step,
+// reward, discount, termination and the observation (dx_task.h).
+template <class Ctx>
+__device__ __forceinline__ void fused_post(const Ctx& c, const DevBatch& B, int env, bool skip) {
+  const TaskParams& P = *(const TaskParams*)(const DXG TaskParams*)B.tp;
+  const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  task_post(P, S, B, env, LANE, skip, (c.I[I_FLAGS] & 1) != 0, c.I[I_NSTEP]);
+}
+
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
 // mode 2: reach sampling pass (goal rollouts / joint sampling), state out only
 template <class SP>
@@ -3190,26 +3392,42 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   CtxT<SP> c(m, Lrt, smem, nullptr, B.stage_acc ? B.stage_acc + (size_t)env * DX_NSTAGE : nullptr);
   c.I = (int*)(smem + c.L.ints);
   c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
-  float time = env_begin(c, B, env);
+  c.np_wide = B.np_wide;
+  c.defer = !prep && B.defer;  // (the reach sampling pass keeps its pool and cuts it)
   if (prep) {  // reach sampling pass (mode 2): new state only, no outputs
+    float time = env_begin(c, B, env);
     reach_prep(c, B, env, time);
     env_store_state(c, B, env, time);
     return;
   }
-  int steps = mode == 0 ? nsub : 1;
-  if (B.skip && B.skip[env]) steps = 0;  // freshly reset by the task: observation pass only
+  // DX_DIVERGED reports this call: cleared here, set by health_check (both write-through)
+  if (LANE == 0 && B.bad) TaskStore<true>::st(B.bad, env, 0);
+  const bool fuse = B.fuse && mode == 0;
+  int skip = fuse ? fused_pre(c, B, env) : (B.skip && B.skip[env]);
+  float time = env_begin(c, B, env);
+  const int steps = skip ? 0 : mode == 0 ? nsub : 1;  // a freshly reset env is only observed
   for (int s = 0; s < steps; s++) {
     if (mode == 0) {
       env_substep(c, B, time, env, s == steps - 1);
     } else {
       forward(c, B.xfrc);
-      if (B.sen_stash) sensor_stash(c, B, env);
-      health_check(c, B, env, time);
+      if (!c.I[I_DEFER]) {
+        if (B.sen_stash) sensor_stash(c, B, env);
+        health_check(c, B, env, time, false);
+      }
+    }
+    if (c.I[I_DEFER]) {
+      env_defer(c, B, env, s, mode != 0, time);
+      return;
     }
   }
   env_finish(c, B, env, time);
-  if (LANE == 0 && B.cost && mode == 0)
-    B.cost[env] = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+  if (mode == 0) {
+    const unsigned cost = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+    if (LANE == 0 && B.cost) B.cost[env] = cost;
+    if (fuse) fused_post(c, B, env, skip);
+    order_key(B, env, cost);
+  }
 }
 
 // Substep queue (mode 0): one task = one physics step of one environment, claimed in
@@ -3230,14 +3448,21 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
 // bounded anyway (B.qerr records a timeout).  Hand-off (MI355X guide, Guideline 16
 // R1): the producer stores the handed-off bytes write-through (sc1), drains vmcnt and
 // stores the progress tag relaxed at agent scope (sc1); the consumer polls relaxed,
-// then one agent acquire + vmcnt(0) before its plain loads.
+// then one agent acquire + vmcnt(0) before its plain loads.  With the task logic fused
+// (DevBatch::fuse), the env's first task runs task_pre (its writes that later tasks read
+// are write-through too) and its last task_post.
 __device__ __forceinline__ unsigned qtag(unsigned epoch, int s) { return epoch * 32u + (unsigned)s; }
+#define DX_TAG_DEFER 31  // progress tag of an env whose control step went to the overflow tier
+#define DX_TAG_DONE 30   // ... whose control step ended in its first task (a fresh reset: observed only)
+#define DX_QUEUE_NSUB 29 // longest control step the queue takes (tags 30, 31 are markers)
 
 template <class SP>
 __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B, const Lds& Lrt, int nsub) {
   extern __shared__ float smem[];
   CtxT<SP> c(m, Lrt, smem, nullptr, nullptr);
   c.I = (int*)(smem + c.L.ints);
+  c.np_wide = B.np_wide;
+  c.defer = B.defer != nullptr;
   const int nqueue = B.nqueue;
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -3261,7 +3486,13 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       int abort = 0;
       if (LANE == 0) {
         unsigned n = 0;
-        while (__hip_atomic_load(B.progress + env, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != qtag(B.epoch, s)) {
+        for (;;) {
+          const unsigned tag = __hip_atomic_load(B.progress + env, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (tag == qtag(B.epoch, s)) break;
+          // an earlier physics step of the env went to the overflow tier, which runs the
+          // rest of its control step, or the control step ended in its first task:
+          // nothing to do here
+          if (tag == qtag(B.epoch, DX_TAG_DEFER) || tag == qtag(B.epoch, DX_TAG_DONE)) { abort = 2; break; }
           __builtin_amdgcn_s_sleep(2);
           // ~seconds without progress (never expected), or another task gave up: the
           // launch is aborted -- no task computes on a state whose predecessor has
@@ -3277,7 +3508,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
           }
         }
       }
-      if (__builtin_amdgcn_readfirstlane(abort)) continue;  // drain: later claims end the loop
+      if (__builtin_amdgcn_readfirstlane(abort)) continue;  // drain (or deferred / done): later claims end the loop
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -3287,15 +3518,29 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     float* rec = B.hand + (size_t)env * B.hand_stride;
     // cost so far (shader cycles / 1024), carried in the record between substeps
     const unsigned cost0 = s > 0 ? __float_as_uint(rec[c.nq + 2 * c.nv + 1]) : 0u;
+    int skip = 0;
+    if (s == 0) {
+      // DX_DIVERGED reports this call: cleared here, set by health_check (write-through)
+      if (LANE == 0 && B.bad) TaskStore<true>::st(B.bad, env, 0);
+      skip = B.fuse ? fused_pre(c, B, env) : (B.skip && B.skip[env]);
+    }
     float time = env_begin(c, B, env, s > 0 ? rec : nullptr);
-    if (!(B.skip && B.skip[env])) env_substep(c, B, time, env, s == nsub - 1);  // a freshly reset env is only observed
-    if (s == nsub - 1) {
+    if (!skip && !(s > 0 && !B.fuse && B.skip && B.skip[env])) env_substep(c, B, time, env, s == nsub - 1);
+    if (c.I[I_DEFER]) {
+      env_defer(c, B, env, s, false, time);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (LANE == 0) __hip_atomic_store(B.progress + env, qtag(B.epoch, DX_TAG_DEFER), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    const bool last = s == nsub - 1 || (skip && B.fuse);  // (a fresh reset is observed right away)
+    const unsigned cost = cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+    if (last) {
       env_finish(c, B, env, time);
-      if (LANE == 0 && B.cost)
-        B.cost[env] = cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+      if (LANE == 0 && B.cost) B.cost[env] = cost;
+      if (B.fuse) fused_post(c, B, env, skip);
+      order_key(B, env, cost);
     } else {
-      env_store_hand(c, rec, B.hand_stride, time,
-                     cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull));
+      env_store_hand(c, rec, B.hand_stride, time, cost);
     }
     // publish: the bytes the env's next task must read (the hand-off record) were
     // stored write-through (sc1), so a drained vmcnt suffices and no release fence (a
@@ -3308,7 +3553,9 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    if (LANE == 0) __hip_atomic_store(B.progress + env, qtag(B.epoch, s + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (LANE == 0)
+      __hip_atomic_store(B.progress + env, qtag(B.epoch, last && s < nsub - 1 ? DX_TAG_DONE : s + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -3319,7 +3566,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
 // (that translation unit holds only that scene's kernel and its launcher), and once
 // without it (generic kernel, dispatch, helper kernels), so the kernels compile in
 // parallel.
-#if __has_include("dx_specs.inc")
+#if __has_include("dx_specs.inc") && !defined(DX_TIER_HI)
 #include "dx_specs.inc"
 #endif
 #ifndef DX_SPECS
@@ -3360,7 +3607,94 @@ static bool spec_matches(const DevModel& d, const Lds& L) {
   hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
                             const Lds& L, int nsub, int mode);
 
-#ifdef DX_SPEC_ONLY
+#if defined(DX_TIER_HI)
+// ------------------------------------------------------------------------ //
+// overflow tier (build.py compiles this file once more with -DDX_TIER_HI
+// -DDX_NCON_MAX=DX_NCON_HI): the physics steps the step kernel deferred (env_defer),
+// each run by one workgroup with the DX_NCON_HI pool, from the state it was deferred at
+// to the end of the env's control step (or its forward pass), with the step kernel's
+// outputs.  Launched behind every step-kernel launch; it exits at once when nothing was
+// deferred, which is nearly always (profiles/r3a_ncon_hist.json: 3.4e-6 of env-substeps).
+// ------------------------------------------------------------------------ //
+static_assert(DX_NCON_MAX == DX_NCON_HI, "the overflow tier is compiled with the DX_NCON_HI pool");
+// The same launch also places every env of the next launch's longest-first order
+// (DevBatch::ohist / okey, written by the step kernel: order_key) -- each workgroup a
+// slice of the envs, from the bucket prefix it computes itself -- and its last workgroup
+// zeroes that histogram and the substep-queue heads for the next step-kernel launch.
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1)))
+dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) {
+  extern __shared__ float smem[];
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  // 1. the order: bucket prefix (four buckets per lane), then this workgroup's envs
+  if (B.onext && B.order) {
+    const unsigned* h = B.ohist + 256 * B.opar;
+    unsigned hv[4], sum = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) { hv[k] = h[4 * LANE + k]; sum += hv[k]; }
+    const unsigned ex = (unsigned)wave_incl_scan((int)sum) - sum;
+    unsigned pre[4];
+    pre[0] = ex; pre[1] = ex + hv[0]; pre[2] = pre[1] + hv[1]; pre[3] = pre[2] + hv[2];
+    const int per = (B.nenv + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int e0 = (int)blockIdx.x * per, e1 = min(B.nenv, e0 + per);
+    for (int base = e0; base < e1; base += DX_WAVE) {  // uniform trip count (the shuffles)
+      const int e = base + LANE;
+      const unsigned key = e < e1 ? B.okey[e] : 0u;
+      const int b = (int)(key >> 16);
+      const unsigned p0 = __shfl(pre[0], b >> 2, 64), p1 = __shfl(pre[1], b >> 2, 64);
+      const unsigned p2 = __shfl(pre[2], b >> 2, 64), p3 = __shfl(pre[3], b >> 2, 64);
+      const unsigned p = (b & 3) == 0 ? p0 : (b & 3) == 1 ? p1 : (b & 3) == 2 ? p2 : p3;
+      if (e < e1) ((int*)B.order)[p + (key & 0xffffu)] = e;
+    }
+  }
+  // 2. the deferred physics steps
+  const unsigned n = B.defer ? B.defer[0] : 0u;
+  for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
+    const unsigned e = B.defer[2 + i];
+    const int env = (int)(e & 0xffffffu), s0 = (int)((e >> 24) & 63u);
+    CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
+    c.I = (int*)(smem + c.L.ints);
+    c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
+    c.np_wide = B.np_wide;
+    float time = env_begin(c, B, env, nullptr, true);
+    if (e & DX_DEFER_FWD) {
+      forward(c, B.xfrc);
+      if (B.sen_stash) sensor_stash(c, B, env);
+      health_check(c, B, env, time, false);
+      env_finish(c, B, env, time);
+    } else {
+      for (int s = s0; s < nsub; s++) env_substep(c, B, time, env, s == nsub - 1);
+      env_finish(c, B, env, time);
+      if (B.fuse) fused_post(c, B, env, false);
+    }
+  }
+  // 3. the last workgroup to finish resets the launch-to-launch state
+  unsigned last = 0;
+  if (LANE == 0) {
+    __threadfence();
+    last = atomicAdd((unsigned*)B.qerr + 1, 1u) == gridDim.x - 1;
+  }
+  if (__shfl(last, 0, 64)) {
+    __threadfence();
+    if (B.defer && LANE < 2) B.defer[LANE] = 0u;          // the deferral list
+    if (B.onext)                                           // this launch's cost histogram
+#pragma unroll
+      for (int k = 0; k < 4; k++) B.ohist[256 * B.opar + 4 * LANE + k] = 0u;
+    if (LANE < DX_QUEUES) B.qhead[LANE * DX_QHEAD_STRIDE] = 0u;  // the queue heads
+    if (LANE == 0) B.qerr[1] = 0u;
+  }
+}
+
+hipError_t dx_launch_step_hi(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B,
+                             const Lds& L, int nsub) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)dx_step_hi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(dx_step_hi_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub);
+  return hipGetLastError();
+}
+#elif defined(DX_SPEC_ONLY)
 #define DX_SPEC_DEFINE(SP)                                                                            \
   bool dx_match_##SP(const DevModel& d, const Lds& L) { return spec_matches<SP>(d, L); }             \
   int dx_occ_##SP(size_t lds) {                                                                       \
@@ -3478,6 +3812,9 @@ extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int
     B.qacc[(size_t)env * m.nv + i] = 0;
   }
   for (int i = LANE; i < m.nu; i += blockDim.x) B.ctrl[(size_t)env * m.nu + i] = 0;
-  if (LANE == 0) B.time[env] = 0;
+  if (LANE == 0) {
+    B.time[env] = 0;
+    if (B.nstep) B.nstep[env] = 0;
+  }
 }
-#endif  // DX_SPEC_ONLY
+#endif  // DX_TIER_HI / DX_SPEC_ONLY

@@ -328,6 +328,11 @@ class GoalEnvironment:
         _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(self._dev_action)))
         return self.timestep()
 
+    def step_random(self, step: int) -> None:
+        """One control step under the random agent: the actions `sample_actions(step)`
+        would draw (manipulation_test.py:44-45), drawn inside the step kernel."""
+        _lib.check(_lib.load().dx_env_step_random(self.ptr, self._seed, step))
+
     def sample_actions(self, step: int) -> int:
         """Fills the device action buffer with uniform actions; returns its address."""
         _lib.check(_lib.load().dx_env_sample_actions(self.ptr, self._seed, step))

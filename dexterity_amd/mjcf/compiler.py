@@ -437,7 +437,9 @@ class Scene:
         attrs["size"] = " ".join(map(str, size))
         self.bodies[0].geoms.append(self._geom_from_attrs(attrs, "", 0))
 
-    def add_free_box(self, name: str, half_size: float, pos, quat=(1, 0, 0, 0), **geom_kw) -> None:
+    def add_free_box(self, name: str, half_size: float, pos, quat=(1, 0, 0, 0), parts=(), **geom_kw) -> None:
+        """A free body with a box geom; `parts`: offsets (body frame) of further boxes of
+        the same size rigidly attached to it (a compound body)."""
         body = _Body(name + "/", 0, np.asarray(pos, float), m3.quat_normalize(np.asarray(quat, float)), None)
         body.joints.append(
             {
@@ -463,6 +465,9 @@ class Scene:
         attrs["name"] = "geom"
         attrs["size"] = f"{half_size} {half_size} {half_size}"
         body.geoms.append(self._geom_from_attrs(attrs, name + "/", 0))
+        for k, off in enumerate(parts):
+            a = dict(attrs, name=f"geom{k + 1}", pos=" ".join(str(float(x)) for x in off))
+            body.geoms.append(self._geom_from_attrs(a, name + "/", k + 1))
         self.bodies.append(body)
 
     def add_site(self, body_name: str, site_name: str, pos=(0, 0, 0)) -> None:
@@ -1115,7 +1120,7 @@ def _mix_pair(g1: dict, g2: dict, i1: int, i2: int) -> dict:
 
 def _inertia_from_geoms(b: _Body, scene: Scene):
     """Body mass/inertia from its geoms at density (box/sphere only; [3P] inertiafromgeom)."""
-    mass = 0.0
+    parts = []
     for g in b.geoms:
         if g["type"] == GEOM_BOX:
             s = g["size"]
@@ -1127,8 +1132,40 @@ def _inertia_from_geoms(b: _Body, scene: Scene):
             diag = np.full(3, 0.4 * m * r * r)
         else:
             continue
-        if mass > 0:
-            raise NotImplementedError("multi-geom inertia")
-        mass = m
-        return mass, g["pos"].copy(), g["quat"].copy(), diag
-    return 0.0, np.zeros(3), np.array([1.0, 0, 0, 0]), np.zeros(3)
+        parts.append((m, g["pos"].copy(), g["quat"].copy(), diag))
+    if not parts:
+        return 0.0, np.zeros(3), np.array([1.0, 0, 0, 0]), np.zeros(3)
+    if len(parts) == 1:
+        return parts[0]
+    # several geoms: total mass, combined com, the inertia tensor about it (parallel
+    # axes), principal axes as the inertial frame ([3P] inertiafromgeom of a body with
+    # several geoms)
+    mass = sum(p[0] for p in parts)
+    com = sum(p[0] * p[1] for p in parts) / mass
+    inert = np.zeros((3, 3))
+    for m, pos, quat, diag in parts:
+        R = m3.quat_to_mat(quat)
+        r = pos - com
+        inert += R @ np.diag(diag) @ R.T + m * (np.dot(r, r) * np.eye(3) - np.outer(r, r))
+    w, V = np.linalg.eigh(inert)
+    if np.linalg.det(V) < 0:
+        V[:, 2] = -V[:, 2]
+    return mass, com, _mat_to_quat(V), w
+
+
+def _mat_to_quat(R: np.ndarray) -> np.ndarray:
+    """Unit quaternion (w, x, y, z) of a rotation matrix (Shepperd's method)."""
+    t = np.trace(R)
+    if t > 0:
+        k = 2.0 * np.sqrt(1.0 + t)
+        q = [0.25 * k, (R[2, 1] - R[1, 2]) / k, (R[0, 2] - R[2, 0]) / k, (R[1, 0] - R[0, 1]) / k]
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, l = (i + 1) % 3, (i + 2) % 3
+        k = 2.0 * np.sqrt(1.0 + R[i, i] - R[j, j] - R[l, l])
+        q = np.zeros(4)
+        q[0] = (R[l, j] - R[j, l]) / k
+        q[1 + i] = 0.25 * k
+        q[1 + j] = (R[j, i] + R[i, j]) / k
+        q[1 + l] = (R[l, i] + R[i, l]) / k
+    return m3.quat_normalize(np.asarray(q, float))

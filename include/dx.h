@@ -87,7 +87,9 @@ enum dx_field {
 /* Loads a compiled-model blob (dexterity_amd/blob.py).  The blob is copied. */
 dx_model* dx_model_load(const void* blob, size_t nbytes);
 void dx_model_free(dx_model* m);
-/* Sizes: out[0..11] = nq nv nbody njnt ngeom nsite nu ntendon nbpair ngpair ncon_max nefc_max */
+/* Sizes: out[0..11] = nq nv nbody njnt ngeom nsite nu ntendon nbpair ngpair ncon_max nefc_max
+ * (ncon_max / nefc_max: the contact pool and constraint-row capacity of a physics step,
+ * DX_NCON_HI = 256 contacts with the overflow tier) */
 int dx_model_sizes(const dx_model* m, int32_t out[12]);
 /* Bytes of LDS one environment (one 64-lane workgroup) of dx_step uses. */
 int dx_model_lds_bytes(const dx_model* m);
@@ -147,14 +149,18 @@ int dx_sensor_enable(dx_batch* b, int enable);
 /* Health (always on) ----------------------------------------------------- */
 /* Counters of capacity overflows and divergences since the batch was created or last
  * cleared, out[0 .. min(n, DX_HEALTH_WORDS)):
- *   0 env-substeps that found more contacts than the DX_NCON_MAX = 32 kept (MuJoCo keeps
- *     up to nconmax = 200 in the Shadow scenes, shadow_hand_series_e.xml:8; the rest
- *     are dropped, as MuJoCo drops contacts beyond nconmax with mjWARN_CONTACTFULL)
+ *   0 env-substeps that found more contacts than the contact pool holds, DX_NCON_HI = 256
+ *     (above the Shadow scenes' nconmax = 200, shadow_hand_series_e.xml:8): the first 256
+ *     in generation (candidate) order are kept, as MuJoCo fills its pool and drops the
+ *     rest with mjWARN_CONTACTFULL
  *   1 env-substeps whose broadphase / narrowphase candidate lists overflowed
  *   2 contacts whose Jacobian spans more than DX_DOFMAX dofs (truncated)
  *   3 env-substeps with more constraint rows than the LDS block holds (truncated)
  *   4 env-substeps that diverged (DX_DIVERGED) and reset their env
- *   5 the most contacts one env-substep found, when above DX_NCON_MAX / 2 (else 0)
+ *   5 the most contacts one env-substep found, when above 16 (else 0)
+ *   6 env-substeps that found more than the 32 contacts the step kernel keeps in LDS and
+ *     were therefore run by the overflow tier (the same physics with the 256-contact
+ *     pool, a second small kernel behind every step launch): not a truncation
  * then, when the histogram is on (dx_ncon_histogram), out[16 .. 16 + 65): env-substeps
  * by contacts found (bins 0..63, then >= 64).  Synchronises the batch's stream. */
 #define DX_HEALTH_WORDS 16
@@ -230,7 +236,10 @@ int dx_env_obs_dim(const dx_env* e);
 int dx_env_goal_dim(const dx_env* e);
 /* Re-initialises every env (initialize_episode) and computes FIRST observations. */
 int dx_env_reset(dx_env* e);
-/* One control step for every env; action is [nenv][nu] float32, device memory. */
+/* One control step for every env; action is [nenv][nu] float32, device memory.  The
+ * reorient task's before_step / after_step / reward / observation run inside the step
+ * kernel: a control step is two kernel launches (the step kernel and the overflow tier's,
+ * which also orders the next launch). */
 int dx_env_step(dx_env* e, const float* action);
 /* composer.Environment's time_limit (manipulation/__init__.py:61,83): an episode also
  * ends (LAST, with the task's discount) once its physics time reaches `seconds`.
@@ -253,6 +262,10 @@ int dx_env_output(dx_env* e, int which, void** devptr);
  * manipulation_test.py:44-45), keyed by (seed, env, step). */
 int dx_env_action_buffer(dx_env* e, void** devptr);
 int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
+/* dx_env_step with the actions dx_env_sample_actions(e, seed, step) would draw, drawn
+ * inside the step kernel (no action buffer, no extra launch): the random agent of the
+ * reference's environment tests and of the benchmark. */
+int dx_env_step_random(dx_env* e, uint64_t seed, int32_t step);
 
 /* Packs [obs | reward | discount | step_type] per env into dst ([nenv][obs_dim+3]
  * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */

@@ -228,6 +228,70 @@ def test_time_limit_on_control_step_boundary(built, limit):
     env.close()
 
 
+def test_time_limit_past_fp32_time_resolution(built):
+    """A 60 s time limit (12,000 physics steps): the episode ends at the control step
+    MuJoCo's fp64 time reaches it.  The env's fp64 time is the sum of exactly as many
+    additions of h as physics steps were taken (an integer count that travels with the
+    state); recovering that count from the fp32 batch time (rint(t / h)) goes wrong after
+    ~11,000 physics steps at h = 0.005."""
+    from dexterity_amd import _lib, manipulation
+
+    cfg = manipulation.ReOrientConfig(fall_termination=False)
+    env = manipulation.GoalEnvironment(manipulation.ReOrient(cfg), num_envs=8, seed=4, time_limit=60.0)
+    _lib.check(_lib.load().dx_env_set_goal_time_limit(env.ptr, 1e9))
+    k = _fp64_time_steps(60.0, cfg.physics_timestep, cfg.n_sub_steps)
+    assert k == 2400
+    env.reset()
+    ended = np.zeros(8, dtype=bool)  # envs that ended early (a success): not checked
+    for i in range(k + 1):
+        env.step_random(i)
+        st = env._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0]
+        if i < k - 1:
+            ended |= st == 2
+        elif i == k - 1:
+            assert np.all(st[~ended] == 2), (st, ended)
+        else:
+            assert np.all(st[~ended] == 0)
+    assert (~ended).sum() >= 4
+    env.close()
+
+
+def test_fused_task_logic_matches_task_kernels(built, monkeypatch):
+    """The reorient task logic fused into the step kernel (task_pre in an env's first
+    physics-step task, task_post in its last; dx_task.h) equals the task kernels around
+    the step kernel (DX_NO_FUSE=1) bit for bit -- resets, goal changes, rewards,
+    observations and the physics state -- over 1024 envs x 30 control steps of random
+    actions; and dx_env_step_random (actions drawn in the kernel) equals stepping with
+    dx_env_sample_actions' buffer."""
+    from dexterity_amd import _lib, manipulation
+
+    outs = []
+    for variant in ("kernels", "fused", "random"):
+        if variant == "kernels":
+            monkeypatch.setenv("DX_NO_FUSE", "1")
+        else:
+            monkeypatch.delenv("DX_NO_FUSE", raising=False)
+        env = manipulation.load("reorient", "state_dense", seed=9, num_envs=1024)
+        env.reset()
+        sts = []
+        for i in range(30):
+            if variant == "random":
+                env.step_random(i)
+            else:
+                env.step(env.sample_actions(i), device_action=True)
+            sts.append(env._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0])
+        ts = env.timestep()
+        outs.append((np.stack(sts), ts.reward, ts.discount,
+                     np.concatenate([v.reshape(1024, -1) for v in ts.observation.values()], axis=1),
+                     env.physics.qpos, env.physics.qvel, env.goals(), env.successes()))
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        env.close()
+    assert (outs[0][0] == 2).any() and (outs[0][0] == 0).any()  # episodes ended and restarted
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            np.testing.assert_array_equal(a, b)
+
+
 def test_goal_time_limit_on_control_step_boundary(built):
     """max_time_per_goal = 2 control steps (0.05 s): GoalTask's time - start > max_time
     in fp64 is first true after the 3rd step (task.py:180-183)."""

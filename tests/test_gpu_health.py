@@ -11,41 +11,30 @@ from dexterity_amd import _lib
 pytestmark = pytest.mark.gpu
 
 
-def _box_field(n_boxes):
-    """A ground plane and `n_boxes` free cubes (half-size 2 cm) resting 1 mm into it,
-    apart from one another: every cube-plane pair yields 4 contacts (plane-box corners),
-    so 10 cubes give 40 contacts, above the 32 kept per env-substep.  Built from the
-    compiler's own primitives (no reference files), so it compiles on the GPU box."""
-    from dexterity_amd.mjcf.compiler import Scene
-
-    s = Scene(timestep=0.005)
-    s.add_world_geom("ground", "plane", (1, 1, 0.1), friction="0.4 0.005 0.0001", solimp="0.95 0.99 0.001",
-                     solref="0.002 1")
-    for i in range(n_boxes):
-        s.add_free_box(f"box{i}", 0.02, [0.1 * (i % 5) - 0.2, 0.1 * (i // 5), 0.019])
-    return s.compile()
-
-
-def test_contact_overflow_is_counted():
+def test_contact_pool_is_reported():
+    """A ground plane and 10 resting cubes (40 contacts, tests/test_gpu_contact_pool.py):
+    each physics step goes to the overflow tier (counted as deferred, not truncated) and
+    keeps all 40 contacts; with 7 cubes (28) the step kernel keeps them itself."""
     from dexterity_amd import physics
+    from tests.test_gpu_contact_pool import box_field
 
-    cm = _box_field(10)
+    cm = box_field(10)
     model = physics.Model(cm)
     ph = physics.BatchedPhysics(model, 8)
     ph.ncon_histogram(True)
     ph.health_clear()
     ph.step(1)
     h = ph.health()
-    assert h["contact_overflow"] == 8, h
+    assert h["contact_overflow"] == 0 and h["contact_deferred"] == 8, h
     assert h["ncon_max"] == 40, h
     assert h["ncon_hist"][40] == 8 and h["ncon_hist"].sum() == 8
     assert h["diverged"] == 0
-    assert np.all(ph.get(_lib.NCON)[:, 0] == 32)
-    # below the cap nothing is reported
-    ph2 = physics.BatchedPhysics(physics.Model(_box_field(7)), 8)
+    assert np.all(ph.get(_lib.NCON)[:, 0] == 40)
+    # below the step kernel's 32 nothing is deferred
+    ph2 = physics.BatchedPhysics(physics.Model(box_field(7)), 8)
     ph2.step(2)
     h2 = ph2.health()
-    assert h2["contact_overflow"] == 0 and h2["ncon_max"] == 28, h2
+    assert h2["contact_overflow"] == 0 and h2["contact_deferred"] == 0 and h2["ncon_max"] == 28, h2
     assert np.all(ph2.get(_lib.NCON)[:, 0] == 28)
 
 

@@ -532,6 +532,36 @@ def test_substep_queue_matches_per_env_launch(gpu, monkeypatch):
         np.testing.assert_array_equal(a, b)
 
 
+def test_narrowphase_group_size_is_invisible(gpu, monkeypatch):
+    """The narrowphase's 4-lane groups (sixteen pairs per wave, dx_step.hip narrow_pass<4>,
+    used above eight candidates) and its 8-lane groups give bit-identical trajectories:
+    every pair's support scan, first-maximiser rule and portal arithmetic are the same,
+    and the separating-direction cache -- whose slots two pairs share, so which pair owns
+    one depends on the order the groups finish -- never decides a verdict MPR would not
+    (mpr_init, DX_SEP_CLEAR).  DX_NP_WIDE=0 forces 4-lane groups on every substep, 64
+    never; 4096 envs, 15 control steps of random actions, contacts included, no
+    allowance for any env to differ."""
+    from dexterity_amd import manipulation
+
+    outs = []
+    for wide in ("0", "64"):
+        monkeypatch.setenv("DX_NP_WIDE", wide)
+        env = manipulation.load("reorient", "state_dense", seed=7, num_envs=4096)
+        env.reset()
+        for step in range(15):
+            env.step(env.sample_actions(step), device_action=True)
+        ts = env.timestep()
+        ncon = env.physics.get(_lib.NCON)[:, 0]
+        outs.append((env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART), ncon, ts.reward))
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        env.close()
+    assert (outs[0][3] > 0).mean() > 0.5
+    differ = np.zeros(4096, dtype=bool)
+    for a, b in zip(*outs):
+        differ |= (np.asarray(a).reshape(4096, -1) != np.asarray(b).reshape(4096, -1)).any(axis=1)
+    assert differ.sum() == 0, np.flatnonzero(differ)
+
+
 def _check_reach_rewards(env, ts, dense):
     from oracle import task_ref
 

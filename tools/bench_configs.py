@@ -39,13 +39,13 @@ def env_config(name, domain, task, nenv, steps=50, warmup=10, solver=None):
         env = manipulation.GoalEnvironment(t, num_envs=nenv, seed=7)
     env.reset()
     for i in range(warmup):
-        env.step(env.sample_actions(i), device_action=True)
+        env.step_random(i)
     env.physics.sync()
     L.dx_timing_enable(env.physics.ptr, 1)
     _kernel_ms(L, env.physics.ptr)
     t = time.perf_counter()
     for i in range(steps):
-        env.step(env.sample_actions(warmup + i), device_action=True)
+        env.step_random(warmup + i)
     env.physics.sync()
     dt = time.perf_counter() - t
     kms, kn = _kernel_ms(L, env.physics.ptr)

@@ -26,7 +26,7 @@ def main(nenv=4096, steps=60):
         if i >= 10:
             _lib.check(L.dx_timing_enable(env.physics.ptr, 1))
             _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int32())))
-        env.step(env.sample_actions(i), device_action=True)
+        env.step_random(i)
         if i >= 10:
             costs.append(env.physics.get(_lib.STEP_COST).ravel().astype(np.float64) * 1024)
             kt, kn = ctypes.c_double(), ctypes.c_int32()

@@ -26,7 +26,7 @@ if scene == "reorient":
     env.reset()
     ph.health_clear()
     for i in range(steps):
-        env.step(env.sample_actions(i), device_action=True)
+        env.step_random(i)
         if i % 100 == 99:
             print(f"step {i + 1}: {ph.health()}", flush=True)
     nsub = env.task.config.n_sub_steps

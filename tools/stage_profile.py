@@ -16,14 +16,14 @@ env = manipulation.load("reorient", "state_dense", seed=3, num_envs=B)
 L = _lib.load()
 env.reset()
 for i in range(10):
-    env.step(env.sample_actions(i), device_action=True)
+    env.step_random(i)
 env.physics.sync()
 _lib.check(L.dx_stage_timing(env.physics.ptr, 1))
 buf = (ctypes.c_uint64 * (_lib.NSTAGE * B))()
 _lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE * B))
 t = time.perf_counter()
 for i in range(steps):
-    env.step(env.sample_actions(100 + i), device_action=True)
+    env.step_random(100 + i)
 env.physics.sync()
 dt = time.perf_counter() - t
 _lib.check(L.dx_stage_read(env.physics.ptr, buf, _lib.NSTAGE * B))
