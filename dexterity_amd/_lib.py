@@ -37,7 +37,7 @@ EXPORTS = (
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
     "dx_env_set_time_limit", "dx_set_outputs", "dx_env_create_shard",
     "dx_health", "dx_health_clear", "dx_ncon_histogram", "dx_env_set_goal_time_limit",
-    "dx_env_step_random",
+    "dx_env_step_random", "dx_env_save", "dx_env_load", "dx_env_state_field",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -134,6 +134,10 @@ def load(path: str = LIB_PATH):
     L.dx_env_action_buffer.argtypes = [vp, ctypes.POINTER(vp)]
     L.dx_env_sample_actions.argtypes = [vp, ctypes.c_uint64, i32]
     L.dx_env_step_random.argtypes = [vp, ctypes.c_uint64, i32]
+    L.dx_env_save.argtypes = [vp, vp, sz]
+    L.dx_env_load.argtypes = [vp, vp, sz]
+    L.dx_env_state_field.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
+                                     ctypes.POINTER(sz)]
     L.dx_env_pack_outputs.argtypes = [vp, vp]
     L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]

@@ -924,6 +924,7 @@ struct dx_batch {
   bool qhead_zero = false;  // the last kernel on the stream zeroed the queue heads
   int* watch_list = nullptr;  // device copy of DevBatch::watch_pairs
   int slots;   // persistent workgroups of a queued launch
+  int hi_grid; // workgroups of the overflow tier's launch
   float* xfrc;
   std::vector<void*> allocs;
   bool debug;
@@ -931,6 +932,8 @@ struct dx_batch {
   float* sen_stash = nullptr;
   unsigned* ncon_hist = nullptr;  // dx_ncon_histogram
 };
+
+#define DX_HI_GRID 32  // workgroups of the overflow tier (each loops over the deferred steps)
 
 static int balloc(dx_batch* b, void** p, size_t bytes) {
   HIPCHK(hipMalloc(p, std::max<size_t>(bytes, 4)));
@@ -1008,6 +1011,8 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
   B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
+  B.defer_at = getenv("DX_DEFER_AT") ? atoi(getenv("DX_DEFER_AT")) : DX_NCON_MAX;  // (tests / probes)
+  b->hi_grid = getenv("DX_HI_GRID") ? std::max(1, atoi(getenv("DX_HI_GRID"))) : DX_HI_GRID;
   {
     int ncu = 0;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu < 1) ncu = 256;
@@ -1179,7 +1184,6 @@ extern "C" int dx_set_watch(dx_batch* b, int32_t geom, int32_t body) {
 static void timing_begin(dx_batch* b, hipEvent_t* start);
 static void timing_end(dx_batch* b, hipEvent_t start);
 
-#define DX_HI_GRID 32  // workgroups of the overflow tier (each loops over the deferred steps)
 static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
@@ -1211,7 +1215,7 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   // (nothing to do unless some env deferred one), the next launch's longest-first order,
   // and the queue heads zeroed for the next launch
   if (b->db.defer && mode != 2) {
-    HIPCHK(dx_launch_step_hi(DX_HI_GRID, (size_t)b->model->lds_hi.total * 4, b->stream, b->dm_dev, b->db,
+    HIPCHK(dx_launch_step_hi(b->hi_grid, (size_t)b->model->lds_hi.total * 4, b->stream, b->dm_dev, b->db,
                              b->model->lds_hi, nsub));
     b->qhead_zero = true;
   }
@@ -1765,6 +1769,98 @@ extern "C" int dx_env_step(dx_env* e, const float* action) {
 extern "C" int dx_env_step_random(dx_env* e, uint64_t seed, int32_t step) {
   if (!e) return fail(DX_EINVAL, "null env");
   return env_run(e, nullptr, true, seed, step);
+}
+
+// ------------------------------------------------------------------------ //
+// checkpoint / resume: every device array whose contents carry from one
+// control step to the next -- physics state (qpos, qvel, ctrl, warm start, fp32 time, the
+// physics-step count behind the fp64 time), task state (goals, counters, step types, fp64
+// times, observation, rewards), both numpy-compatible MT19937 streams of an env (reach:
+// the RandomState block with numpy's cached gaussian), and the longest-first order.  The
+// separating-direction cache is left out: it never changes a result (dx_step.hip
+// mpr_init).  Restoring into an env of the same task, model and size resumes the run bit
+// for bit.
+// ------------------------------------------------------------------------ //
+struct StateField {
+  const char* name;
+  void* ptr;
+  size_t bytes;
+};
+static std::vector<StateField> env_state_fields(dx_env* e) {
+  dx_batch* b = e->batch;
+  const DevBatch& B = b->db;
+  const TaskState& S = e->S;
+  const TaskParams& P = e->P;
+  const size_t E = b->nenv;
+  const DevModel& d = b->dm;
+  std::vector<StateField> f = {
+      {"qpos", B.qpos, E * d.nq * 4}, {"qvel", B.qvel, E * d.nv * 4},
+      {"ctrl", B.ctrl, E * std::max(d.nu, 1) * 4}, {"qacc_warmstart", B.qacc_ws, E * d.nv * 4},
+      {"qacc", B.qacc, E * d.nv * 4}, {"time", B.time, E * 4}, {"nstep", B.nstep, E * 4},
+      {"diverged", B.bad, E * 4},
+      {"goal", S.goal, E * P.goal_dim * 4}, {"solve_start", S.solve_start, E * 4},
+      {"reward", S.reward, E * 4}, {"discount", S.discount, E * 4}, {"obs", S.obs, E * P.obs_dim * 4},
+      {"successes", S.successes, E * 4}, {"counter", S.counter, E * 4}, {"registered", S.registered, E * 4},
+      {"exceeded", S.exceeded, E * 4}, {"step_type", S.step_type, E * 4}, {"episode", S.episode, E * 4},
+      {"skip", S.skip, E * 4}, {"failure", S.failure, E * 4}, {"need", S.need, E * 4},
+      {"goalnum", S.goalnum, E * 4}, {"goalfail", S.goalfail, E * 4}, {"time_d", S.time_d, E * 8},
+      {"solve_start_d", S.solve_start_d, E * 8}, {"nsub_d", S.nsub_d, E * 4}, {"solve_n", S.solve_n, E * 4},
+  };
+  if (S.goal_qpos) f.push_back({"goal_qpos", S.goal_qpos, E * d.nq * 4});
+  if (S.mt_env) f.push_back({"mt_env", S.mt_env, E * DX_MT_WORDS * 4});
+  if (S.mt_goal) f.push_back({"mt_goal", S.mt_goal, E * DX_MT_WORDS * 4});
+  if (S.mt_reach) f.push_back({"mt_reach", S.mt_reach, E * DX_MTW_WORDS * 4});
+  if (B.cost) f.push_back({"step_cost", B.cost, E * 4});
+  if (B.order) f.push_back({"order", (void*)B.order, E * 4});
+  return f;
+}
+
+extern "C" int dx_env_state_field(dx_env* e, int32_t i, const char** name, size_t* offset, size_t* nbytes) {
+  if (!e || !name || !offset || !nbytes) return fail(DX_EINVAL, "null argument");
+  const auto f = env_state_fields(e);
+  if (i < 0) return (int)f.size();
+  if (i >= (int)f.size()) return fail(DX_EINVAL, "state field out of range");
+  size_t off = 0;
+  for (int k = 0; k < i; k++) off += f[k].bytes;
+  *name = f[i].name;
+  *offset = off;
+  *nbytes = f[i].bytes;
+  return (int)f.size();
+}
+
+extern "C" int dx_env_save(dx_env* e, void* dst, size_t nbytes) {
+  if (!e) return fail(DX_EINVAL, "null env");
+  const auto f = env_state_fields(e);
+  size_t tot = 0;
+  for (auto& x : f) tot += x.bytes;
+  if (!dst) return (int)std::min<size_t>(tot, 0x7fffffff);  // the size query
+  if (nbytes < tot) return fail(DX_EINVAL, "checkpoint buffer too small");
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  size_t off = 0;
+  for (auto& x : f) {
+    HIPCHK(hipMemcpyAsync((char*)dst + off, x.ptr, x.bytes, hipMemcpyDefault, b->stream));
+    off += x.bytes;
+  }
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return queue_check(b);
+}
+
+extern "C" int dx_env_load(dx_env* e, const void* src, size_t nbytes) {
+  if (!e || !src) return fail(DX_EINVAL, "null argument");
+  const auto f = env_state_fields(e);
+  size_t tot = 0;
+  for (auto& x : f) tot += x.bytes;
+  if (nbytes != tot) return fail(DX_EINVAL, "checkpoint size does not match this env (task, model, batch size)");
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  size_t off = 0;
+  for (auto& x : f) {
+    HIPCHK(hipMemcpyAsync(x.ptr, (const char*)src + off, x.bytes, hipMemcpyDefault, b->stream));
+    off += x.bytes;
+  }
+  HIPCHK(hipStreamSynchronize(b->stream));
+  return 0;
 }
 
 extern "C" int dx_env_output(dx_env* e, int which, void** devptr) {

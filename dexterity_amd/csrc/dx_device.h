@@ -217,6 +217,7 @@ struct CtxT {
   float4* sep = nullptr;  // this env's separating-direction cache (DX_SEP_SLOTS), or null
   int np_wide = DX_WAVE / 8;  // narrowphase: 4-lane groups above this many candidates
   bool defer = false;         // a full contact pool defers the physics step (I_DEFER)
+  int defer_at = DX_NCON_MAX; // ... or more contacts than this (DX_DEFER_AT: tests, probes)
   __device__ CtxT(const DevModel& m_, const Lds&, float* S_, int* I_, unsigned long long* acc)
       : m(m_), S(S_), I(I_), stage_acc(acc) {}
   __device__ float* f(int off) const { return S + off; }
@@ -235,6 +236,7 @@ struct CtxT<SpecRT> {
   float4* sep = nullptr;
   int np_wide = DX_WAVE / 8;
   bool defer = false;
+  int defer_at = DX_NCON_MAX;
   __device__ CtxT(const DevModel& m_, const Lds& L_, float* S_, int* I_, unsigned long long* acc)
       : m(m_), L(L_),
 #define DX_X(n) n(m_.n),
@@ -1033,6 +1035,62 @@ __device__ __forceinline__ void mfma_sweep_solve30(const float* A, int n, float 
       const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
       if (i < n) x[i] = C[v];
     }
+  }
+  SYNC();
+}
+
+// The inverse of an n <= 30 SPD matrix by the same sweep: sweeping every pivot of A
+// leaves -A^-1 in the accumulator.  Unlike mfma_sweep_solve30 every entry is kept exact
+// (the pivot rows and columns are zeroed whole before each rank-2 update), and -C is
+// written to Ainv as a packed lower triangle (may not alias A).  For repeated solves with
+// one matrix: CG's M^-1 grad, one matrix-vector product per iteration instead of a sweep.
+__device__ __forceinline__ void mfma_sweep_inverse30(const float* A, int n, float* Ainv) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  const int jc = min(j, n - 1);
+  float av[16];
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int ic = min(8 * (v >> 2) + 4 * hi + (v & 3), n - 1);
+    av[v] = A[ti(max(ic, jc)) + min(ic, jc)];
+  }
+  dx_f16v C;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    C[v] = i < n && j < n ? av[v] : (i == j ? 1.f : 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 30; k += 2) {
+    if (k >= n) continue;  // identity padding (a uniform branch)
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // S[k][j], S[k+1][j]
+    const float p00 = rl(rk, k), p10 = rl(rk1, k), p11 = rl(rk1, k + 1);
+    const float id = 1.0f / (p00 * p11 - p10 * p10);
+    const float w00 = p11 * id, w01 = -p10 * id, w11 = p00 * id;
+    const bool pc = j == k || j == k + 1;  // a pivot column
+    const float v0 = pc ? (j == k ? -1.f : 0.f) : rk;
+    const float v1 = pc ? (j == k ? 0.f : -1.f) : rk1;
+    const float a = hi ? v1 : v0;
+    const float b = hi ? fmaf(w01, v0, w11 * v1) : fmaf(w00, v0, w01 * v1);
+    const dx_f2v mk = {pc ? 0.f : 1.f, pc ? 0.f : 1.f};
+#pragma unroll
+    for (int v = 0; v < 16; v += 2) {  // the pivot columns, every row
+      dx_f2v t = {C[v], C[v + 1]};
+      t = t * mk;
+      C[v] = t.x;
+      C[v + 1] = t.y;
+    }
+    const bool ph = hi == (up ? 1 : 0);  // the pivot rows, every column
+    C[vk] = ph ? 0.f : C[vk];
+    C[vk + 1] = ph ? 0.f : C[vk + 1];
+    C = __builtin_amdgcn_mfma_f32_32x32x2f32(-a, b, C, 0, 0, 0);
+  }
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    if (i < n && j <= i) Ainv[ti(i) + j] = -C[v];
   }
   SYNC();
 }

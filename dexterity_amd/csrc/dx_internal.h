@@ -177,6 +177,7 @@ struct DevBatch {
   // << 24 | forward-only << 30, appended by the step kernel, emptied by the overflow
   // kernel's last workgroup
   unsigned* defer;
+  int defer_at;  // defer a physics step with more contacts than this (DX_NCON_MAX; DX_DEFER_AT for tests)
   // Task logic fused into the step kernel (dx_task.h; DevBatch::tp / ts): task_pre in the
   // env's first physics-step task, with ctrl = the action (`action`, [nenv][nu], or drawn
   // in the kernel by the random agent when act_random: dx_urand(act_seed, env0 + env,

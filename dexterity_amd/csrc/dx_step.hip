@@ -91,7 +91,12 @@ __device__ __forceinline__ void msel(MPoint& dst, const MPoint& src, bool c) {
   }
 }
 
-__device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-10f; }
+// MPR's zero test: the oracle's (dx_oracle.c is_zero, |x| < 1e-14), absolute as there.
+// (A looser 1e-10 made the degenerate-portal test |v0 x v1|^2 ~ 0 fire for centimetre-scale
+// Minkowski vectors up to ~1.4 degrees apart: the "origin on segment v0-v1" shortcut then
+// reported a contact whose depth and normal are not a face of the Minkowski difference --
+// found on deep finger-finger contacts of the bench's state mix, tools/full_batch_diag.py.)
+__device__ __forceinline__ bool fzero(float x) { return fabsf(x) < 1e-14f; }
 // The portal points are four separate MPoint variables (not an array): an array of
 // structs with conditional element copies stayed an alloca in scratch memory.
 __device__ __forceinline__ void portal_dir(const MPoint& P1, const MPoint& P2, const MPoint& P3, float* dir) {
@@ -1227,7 +1232,7 @@ __device__ __forceinline__ void collision(const Ctx& c, int watch_only, int wg, 
                                       : narrow_pass<8>(c, ng, gcand, gcrec, con, cntq);
   int ncon = ncon_raw;
   SYNC();
-  if (ncon_raw > DX_NCON_MAX && !watch_only) {
+  if (ncon_raw > (c.defer ? min(DX_NCON_MAX, c.defer_at) : DX_NCON_MAX) && !watch_only) {
     if (c.defer) {
       // the step kernel's pool is full: this physics step runs in the overflow tier
       // (dx_step_hi, DX_NCON_HI contacts) from the unchanged state (env_substep)
@@ -2417,14 +2422,26 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
   const float* M = c.f(c.L.M);
   const float* qs = c.f(c.L.qfrc_smooth);
   float* T = c.f(c.L.H);
+  // M^-1 once per solve (nv <= 30: the sweep's inverse, packed in the Newton Hessian's
+  // region, which CG does not use), then one product per iteration; larger nv solve each
+  // time (the LDS Cholesky)
+  const bool inv = DX_SWEEP && nv <= 30;
+  if (inv) mfma_sweep_inverse30(M, nv, T);
+  auto minv = [&]() {
+    if (inv) {
+      mat_vec(T, grad, Mg, nv);
+      SYNC();
+    } else {
+      for (int i = LANE; i < nv; i += DX_WAVE) Mg[i] = grad[i];
+      SYNC();
+      chol_solve(M, nv, Mg, T);
+    }
+  };
   int it = 0;
   jac_t_force(c, grad);  // grad <- J^T f
-  for (int i = LANE; i < nv; i += DX_WAVE) {
-    grad[i] = Ma[i] - qs[i] - grad[i];
-    Mg[i] = grad[i];
-  }
+  for (int i = LANE; i < nv; i += DX_WAVE) grad[i] = Ma[i] - qs[i] - grad[i];
   SYNC();
-  chol_solve(M, nv, Mg, T);
+  minv();
   float gmg = 0;
   for (int i = LANE; i < nv; i += DX_WAVE) {
     dir[i] = -Mg[i];
@@ -2454,12 +2471,11 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
     float gn = 0;
     for (int i = LANE; i < nv; i += DX_WAVE) {
       grad[i] = Ma[i] - qs[i] - grad[i];
-      Mg[i] = grad[i];
       gn += grad[i] * grad[i];
     }
     gn = sqrtf(wave_sum(gn)) * scale;
     SYNC();
-    chol_solve(M, nv, Mg, T);
+    minv();
     stage_mark(c, ST_NEWTON_GRAD);
     if (impr < tol || gn < tol) {
       it++;
@@ -3393,6 +3409,7 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   c.I = (int*)(smem + c.L.ints);
   c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
   c.np_wide = B.np_wide;
+  c.defer_at = B.defer_at;
   c.defer = !prep && B.defer;  // (the reach sampling pass keeps its pool and cuts it)
   if (prep) {  // reach sampling pass (mode 2): new state only, no outputs
     float time = env_begin(c, B, env);
@@ -3462,6 +3479,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   CtxT<SP> c(m, Lrt, smem, nullptr, nullptr);
   c.I = (int*)(smem + c.L.ints);
   c.np_wide = B.np_wide;
+  c.defer_at = B.defer_at;
   c.defer = B.defer != nullptr;
   const int nqueue = B.nqueue;
   unsigned xcc;

@@ -338,6 +338,61 @@ class GoalEnvironment:
         _lib.check(_lib.load().dx_env_sample_actions(self.ptr, self._seed, step))
         return self._dev_action
 
+    # ---------------------------------------------------------------- checkpoint
+    # dtype of the state fields that are not float32 (include/dx.h dx_env_save)
+    _STATE_DTYPES = {"nstep": np.int32, "diverged": np.int32, "successes": np.int32, "counter": np.int32,
+                     "registered": np.int32, "exceeded": np.int32, "step_type": np.int32, "episode": np.int32,
+                     "skip": np.int32, "failure": np.int32, "need": np.int32, "goalnum": np.int32,
+                     "goalfail": np.int32, "time_d": np.float64, "solve_start_d": np.float64,
+                     "nsub_d": np.int32, "solve_n": np.int32, "mt_env": np.uint32, "mt_goal": np.uint32,
+                     "mt_reach": np.uint32, "step_cost": np.uint32, "order": np.int32}
+
+    def _state_fields(self):
+        L = _lib.load()
+        name, off, nb = ctypes.c_char_p(), ctypes.c_size_t(), ctypes.c_size_t()
+        n = _lib.check(L.dx_env_state_field(self.ptr, -1, ctypes.byref(name), ctypes.byref(off), ctypes.byref(nb)))
+        out = []
+        for i in range(n):
+            _lib.check(L.dx_env_state_field(self.ptr, i, ctypes.byref(name), ctypes.byref(off), ctypes.byref(nb)))
+            out.append((name.value.decode(), off.value, nb.value))
+        return out
+
+    def save(self, path: str) -> None:
+        """Checkpoint every env's state (physics, task, RNG streams, dispatch order) to an
+        .npz of named [num_envs, ...] arrays (SURVEY.md §5 checkpoint / resume); `load`
+        into an env of the same task and size continues the run bit for bit."""
+        L = _lib.load()
+        nbytes = _lib.check(L.dx_env_save(self.ptr, None, 0))
+        buf = np.empty(nbytes, dtype=np.uint8)
+        _lib.check(L.dx_env_save(self.ptr, buf.ctypes.data, nbytes))
+        arrays = {}
+        for name, off, nb in self._state_fields():
+            a = buf[off:off + nb].view(self._STATE_DTYPES.get(name, np.float32))
+            arrays[name] = a.reshape(self.num_envs, -1) if name not in ("mt_env", "mt_goal") else a.reshape(-1, self.num_envs)
+        meta = np.array([self.num_envs, self.model.nq, self.model.nv, self.model.nu, self.obs_dim, self.env_offset],
+                        dtype=np.int64)
+        np.savez(path, __meta__=meta, **arrays)
+
+    def load(self, path: str) -> None:
+        """Restores a checkpoint written by `save` (same task, model and num_envs)."""
+        L = _lib.load()
+        with np.load(path, allow_pickle=False) as z:
+            meta = z["__meta__"]
+            want = [self.num_envs, self.model.nq, self.model.nv, self.model.nu, self.obs_dim, self.env_offset]
+            if list(meta) != want:
+                raise ValueError(f"checkpoint is for (num_envs, nq, nv, nu, obs_dim, env_offset) = {list(meta)}, "
+                                 f"this env is {want}")
+            fields = self._state_fields()
+            nbytes = sum(nb for _, _, nb in fields)
+            buf = np.empty(nbytes, dtype=np.uint8)
+            for name, off, nb in fields:
+                a = np.ascontiguousarray(z[name])
+                if a.nbytes != nb:
+                    raise ValueError(f"checkpoint field {name}: {a.nbytes} bytes, expected {nb}")
+                buf[off:off + nb] = a.view(np.uint8).ravel()
+        self.physics.sync()
+        _lib.check(L.dx_env_load(self.ptr, buf.ctypes.data, nbytes))
+
     def _read(self, which: int, dtype, width: int) -> np.ndarray:
         out = np.empty((self.num_envs, width), dtype=dtype)
         ptr = self._out(which)

@@ -267,6 +267,17 @@ int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step);
  * reference's environment tests and of the benchmark. */
 int dx_env_step_random(dx_env* e, uint64_t seed, int32_t step);
 
+/* Checkpoint / resume.  An env's state is the set of device arrays that carry from one
+ * control step to the next (physics and task state, the numpy-compatible MT19937 streams,
+ * the dispatch order).  dx_env_save(e, NULL, 0) returns the state's size in bytes;
+ * dx_env_save copies it to dst (host or device memory), dx_env_load restores it into an
+ * env of the same task, model and batch size: the run then continues bit for bit as the
+ * saved one would have.  dx_env_state_field(e, i, ...) describes field i (name, byte
+ * offset in the saved buffer, bytes; i < 0: the count) and returns the field count. */
+int dx_env_save(dx_env* e, void* dst, size_t nbytes);
+int dx_env_load(dx_env* e, const void* src, size_t nbytes);
+int dx_env_state_field(dx_env* e, int32_t i, const char** name, size_t* offset, size_t* nbytes);
+
 /* Packs [obs | reward | discount | step_type] per env into dst ([nenv][obs_dim+3]
  * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */
 int dx_env_pack_outputs(dx_env* e, float* dst_dev);

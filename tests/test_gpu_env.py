@@ -292,6 +292,56 @@ def test_fused_task_logic_matches_task_kernels(built, monkeypatch):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("domain", ["reorient", "reach"])
+def test_checkpoint_resume_is_bit_exact(built, domain, tmp_path):
+    """Checkpoint / resume: a run saved after control step 10 and resumed
+    in a fresh env (another seed, so nothing but the checkpoint carries the state) equals
+    the uninterrupted run bit for bit at step 25 -- physics, task counters, goals,
+    observations, and the MT19937 streams that later resets draw from (episodes end and
+    restart within the window)."""
+    from dexterity_amd import _lib, manipulation
+
+    task = "state_dense"
+    n = 512
+
+    def run(env, steps):
+        st = []
+        for i in steps:
+            env.step_random(i)
+            st.append(env._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0])
+        return np.stack(st)
+
+    def outputs(env):
+        ts = env.timestep()
+        return (ts.reward, ts.discount, ts.step_type,
+                np.concatenate([v.reshape(n, -1) for v in ts.observation.values()], axis=1),
+                env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART), env.goals(),
+                env.successes())
+
+    a = manipulation.load(domain, task, seed=21, num_envs=n)
+    a.reset()
+    run(a, range(10))
+    path = str(tmp_path / "ckpt.npz")
+    a.save(path)
+    sa = run(a, range(10, 25))
+    ref = outputs(a)
+    a.close()
+    b = manipulation.load(domain, task, seed=99, num_envs=n)
+    b.reset()
+    b._seed = 21  # the random agent's key (dx_env_step_random) is the caller's, as in the run
+    b.load(path)
+    sb = run(b, range(10, 25))
+    got = outputs(b)
+    b.close()
+    if domain == "reorient":
+        assert (sa == 2).any() and (sa == 0).any()  # episodes ended and restarted in the window
+    np.testing.assert_array_equal(sa, sb)
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
+    with np.load(path) as z:
+        assert z["qpos"].shape[0] == n and z["time_d"].dtype == np.float64
+
+
 def test_goal_time_limit_on_control_step_boundary(built):
     """max_time_per_goal = 2 control steps (0.05 s): GoalTask's time - start > max_time
     in fp64 is first true after the 3rd step (task.py:180-183)."""

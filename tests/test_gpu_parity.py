@@ -443,22 +443,99 @@ def test_success_kat_on_gpu(gpu):
     env.close()
 
 
-def test_full_batch_properties(gpu):
-    """4096 envs (BASELINE config 3), 40 control steps: finite, resets exercised."""
+def _nearest_perturbed(oracle_mod, om, xfrc32, st, nsub, gq, gv, scale, k=32, rel=6e-8, seed=0):
+    """The GPU's result (gq, gv) against the nearest of k oracle runs from the state
+    perturbed at fp32 resolution (relative `rel` on qpos and qvel; run 0 unperturbed):
+    (qpos err, qvel err / scale).  MPR is discontinuous at deep or flat contacts -- the
+    fp64 oracle's own contact normal jumps by up to 0.16 rad under 6e-8 relative input
+    perturbations in 4 of 60 deep-contact states (round 4) -- so a GPU result equal to one
+    of these runs is the reference algorithm's answer for an input within the fp32
+    rounding of the GPU's (the generalisation of _oracle_pair)."""
+    rng = np.random.RandomState(seed)
+    q, v, w, c = (np.asarray(x, dtype=np.float64) for x in st)
+    Q = np.tile(q, (k, 1))
+    V = np.tile(v, (k, 1))
+    Q[1:] *= 1 + rng.standard_normal(Q[1:].shape) * rel
+    V[1:] *= 1 + rng.standard_normal(V[1:].shape) * rel
+    rc, oq, ov, _ = oracle_mod.batch_step(om, Q, V, np.tile(c, (k, 1)), np.tile(w, (k, 1)), xfrc32, nsub=nsub)
+    assert rc == 0
+    eq = np.abs(oq - gq).max(axis=1)
+    ev = np.abs(ov - gv).max(axis=1) / scale
+    i = int(np.argmin(eq + 1e-3 * ev))
+    return eq[i], ev[i]
+
+
+# Full-size check on the bench's own state mix (BASELINE config 3).  A state outside the
+# tight bound must equal one of the oracle's runs from fp32-rounding perturbations of it
+# (_nearest_perturbed); measured round 4: 207 of 4096 states outside the tight bound, all
+# contact ties of this kind once MPR's zero test matched the oracle's (dx_step.hip fzero).
+FULL_BATCH_UNEXPLAINED = 0
+
+
+def test_full_batch_parity(gpu, oracle_mod):
+    """BASELINE config 3 at full size, on the bench's own state mix: 4096 reorient envs
+    after 40 control steps of the random agent (auto-resets, falls, deep contact-rich
+    grasps, the overflow tier included).  Every env's fp32 state then takes one physics
+    step on the GPU and in the fp64 oracle (OpenMP over envs): qpos within 1e-6 and qvel
+    within 5e-4 of max(1, |qacc_smooth|) of the oracle -- or, for a state at one of MPR's
+    discontinuities, of one of the oracle's runs from the state perturbed at fp32
+    resolution (_nearest_perturbed).  Replaces the finiteness-only full-batch check."""
     from dexterity_amd import manipulation
 
-    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=4096)
+    n = 4096
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=n)
     env.reset()
     for step in range(40):
-        env.step(env.sample_actions(step), device_action=True)
+        env.step_random(step)
     ts = env.timestep()
     for k, v in ts.observation.items():
         assert np.all(np.isfinite(v)), k
     assert np.all(np.isfinite(ts.reward))
-    ncon = env.physics.get(_lib.NCON)[:, 0]
-    assert (ncon > 0).mean() > 0.5
     assert env.physics.debug_get("queue_timeouts")[0] == 0
+    ph = env.physics
+    qpos, qvel = ph.qpos, ph.qvel
+    ws, ctrl = ph.get(_lib.QACC_WARMSTART), ph.get(_lib.CTRL)
+    ncon = ph.get(_lib.NCON)[:, 0]
+    assert (ncon > 0).mean() > 0.5
+    xfrc = env.task.gravity_compensation
+    model = env.model
     env.close()
+    # the GPU: one physics step from exactly these states (and the forward pass's
+    # qacc_smooth, the error scale)
+    phys = gpu.BatchedPhysics(model, n)
+    phys.set_xfrc(xfrc)
+    for f, v in ((_lib.QPOS, qpos), (_lib.QVEL, qvel), (_lib.QACC_WARMSTART, ws), (_lib.CTRL, ctrl)):
+        phys.set(f, v)
+    phys.debug(True)
+    phys.forward()
+    scale = np.maximum(1.0, np.abs(phys.debug_get("qacc_smooth")).max(axis=1))
+    for f, v in ((_lib.QPOS, qpos), (_lib.QVEL, qvel), (_lib.QACC_WARMSTART, ws)):
+        phys.set(f, v)
+    phys.debug(False)
+    phys.step(1)
+    gq, gv = phys.qpos, phys.qvel
+    phys.close()
+    # the oracle from the same fp32 states
+    om = oracle_mod.OracleModel(model.blob)
+    x32 = np.asarray(xfrc, dtype=np.float32).astype(np.float64).ravel()
+    rc, oq, ov, _ = oracle_mod.batch_step(om, qpos.astype(np.float64), qvel.astype(np.float64),
+                                          ctrl.astype(np.float64), ws.astype(np.float64), x32, nsub=1)
+    assert rc == 0
+    eq = np.abs(gq - oq).max(axis=1)
+    ev = np.abs(gv - ov).max(axis=1) / scale
+    tight = (eq <= 1e-6) & (ev <= 5e-4)
+    unexplained = []
+    for e in np.flatnonzero(~tight):
+        pq, pv = _nearest_perturbed(oracle_mod, om, x32, (qpos[e], qvel[e], ws[e], ctrl[e]), 1, gq[e], gv[e],
+                                    scale[e])
+        if not (pq <= 1e-6 and pv <= 5e-4):
+            unexplained.append((int(e), float(eq[e]), float(pq), float(pv)))
+    print(f"full batch: {(~tight).sum()} of {n} states outside the tight bound (max qpos err {eq.max():.2e}, "
+          f"max qvel err / scale {ev.max():.2e}; tight set {eq[tight].max():.2e} / {ev[tight].max():.2e}); "
+          f"{(~tight).sum() - len(unexplained)} equal an oracle run from a perturbed state; unexplained "
+          f"{unexplained[:10]}")
+    assert (~tight).mean() <= 0.1
+    assert len(unexplained) <= FULL_BATCH_UNEXPLAINED
 
 
 def test_ground_contact_watch_matches_oracle(gpu, oracle_mod, reorient_setup):
@@ -787,6 +864,12 @@ def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):
                 sc = max(1.0, np.abs(d.qacc_smooth).max())
                 q, v = np.abs(qpos[e] - d.qpos).max(), np.abs(qvel[e] - d.qvel).max() / sc
                 best = (q, v) if best is None or q < best[0] else best
+            if best[0] > CG_QPOS_MAX * nsub or best[1] > CG_QVEL_MAX:
+                # a contact tie along the way (MPR's discontinuities): the nearest of the
+                # oracle's runs from fp32-resolution perturbations of the state
+                pq, pv = _nearest_perturbed(oracle_mod, om_d, np.asarray(xfrc, dtype=np.float32).astype(np.float64).ravel(),
+                                            _f32(st), nsub, qpos[e], qvel[e], sc)
+                best = min(best, (pq, pv))
             eq.append(best[0])
             ev.append(best[1])
         eq, ev = np.array(eq), np.array(ev)

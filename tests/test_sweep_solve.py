@@ -75,3 +75,42 @@ def test_sweep_matches_cholesky_on_newton_hessians(nefc):
         worse.append(err_s / max(err_c, 1e-12))
         assert err_s < max(1e-4, 10 * err_c)
     assert np.median(worse) < 4.0
+
+
+def sweep_inverse(A, dtype=np.float32):
+    """dx_device.h mfma_sweep_inverse30: every pivot pair swept with its whole rows and
+    columns zeroed first; the result is -A^-1."""
+    n = len(A)
+    S = np.eye(32, dtype=dtype)
+    S[:n, :n] = A
+    for k in range(0, 30, 2):
+        if k >= n:
+            break
+        p00, p10, p11 = S[k, k], S[k + 1, k], S[k + 1, k + 1]
+        idet = dtype(1) / (p00 * p11 - p10 * p10)
+        W = np.array([[p11 * idet, -p10 * idet], [-p10 * idet, p00 * idet]], dtype=dtype)
+        V = S[:, [k, k + 1]].copy()
+        V[k] = [-1, 0]
+        V[k + 1] = [0, -1]
+        S[[k, k + 1], :] = 0
+        S[:, [k, k + 1]] = 0
+        S = (S - V @ (W @ V.T)).astype(dtype)
+    return -S[:n, :n]
+
+
+@pytest.mark.parametrize("n", [2, 7, 24, 30])
+def test_sweep_inverse_of_mass_matrices(n):
+    """The CG solver's M^-1 (one sweep per solve, then a product per iteration) equals
+    the inverse, and M^-1 g agrees with the sweep solve of the same system in fp32."""
+    rng = np.random.default_rng(200 + n)
+    for _ in range(20):
+        M = hessian_like(rng, n, 0, 0.0)
+        Mi = sweep_inverse(M.astype(np.float32)).astype(np.float64)
+        ref = np.linalg.inv(M)
+        assert np.abs(Mi - ref).max() <= 1e-4 * np.abs(ref).max()
+        assert np.abs(Mi - Mi.T).max() <= 1e-5 * np.abs(ref).max()
+        g = rng.standard_normal(n)
+        x = (Mi.astype(np.float32) @ g.astype(np.float32)).astype(np.float64)
+        xs = sweep_solve(M.astype(np.float32), g.astype(np.float32)).astype(np.float64)
+        xr = np.linalg.solve(M, g)
+        assert np.abs(x - xr).max() <= max(3 * np.abs(xs - xr).max(), 1e-5 * np.abs(xr).max())
