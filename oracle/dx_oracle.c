@@ -203,6 +203,8 @@ struct dxo_data {
   int niter;
   double flops[DXO_NSTAGE];
   const dxo_model* model;
+  int ncon_fixed;      /* test helper dxo_set_contacts: < 0 = run the narrowphase */
+  double* con_fixed;   /* [ncon_fixed][16] records in dxo_contact's layout */
 };
 
 dxo_data* dxo_data_create(const dxo_model* m) {
@@ -242,6 +244,8 @@ dxo_data* dxo_data_create(const dxo_model* m) {
   d->tmp1 = calloc(nt * 6, 8); d->tmp2 = calloc(nt * 6, 8); d->tmp3 = calloc(nt * 6, 8);
   d->tmp4 = calloc(nt * 6, 8); d->tmp5 = calloc(nt * 6, 8);
   d->mcom = calloc(3 * nb, 8); d->msum = calloc(nb, 8);
+  d->ncon_fixed = -1;
+  d->con_fixed = calloc(16 * NCON_MAX, 8);
   dxo_reset(m, d);
   return d;
 }
@@ -258,7 +262,8 @@ void dxo_data_free(dxo_data* d) {
                   d->contact, d->efc_type, d->efc_id, d->efc_state, d->efc_J, d->efc_pos,
                   d->efc_margin, d->efc_floss, d->efc_diag, d->efc_R, d->efc_D, d->efc_K,
                   d->efc_B, d->efc_imp, d->efc_vel, d->efc_aref, d->efc_jar, d->efc_force,
-                  d->efc_jv, d->tmp1, d->tmp2, d->tmp3, d->tmp4, d->tmp5, d->mcom, d->msum};
+                  d->efc_jv, d->tmp1, d->tmp2, d->tmp3, d->tmp4, d->tmp5, d->mcom, d->msum,
+                  d->con_fixed};
   for (size_t i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); i++) free(ptrs[i]);
   free(d);
 }
@@ -1192,9 +1197,30 @@ static int sphere_overlap(const double* c1, double r1, const double* c2, double 
   return dot3(t, t) <= rr * rr;
 }
 
+/* Test helper (dxo_set_contacts): the contact list given instead of the narrowphase's --
+ * point, normal, depth and geom pair from each record; frame, condim, friction, solref,
+ * solimp and margin from the pair, as add_contact sets them for a found contact. */
+static void fixed_contacts(const dxo_model* m, dxo_data* d) {
+  for (int i = 0; i < d->ncon_fixed; i++) {
+    const double* r = d->con_fixed + 16 * i;
+    const int g1 = (int)r[13], g2 = (int)r[14];
+    for (int gp = 0; gp < m->ngpair; gp++)
+      if (m->gpair_geom[2 * gp] == g1 && m->gpair_geom[2 * gp + 1] == g2) {
+        double n[3] = {r[3], r[4], r[5]};
+        normalize3(n);
+        add_contact(d, m, gp, g1, g2, r, n, r[12]);
+        break;
+      }
+  }
+}
+
 static void collision(const dxo_model* m, dxo_data* d) {
   d->ncon = 0;
   if (m->disable_contact) return;
+  if (d->ncon_fixed >= 0) {
+    fixed_contacts(m, d);
+    return;
+  }
   for (int bp = 0; bp < m->nbpair; bp++) {
     int b1 = m->bpair_body[2 * bp], b2 = m->bpair_body[2 * bp + 1];
     const double* s1 = m->bpair_sphere + 8 * bp;
@@ -1950,6 +1976,26 @@ double* dxo_field(dxo_data* d, const char* name, int* len) {
 #undef F
   if (len) *len = 0;
   return NULL;
+}
+
+/* Test helper: the solver's scaled primal cost scale * f(qacc) (the quantity whose
+ * improvement solve_newton compares with the tolerance) of the constraint problem the
+ * last dxo_forward built, at an arbitrary qacc -- how optimal another solver's
+ * acceleration is in this problem.  Overwrites efc_force / efc_state / efc_jar. */
+double dxo_solver_cost(const dxo_model* m, dxo_data* d, const double* qacc) {
+  const double scale = 1.0 / (m->meaninertia * (m->nv > 1 ? m->nv : 1));
+  return scale * eval_cost(m, d, qacc, d->tmp1);
+}
+
+/* Test helper: every later collision pass of d yields these n contacts (records in
+ * dxo_contact's layout: pos, frame -- only its normal row is read -- dist, geom1, geom2,
+ * condim) instead of running the narrowphase; n < 0 restores the narrowphase.  Lets a
+ * test run the oracle's dynamics on another implementation's contact list. */
+int dxo_set_contacts(dxo_data* d, int n, const double* recs) {
+  if (n > NCON_MAX) return -1;
+  d->ncon_fixed = n;
+  if (n > 0) memcpy(d->con_fixed, recs, sizeof(double) * 16 * (size_t)n);
+  return 0;
 }
 
 int dxo_ncon(const dxo_data* d) { return d->ncon; }

@@ -87,6 +87,8 @@ int dxo_ncon(const dxo_data* d);
 void dxo_contact(const dxo_data* d, int i, double out[16]);
 int dxo_nefc(const dxo_data* d);
 int dxo_solver_niter(const dxo_data* d);
+double dxo_solver_cost(const dxo_model* m, dxo_data* d, const double* qacc);
+int dxo_set_contacts(dxo_data* d, int n, const double* recs);
 void dxo_flops(const dxo_data* d, double out[DXO_NSTAGE]);
 void dxo_flops_reset(dxo_data* d);
 

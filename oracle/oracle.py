@@ -51,6 +51,10 @@ def lib():
         L.dxo_nefc.restype = ip
         L.dxo_solver_niter.argtypes = [vp]
         L.dxo_solver_niter.restype = ip
+        L.dxo_solver_cost.argtypes = [vp, vp, dp]
+        L.dxo_solver_cost.restype = ctypes.c_double
+        L.dxo_set_contacts.argtypes = [vp, ip, dp]
+        L.dxo_set_contacts.restype = ip
         L.dxo_contact.argtypes = [vp, ip, dp]
         L.dxo_flops.argtypes = [vp, dp]
         L.dxo_flops_reset.argtypes = [vp]
@@ -134,6 +138,22 @@ class OracleData:
     @property
     def niter(self) -> int:
         return lib().dxo_solver_niter(self.ptr)
+
+    def set_contacts(self, recs):
+        """Every later collision pass yields these contacts ([n][16] records in
+        `contacts()`'s layout) instead of the narrowphase's; None restores it."""
+        if recs is None:
+            lib().dxo_set_contacts(self.ptr, -1, None)
+            return
+        r = np.ascontiguousarray(recs, dtype=np.float64).reshape(-1, 16)
+        self._fixed = r
+        if lib().dxo_set_contacts(self.ptr, len(r), r.ctypes.data_as(ctypes.POINTER(ctypes.c_double))) != 0:
+            raise ValueError("too many contacts")
+
+    def solver_cost(self, qacc) -> float:
+        """Scaled primal cost of the last forward's constraint problem at `qacc`."""
+        q = np.ascontiguousarray(qacc, dtype=np.float64)
+        return lib().dxo_solver_cost(self.model.ptr, self.ptr, q.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
 
     def contacts(self) -> np.ndarray:
         out = np.zeros((self.ncon, 16))
