@@ -89,6 +89,19 @@ def reorient_setup(gpu, oracle_mod):
     return cm, xfrc, om, states, model
 
 
+def _qacc_on_gpu_contacts(oracle_mod, om, xfrc, st, recs):
+    """The oracle's constrained qacc at the state the GPU holds (`_f32`) with the GPU's
+    contact list `recs` in place of its own narrowphase (dxo_set_contacts): what a tie
+    state's accelerations must equal if the tie (MPR's choice of point or normal) is the
+    whole difference."""
+    d = oracle_mod.OracleData(om)
+    d.xfrc_applied[:] = np.asarray(xfrc, dtype=np.float32).astype(np.float64).ravel()
+    d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = _f32(st)
+    d.set_contacts(np.asarray(recs, dtype=np.float64))
+    d.forward()
+    return d.qacc.copy()
+
+
 def _geom_points(cm, d, g):
     """World-frame vertices of a box or mesh geom (a mesh collides as the convex hull of
     its vertices) at the oracle state d."""
@@ -201,7 +214,7 @@ def _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
         assert np.abs(a0[e] - d.qacc_smooth).max() <= 1e-5 * scale
         oc = d.contacts()
         n = cnt[e, 0]
-        gc = con[e, : (con[e, :, 13] != 0).sum()]
+        gc = con[e, : (con[e, :, 15] != 0).sum()]
         assert cnt[e, 1] == 0, "overflow flag set"
         assert len(gc) == len(oc)
         ok = {(int(r[13]), int(r[14])): r for r in oc}
@@ -229,6 +242,10 @@ def _check_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
             TIE_ERR.append(float(err.max() / sc))
             assert err[: cm.nv - 6].max() <= TIE_QACC_HAND * sc, (f"tie env {e}", err.max() / sc)
             assert err[cm.nv - 6 :].max() <= TIE_QACC_CUBE * sc, (f"tie env {e}", err.max() / sc)
+            # and the tie is the whole difference: on the GPU's own contacts the oracle's
+            # accelerations equal the GPU's within the tight bound
+            fix = np.abs(qacc[e] - _qacc_on_gpu_contacts(oracle_mod, om, xfrc, st, gc))
+            assert fix.max() <= 5e-4 * sc, (f"tie env {e} on the GPU's contacts", fix.max() / sc)
     return ncontact_states, degenerate
 
 
@@ -260,7 +277,7 @@ def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
     skip = set()
     for e, st in enumerate(states):
         ds = _oracle_pair(oracle_mod, om, cm, xfrc, st)
-        for r in con[e, : (con[e, :, 13] != 0).sum()]:
+        for r in con[e, : (con[e, :, 15] != 0).sum()]:
             if _contact_tie(cm, ds, r):
                 skip.add(e)
     probe.close()
@@ -281,6 +298,13 @@ def _check_substep(gpu, oracle_mod, cm, xfrc, om, states, model):
         qt, vt = (TIE_QPOS, TIE_QACC_CUBE) if e in skip else (1e-6, 5e-4)
         if e in skip:
             TIE_STEP_ERR.append(min(errs, key=lambda qv: qv[0]))
+            # on the GPU's own contacts the oracle's step equals the GPU's tightly
+            d = oracle_mod.OracleData(om)
+            d.xfrc_applied[:] = np.asarray(xfrc, dtype=np.float32).astype(np.float64).ravel()
+            d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = _f32(st)
+            d.set_contacts(con[e, : (con[e, :, 15] != 0).sum()].astype(np.float64))
+            d.step()
+            assert np.abs(qpos[e] - d.qpos).max() < 1e-6, (e, "on the GPU's contacts")
         assert any(q < qt and v < vt for q, v in errs), (e, e in skip, errs)
     return skip
 
@@ -841,16 +865,27 @@ def _check_bimanual_forward(gpu, oracle_mod, cm, xfrc, om, states, model):
         scale = np.abs(d.qacc_smooth).max()
         assert np.abs(a0[e] - d.qacc_smooth).max() <= 1e-5 * scale
         oc = d.contacts()
-        gc = con[e, : (con[e, :, 13] != 0).sum()]
+        gc = con[e, : (con[e, :, 15] != 0).sum()]
         assert cnt[e, 1] == 0, "overflow flag set"
         assert {(int(r[13]), int(r[14])) for r in gc} == {(int(r[13]), int(r[14])) for r in oc}
         with_contacts += len(oc) > 0
         tie = sum(_contact_tie(cm, ds, r) for r in gc) > 0
         ties += tie
+        sc = max(1.0, scale)
         if not tie:
             err = np.minimum(np.abs(qacc[e] - ds[0].qacc), np.abs(qacc[e] - ds[1].qacc))
-            assert err[:48].max() <= 5e-4 * max(1.0, scale), f"env {e}"
-            assert err[48:].max() <= 3e-3 * max(1.0, scale), f"env {e}"
+            assert err[:48].max() <= 5e-4 * sc, f"env {e}"
+            assert err[48:].max() <= 3e-3 * sc, f"env {e}"
+        else:
+            # a tie state is not skipped: on the GPU's own contacts the oracle's
+            # accelerations equal the GPU's within the tight bound (the tie is the whole
+            # difference), and the difference itself stays within the tie bounds
+            fix = np.abs(qacc[e] - _qacc_on_gpu_contacts(oracle_mod, om, xfrc, st, gc))
+            assert fix.max() <= 5e-4 * sc, (f"tie env {e} on the GPU's contacts", fix.max() / sc)
+            err = min((np.abs(qacc[e] - dd.qacc) for dd in ds), key=lambda x: x.max())
+            BIMANUAL_TIE_ERR.append(float(err.max() / sc))
+            assert err[:48].max() <= TIE_QACC_HAND * sc, (f"tie env {e}", err.max() / sc)
+            assert err[48:].max() <= TIE_QACC_CUBE * sc, (f"tie env {e}", err.max() / sc)
     phys.close()
     return with_contacts, ties
 
@@ -865,13 +900,21 @@ def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
     assert with_contacts >= 3
 
 
+BIMANUAL_TIE_ERR = []
+
+
 def test_bimanual_forward_parity_wide_sample(gpu, oracle_mod, bimanual_setup):
-    """As above over 12 trajectories (24 states); face ties at most 1 in 6."""
+    """As above over 12 trajectories (24 states).  Tie states are held to the tie bounds
+    and, on the GPU's own contacts, to the tight bound (_check_bimanual_forward); at most
+    1 of the 24 (measured round 4: none)."""
     cm, xfrc, _, _, model = bimanual_setup
     om, states = _bimanual_states(oracle_mod, cm, xfrc, n_traj=12, seed=11)
+    BIMANUAL_TIE_ERR.clear()
     with_contacts, ties = _check_bimanual_forward(gpu, oracle_mod, cm, xfrc, om, states, model)
+    print(f"bimanual wide sample: {with_contacts} of {len(states)} states in contact, {ties} tie states, "
+          f"their qacc errors / scale {BIMANUAL_TIE_ERR}")
     assert with_contacts >= 15
-    assert ties <= len(states) // 6
+    assert ties <= 1
 
 
 def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):

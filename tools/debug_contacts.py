@@ -17,7 +17,7 @@ con = phys.debug_get("contact"); qacc = phys.qacc
 for e, st in enumerate(states):
     d = _oracle_forward(O, om, cm, xfrc, st)
     oc = {(int(r[13]), int(r[14])): r for r in d.contacts()}
-    gc = con[e, : (con[e, :, 13] != 0).sum()]
+    gc = con[e, : (con[e, :, 15] != 0).sum()]
     print(f"env {e}: ncon gpu {len(gc)} oracle {len(oc)}  qacc err {np.abs(qacc[e]-d.qacc).max():.2e}")
     for r in gc:
         o = oc.get((int(r[13]), int(r[14])))

@@ -40,7 +40,7 @@ def main():
         d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
         oc = {(int(r[13]), int(r[14])): r for r in d.contacts()}
         worst = 0.0
-        for r in con[e, : (con[e, :, 13] != 0).sum()]:
+        for r in con[e, : (con[e, :, 15] != 0).sum()]:
             key = (int(r[13]), int(r[14]))
             o = oc.get(key)
             if o is None:
