@@ -66,6 +66,8 @@ def _units() -> list:
     units += [(f"dx_step_{n}", "dx_step.hip", (f"-DDX_SPEC_ONLY={n}",)) for n in _spec_names()]
     # the overflow tier: the step kernel's physics with the DX_NCON_HI contact pool
     units.append(("dx_step_hi", "dx_step.hip", ("-DDX_TIER_HI", "-DDX_NCON_MAX=DX_NCON_HI")))
+    # the mid tier: the same physics with the DX_NCON_MID pool, beside queued launches
+    units.append(("dx_step_mid", "dx_step.hip", ("-DDX_TIER_MID", "-DDX_NCON_MAX=DX_NCON_MID")))
     return units
 
 

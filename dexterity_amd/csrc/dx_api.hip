@@ -81,6 +81,7 @@ struct dx_model {
   std::map<int, const DevModel*> dev_model_ptrs;  // device copy of dev_models[device]
   Lds lds;     // the step kernel's per-env LDS layout (contact pool DX_NCON_MAX)
   Lds lds_hi;  // the overflow tier's (DX_NCON_HI)
+  Lds lds_mid; // the mid tier's (DX_NCON_MID; nefc_max 0: not available for this model)
   int ncon_max, nefc_max;
 };
 
@@ -716,6 +717,8 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   // the step kernel's layout (pool DX_NCON_MAX) and the overflow tier's (DX_NCON_HI)
   layout(DX_NCON_MAX, m->lds);
   layout(DX_NCON_HI, m->lds_hi);
+  layout(DX_NCON_MID, m->lds_mid);
+  if (m->lds_mid.nefc_max > 5 * 64) m->lds_mid.nefc_max = 0;  // (its line search keeps 5 register slots)
   m->ncon_max = DX_NCON_HI;
   m->nefc_max = m->lds_hi.nefc_max;
   // line-search register slots (dx_step.hip DX_LS_SLOTS: 5 in the step kernel, 20 in the
@@ -931,6 +934,11 @@ struct dx_batch {
   float* sensor = nullptr;  // DX_SENSOR_TORQUE [nenv][nbody][3] (allocated by dx_sensor_enable)
   float* sen_stash = nullptr;
   unsigned* ncon_hist = nullptr;  // dx_ncon_histogram
+  // the mid tier beside queued launches (dx_step.hip dx_step_mid_kernel): its stream, the
+  // queued workgroups' exit count it waits for (DevBatch::qdone[0]) and its launch count
+  bool mid = false;
+  hipStream_t side = nullptr;
+  unsigned qdone_target = 0, mid_epoch = 0;
 };
 
 #define DX_HI_GRID 32  // workgroups of the overflow tier (each loops over the deferred steps)
@@ -1012,6 +1020,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
   B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
   B.defer_at = getenv("DX_DEFER_AT") ? atoi(getenv("DX_DEFER_AT")) : DX_NCON_MAX;  // (tests / probes)
+  B.order_last = getenv("DX_ORDER_LAST") ? atoi(getenv("DX_ORDER_LAST")) : 0;
   b->hi_grid = getenv("DX_HI_GRID") ? std::max(1, atoi(getenv("DX_HI_GRID"))) : DX_HI_GRID;
   {
     int ncu = 0;
@@ -1023,6 +1032,19 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
     int per = dx_step_occupancy(b->spec, lds);
     if (per < 1) per = (int)std::max<size_t>(1, std::min<size_t>(8, 163840 / lds));
     b->slots = ncu * per;
+    // the mid tier: its workgroup fits a CU that holds one step-kernel workgroup fewer
+    // (LDS in 512-B granules; its VGPRs fit the SIMD that then runs one wave)
+    auto g512 = [](size_t x) { return (x + 511) / 512 * 512; };
+    const size_t lmid = (size_t)m->lds_mid.total * 4;
+    b->mid = b->queue && B.defer && m->lds_mid.nefc_max > 0 && !getenv("DX_NO_MID") && per >= 2 &&
+             (size_t)(per - 1) * g512(lds) + g512(lmid) <= 163840;
+  }
+  if (b->mid) {
+    rc |= balloc(b, (void**)&B.defer2, (E + 2) * 4);
+    rc |= balloc(b, (void**)&B.qdone, 2 * 4);
+    B.mid_defer_at = getenv("DX_MID_DEFER_AT") ? atoi(getenv("DX_MID_DEFER_AT")) : DX_NCON_MID;  // (tests)
+    if (hipStreamCreateWithFlags(&b->side, hipStreamNonBlocking) != hipSuccess)
+      rc |= fail(DX_EHIP, "mid-tier stream creation failed");
   }
   if (rc) { dx_batch_destroy(b); return nullptr; }
   B.xfrc = nullptr;  // enabled by dx_set_xfrc
@@ -1035,6 +1057,13 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   B.watch_body = -1;
   B.out_bodies = 1;
   if (dx_reset(b, 0, nenv) != 0) { dx_batch_destroy(b); return nullptr; }
+  // the mid tier's stream is ordered after nothing on the batch stream: its first launch
+  // must not read the deferral list or the exit counts before their zeroing above
+  if (b->mid && hipStreamSynchronize(b->stream) != hipSuccess) {
+    fail(DX_EHIP, "stream sync failed");
+    dx_batch_destroy(b);
+    return nullptr;
+  }
   return b;
 }
 
@@ -1042,7 +1071,9 @@ extern "C" void dx_batch_destroy(dx_batch* b) {
   if (!b) return;
   (void)hipSetDevice(b->device);
   (void)hipStreamSynchronize(b->stream);
+  if (b->side) (void)hipStreamSynchronize(b->side);
   for (void* p : b->allocs) (void)hipFree(p);
+  if (b->side) (void)hipStreamDestroy(b->side);
   (void)hipStreamDestroy(b->stream);
   delete b;
 }
@@ -1195,7 +1226,9 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   DevBatch& Bo = b->db;
   Bo.onext = (mode == 0 && Bo.order && Bo.defer) ? 1 : 0;
   if (Bo.onext) Bo.opar ^= 1;
-  const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots) : b->nenv;
+  // a queued launch with the mid tier beside it leaves one workgroup slot for it
+  const bool mid = queued && b->mid;
+  const int grid = queued ? (int)std::min<long>((long)b->nenv * nsub, b->slots - (mid ? 1 : 0)) : b->nenv;
   if (queued) {
     // substep queue: a new progress epoch and zeroed task counters
     DevBatch& B = b->db;
@@ -1206,11 +1239,23 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
     if (!b->qhead_zero) HIPCHK(hipMemsetAsync(B.qhead, 0, DX_QUEUES * DX_QHEAD_STRIDE * 4, b->stream));
     b->qhead_zero = false;
   }
+  Bo.mid = mid ? 1 : 0;
+  if (mid) Bo.mid_epoch = ++b->mid_epoch;
   hipEvent_t t0;
   timing_begin(b, &t0);
   hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);
   timing_end(b, t0);
   HIPCHK(e);
+  // the mid tier, on its own stream, with no stream event in between (dx_step.hip
+  // dx_step_mid_kernel: it waits on the device for this launch's workgroups to exit, and
+  // the overflow tier below waits for it).  It is submitted after the step kernel: should
+  // the two streams share a hardware queue it then runs after the step kernel instead of
+  // ahead of it -- the mid tier waits for the step kernel, never the other way round.
+  if (mid) {
+    b->qdone_target += (unsigned)grid;
+    HIPCHK(dx_launch_step_mid(1, (size_t)b->model->lds_mid.total * 4, b->side, b->dm_dev, b->db, b->model->lds_mid,
+                              nsub, b->qdone_target));
+  }
   // the overflow tier: physics steps whose contacts did not fit the step kernel's pool
   // (nothing to do unless some env deferred one), the next launch's longest-first order,
   // and the queue heads zeroed for the next launch
@@ -1219,6 +1264,7 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
                              b->model->lds_hi, nsub));
     b->qhead_zero = true;
   }
+  Bo.mid = 0;
   // torque sensors from the last substep's stash (mode 0 step, mode 1 forward)
   if (b->db.sen_stash && mode != 2)
     HIPCHK(dx_launch_sensor(b->nenv, ((size_t)b->model->lds.total + 6 * DX_MAX_NV) * 4, b->stream, b->dm_dev, b->db,

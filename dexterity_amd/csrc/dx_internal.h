@@ -14,6 +14,11 @@
 // DX_NCON_HI = 256, above the reference scenes' nconmax 200, shadow_hand_series_e.xml:8).
 // A pool that still overflows keeps its first contacts in candidate (generation) order.
 #define DX_NCON_HI 256
+// The mid tier (-DDX_TIER_MID, pool DX_NCON_MID) runs beside a queued step-kernel launch, in
+// the LDS one step-kernel workgroup leaves free on a CU, and takes the deferred physics
+// steps as they are published (dx_step.hip dx_step_mid_kernel); a step beyond its pool
+// goes on to the overflow tier after the launch.
+#define DX_NCON_MID 64
 #ifndef DX_NCON_MAX
 #define DX_NCON_MAX 32    // contacts kept per env per substep by this translation unit
 #endif
@@ -177,7 +182,16 @@ struct DevBatch {
   // << 24 | forward-only << 30, appended by the step kernel, emptied by the overflow
   // kernel's last workgroup
   unsigned* defer;
+  // with the mid tier running beside a queued launch (mid = 1): the step kernel publishes
+  // each deferral (state in the env's hand-off record, entry | DX_DEFER_VALID stored after
+  // it), its workgroups count themselves in qdone[0] as they exit, and the mid tier's own
+  // deferrals go to defer2 (same layout, batch arrays) for the overflow tier
+  unsigned* defer2;
+  unsigned* qdone;  // [0] exits of queued workgroups (never reset), [1] the last mid launch that finished
+  int mid, mid_defer_at;
+  unsigned mid_epoch;  // this launch's number among the mid tier's launches
   int defer_at;  // defer a physics step with more contacts than this (DX_NCON_MAX; DX_DEFER_AT for tests)
+  int order_last;  // longest-first key from the control step's last physics step (x nsub), not its sum
   // Task logic fused into the step kernel (dx_task.h; DevBatch::tp / ts): task_pre in the
   // env's first physics-step task, with ctrl = the action (`action`, [nenv][nu], or drawn
   // in the kernel by the random agent when act_random: dx_urand(act_seed, env0 + env,
@@ -195,6 +209,7 @@ struct DevBatch {
   int opar, onext;
 };
 #define DX_DEFER_FWD (1u << 30)
+#define DX_DEFER_VALID (1u << 31)  // a published entry (mid tier: consumed entries are zeroed)
 #define DX_HEALTH_WORDS 16
 #define DX_NCON_HIST 65   // bins 0..63, and >= 64
 #define DX_MAXVAL 1e10f   // mjMAXVAL: |qacc| beyond this is a diverged state (mj_checkAcc)
@@ -368,6 +383,10 @@ hipError_t dx_launch_order(int nenv, hipStream_t stream, const unsigned* cost, i
 // the overflow tier (dx_step.hip, DX_TIER_HI): the physics steps deferred by the last launch
 hipError_t dx_launch_step_hi(int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                              const Lds& L, int nsub);
+// the mid tier (dx_step.hip, DX_TIER_MID): beside the queued launch after which qdone[0]
+// reaches `target`
+hipError_t dx_launch_step_mid(int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
+                              const Lds& L, int nsub, unsigned target);
 
 // dx_sensor.hip: joint torque sensors from the step kernel's stash (host side)
 hipError_t dx_launch_sensor(int nenv, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,

@@ -3344,19 +3344,37 @@ __device__ __forceinline__ void order_key(const DevBatch& B, int env, unsigned c
 // arrays, the env to the deferral list (substep s; forward-only for a dx_forward), its
 // cost to the top bucket of the next launch's longest-first order, and the count of
 // deferrals to the health counters.  Nothing of the env is written after this.
+// With the mid tier running beside the launch (B.mid, queued mode 0 only) the deferral is
+// published while the launch runs: the state goes write-through (sc1) into the env's
+// hand-off record, vmcnt drains, and only then is the entry stored (relaxed, agent scope,
+// DX_DEFER_VALID set) -- the queue's own hand-off protocol.  `list` is the deferral list:
+// B.defer from the step kernel, B.defer2 from the mid tier (the health count of deferrals
+// counts the step kernel's only).
 template <class Ctx>
-__device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int env, int s, bool fwd, float time) {
-  env_store_state(c, B, env, rl(time, 0));
+__device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int env, int s, bool fwd, float time,
+                                          unsigned* list = nullptr) {
+  const bool publish = B.mid && list == nullptr;
+  if (!list) list = B.defer;
+  const unsigned val = (unsigned)env | ((unsigned)s << 24) | (fwd ? DX_DEFER_FWD : 0u);
+  if (publish) {
+    env_store_hand(c, B.hand + (size_t)env * B.hand_stride, B.hand_stride, time, 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    env_store_state(c, B, env, rl(time, 0));
+  }
   if (LANE == 0) {
-    const unsigned k = atomicAdd(B.defer, 1u);
-    B.defer[2 + k] = (unsigned)env | ((unsigned)s << 24) | (fwd ? DX_DEFER_FWD : 0u);
+    const unsigned k = atomicAdd(list, 1u);
+    if (publish)
+      __hip_atomic_store(list + 2 + k, val | DX_DEFER_VALID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      list[2 + k] = val;
     if (B.cost) B.cost[env] = 0xffffffffu;
     if (B.health) {
-      atomicAdd(B.health + 6, 1u);
+      if (list == B.defer) atomicAdd(B.health + 6, 1u);
       atomicMax(B.health + 5, (unsigned)c.I[I_NRAW]);
     }
   }
-  if (!fwd) order_key(B, env, 0xffffffffu);
+  if (!fwd && list == B.defer) order_key(B, env, 0xffffffffu);
 }
 
 // Fused task_pre (DevBatch::fuse) in the env's first physics-step task: before_step /
@@ -3551,12 +3569,16 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       continue;
     }
     const bool last = s == nsub - 1 || (skip && B.fuse);  // (a fresh reset is observed right away)
-    const unsigned cost = cost0 + (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+    const unsigned tcost = (unsigned)min((__builtin_amdgcn_s_memtime() - t_start) >> 10, 0xffffffffull);
+    const unsigned cost = cost0 + tcost;
     if (last) {
       env_finish(c, B, env, time);
       if (LANE == 0 && B.cost) B.cost[env] = cost;
       if (B.fuse) fused_post(c, B, env, skip);
-      order_key(B, env, cost);
+      // the next launch's longest-first key: this control step's cost, or (DX_ORDER_LAST 1)
+      // its last physics step's x nsub, or (2) the mean of the two
+      const unsigned lcost = tcost * (unsigned)nsub;
+      order_key(B, env, skip || !B.order_last ? cost : B.order_last == 1 ? lcost : (cost >> 1) + (lcost >> 1));
     } else {
       env_store_hand(c, rec, B.hand_stride, time, cost);
     }
@@ -3575,6 +3597,9 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       __hip_atomic_store(B.progress + env, qtag(B.epoch, last && s < nsub - 1 ? DX_TAG_DONE : s + 1), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
   }
+  // the mid tier's end-of-launch signal: every deferral of this workgroup was published
+  // (its count atomic returned before the entry store) before this count
+  if (B.mid && LANE == 0) __hip_atomic_fetch_add(B.qdone, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ------------------------------------------------------------------------ //
@@ -3584,7 +3609,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
 // (that translation unit holds only that scene's kernel and its launcher), and once
 // without it (generic kernel, dispatch, helper kernels), so the kernels compile in
 // parallel.
-#if __has_include("dx_specs.inc") && !defined(DX_TIER_HI)
+#if __has_include("dx_specs.inc") && !defined(DX_TIER_HI) && !defined(DX_TIER_MID)
 #include "dx_specs.inc"
 #endif
 #ifndef DX_SPECS
@@ -3664,10 +3689,24 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
       if (e < e1) ((int*)B.order)[p + (key & 0xffffu)] = e;
     }
   }
-  // 2. the deferred physics steps
-  const unsigned n = B.defer ? B.defer[0] : 0u;
+  // 2. the deferred physics steps (beside a mid-tier launch: those beyond its pool, once
+  // the mid tier has finished)
+  if (B.mid) {
+    int ok = 1;
+    if (LANE == 0) {
+      for (unsigned w = 0; (int)(__hip_atomic_load(B.qdone + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - B.mid_epoch) < 0; w++) {
+        __builtin_amdgcn_s_sleep(4);
+        if (w > (1u << 25)) { __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); ok = 0; break; }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!__shfl(ok, 0, 64)) return;
+  }
+  unsigned* list = B.mid ? B.defer2 : B.defer;
+  const unsigned n = list ? list[0] : 0u;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
-    const unsigned e = B.defer[2 + i];
+    const unsigned e = list[2 + i];
+    if (LANE == 0) list[2 + i] = 0u;
     const int env = (int)(e & 0xffffffu), s0 = (int)((e >> 24) & 63u);
     CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
     c.I = (int*)(smem + c.L.ints);
@@ -3693,7 +3732,8 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
   }
   if (__shfl(last, 0, 64)) {
     __threadfence();
-    if (B.defer && LANE < 2) B.defer[LANE] = 0u;          // the deferral list
+    if (B.defer && LANE < 2) B.defer[LANE] = 0u;          // the deferral lists
+    if (B.defer2 && LANE < 2) B.defer2[LANE] = 0u;
     if (B.onext)                                           // this launch's cost histogram
 #pragma unroll
       for (int k = 0; k < 4; k++) B.ohist[256 * B.opar + 4 * LANE + k] = 0u;
@@ -3710,6 +3750,85 @@ hipError_t dx_launch_step_hi(int grid, size_t lds, hipStream_t stream, const Dev
     attr = true;
   }
   hipLaunchKernelGGL(dx_step_hi_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub);
+  return hipGetLastError();
+}
+#elif defined(DX_TIER_MID)
+// ------------------------------------------------------------------------ //
+// mid tier (build.py compiles this file once more with -DDX_TIER_MID
+// -DDX_NCON_MAX=DX_NCON_MID): launched on a side stream beside a queued step-kernel launch
+// of nslot workgroups (one slot short of the chip's, so one CU keeps room for this
+// workgroup's LDS), it takes the physics steps the step kernel defers while that launch
+// runs -- instead of after it, on an otherwise idle chip -- and runs each deferred env
+// from its hand-off record to the end of its control step with the DX_NCON_MID pool, with
+// the step kernel's outputs and task logic.  A physics step beyond this pool goes on to
+// the overflow tier's list (B.defer2).  Entries are consumed in order (workgroup w takes
+// entries w, w + grid, ...); consumed entries are zeroed, so a published entry is always
+// this launch's.  The launch's end is its workgroups' exit count (B.qdone[0], never reset)
+// reaching `target`; after it the count is this launch's (the overflow tier that reset it
+// ran before this launch on the batch stream) and every entry below it is taken.  No
+// stream event joins the two streams: the mid tier stores its launch number in
+// B.qdone[1] when it exits (release), and the overflow tier that follows the step kernel
+// waits for it (acquire).  The waits are bounded (B.qerr).
+// ------------------------------------------------------------------------ //
+static_assert(DX_NCON_MAX == DX_NCON_MID, "the mid tier is compiled with the DX_NCON_MID pool");
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
+dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, unsigned target) {
+  extern __shared__ float smem[];
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  for (unsigned i = blockIdx.x;; i += gridDim.x) {
+    unsigned e = 0;
+    int got = 0;
+    if (LANE == 0) {
+      for (unsigned n = 0;; n++) {
+        const bool done = (int)(__hip_atomic_load(B.qdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned cnt = __hip_atomic_load(B.defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i < cnt) {
+          e = __hip_atomic_load(B.defer + 2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (e & DX_DEFER_VALID) { got = 1; break; }
+        } else if (done) {
+          break;  // the launch is over and every deferral below cnt was taken
+        }
+        __builtin_amdgcn_s_sleep(4);
+        if (++n > (1u << 25) || ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    if (!__shfl(got, 0, 64)) break;
+    e = __shfl(e, 0, 64);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (LANE == 0) B.defer[2 + i] = 0u;  // consumed (the next launch's entries start unpublished)
+    const int env = (int)(e & 0xffffffu), s0 = (int)((e >> 24) & 63u);
+    CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
+    c.I = (int*)(smem + c.L.ints);
+    c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
+    c.np_wide = B.np_wide;
+    c.defer = true;
+    c.defer_at = B.mid_defer_at;
+    const float* rec = B.hand + (size_t)env * B.hand_stride;
+    float time = env_begin(c, B, env, rec, true);
+    int s = s0;
+    for (; s < nsub; s++) {
+      env_substep(c, B, time, env, s == nsub - 1);
+      if (c.I[I_DEFER]) break;
+    }
+    if (s < nsub) {
+      env_defer(c, B, env, s, false, time, B.defer2);
+    } else {
+      env_finish(c, B, env, time);
+      if (B.fuse) fused_post(c, B, env, false);
+    }
+  }
+  // finished: every store above before the overflow tier's wait sees this launch's number
+  if (LANE == 0) __hip_atomic_store(B.qdone + 1, B.mid_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+hipError_t dx_launch_step_mid(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B,
+                              const Lds& L, int nsub, unsigned target) {
+  hipLaunchKernelGGL(dx_step_mid_kernel, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, target);
   return hipGetLastError();
 }
 #elif defined(DX_SPEC_ONLY)
@@ -3835,4 +3954,4 @@ extern "C" __global__ void dx_reset_kernel(DevModel m, DevBatch B, int env0, int
     if (B.nstep) B.nstep[env] = 0;
   }
 }
-#endif  // DX_TIER_HI / DX_SPEC_ONLY
+#endif  // DX_TIER_HI / DX_TIER_MID / DX_SPEC_ONLY

@@ -141,6 +141,29 @@ def test_pool_beyond_step_kernel_matches_oracle(oracle_mod, nstep):
     ph.close()
 
 
+def test_steps_beyond_mid_tier_match_oracle(oracle_mod):
+    """A queued physics step with 256 contacts (10 bars of 8 cubes, two lifted) passes the
+    step kernel (32) and the mid tier running beside it (64, dx_step_mid_kernel) and ends
+    in the overflow tier (256): one step and three match the oracle, nothing is cut."""
+    cm = bar_field()
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    q1 = cm.qpos0.copy()
+    q1[7 * 3 + 2] += 0.05
+    q1[7 * 6 + 2] += 0.05
+    rng = np.random.RandomState(3)
+    states = [(q1, rng.uniform(-0.01, 0.01, size=cm.nv)) for _ in range(3)]
+    for nstep in (1, 3):
+        ph = _run(None, cm, states, nstep)
+        h = ph.health()
+        assert h["contact_overflow"] == 0 and h["diverged"] == 0 and h["contact_deferred"] >= 3, h
+        qpos, qvel = ph.qpos, ph.qvel
+        for e, (q, v) in enumerate(states):
+            d = _oracle(oracle_mod, om, q, v, nstep)
+            np.testing.assert_allclose(qpos[e], d.qpos, atol=1e-6 if nstep == 1 else 1e-5)
+            np.testing.assert_allclose(qvel[e], d.qvel, atol=5e-4 * max(1.0, np.abs(d.qvel).max()))
+        ph.close()
+
+
 def test_pool_cut_keeps_candidate_order(oracle_mod):
     """10 bars of 8 cubes on the ground: 320 contacts, beyond the 256-contact pool.  The
     first 256 in candidate order are kept -- the oracle's list, whose pool (256) fills

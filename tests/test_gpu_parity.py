@@ -745,6 +745,41 @@ def test_narrowphase_group_size_is_invisible(gpu, monkeypatch):
     assert differ.sum() == 0, np.flatnonzero(differ)
 
 
+def test_contact_tiers_are_invisible(gpu, monkeypatch):
+    """Which tier runs a physics step changes nothing: the step kernel with the mid tier
+    beside it (the default: deferred steps run while the launch goes on), without it
+    (DX_NO_MID=1: the overflow tier after the launch), and with every step that has a
+    contact deferred to the mid tier (DX_DEFER_AT=0) give bit-identical trajectories --
+    1024 envs, 12 control steps of random actions, outputs and task logic included."""
+    from dexterity_amd import manipulation
+
+    outs = []
+    for env_vars in ({}, {"DX_NO_MID": "1"}, {"DX_DEFER_AT": "0"}):
+        for k in ("DX_NO_MID", "DX_DEFER_AT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env_vars.items():
+            monkeypatch.setenv(k, v)
+        env = manipulation.load("reorient", "state_dense", seed=5, num_envs=1024)
+        env.reset()
+        for step in range(12):
+            env.step_random(step)
+        ts = env.timestep()
+        h = env.physics.health()
+        outs.append((env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART), ts.reward,
+                     ts.observation["shadow_hand_e/joint_positions"] if "shadow_hand_e/joint_positions" in ts.observation
+                     else next(iter(ts.observation.values()))))
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        assert h["contact_overflow"] == 0 and h["diverged"] == 0
+        if env_vars.get("DX_DEFER_AT") == "0":
+            assert h["contact_deferred"] > 2000, h
+        env.close()
+    for o in outs[1:]:
+        differ = np.zeros(1024, dtype=bool)
+        for a, b in zip(outs[0], o):
+            differ |= (np.asarray(a).reshape(1024, -1) != np.asarray(b).reshape(1024, -1)).any(axis=1)
+        assert differ.sum() == 0, np.flatnonzero(differ)
+
+
 def _check_reach_rewards(env, ts, dense):
     from oracle import task_ref
 
