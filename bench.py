@@ -184,7 +184,8 @@ def main():
 
     def one_step(i):
         # the random agent (manipulation_test.py:44-45), its actions drawn inside the step
-        # kernel: a control step is two launches (step kernel + overflow tier / order)
+        # kernel: a control step is the step kernel, the mid contact tier beside it on a
+        # side stream, and the overflow tier / order launch after it
         env.step_random(i)
         if collator:
             collator.gather()  # enqueued on the env stream behind the step: no host sync
@@ -196,7 +197,9 @@ def main():
     if comm:
         comm.barrier()
     env.physics.health_clear()  # the timed region's own health counters
-    _lib.check(L.dx_timing_enable(env.physics.ptr, 1))
+    # the step kernel's mean launch time: HIP events around every 4th launch of the timed
+    # region (each bracket's two event packets cost ~5 us of the step they sit in)
+    _lib.check(L.dx_timing_enable(env.physics.ptr, 4))
     _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(ctypes.c_double()), ctypes.byref(ctypes.c_int32())))
     t0 = time.perf_counter()
     for i in range(args.steps):

@@ -45,7 +45,7 @@ STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constra
           "qfrc_constraint", "euler", "observe", "io", "matvec", "np_mpr", "jacvec")
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
             26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc",
-            31: "np_trips", 32: "broad_keep", 33: "mid_pairs", 34: "mid_keep"}
+            31: "np_trips", 32: "broad_keep", 33: "mid_pairs", 34: "mid_keep", 35: "queue_wait"}
 NSTAGE = 40
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES, OUT_GOAL_QPOS = range(8)
 TASK_REORIENT, TASK_REACH = 0, 1

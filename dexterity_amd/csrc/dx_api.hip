@@ -1013,6 +1013,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.qhead, DX_QUEUES * DX_QHEAD_STRIDE * 4);
   rc |= balloc(b, (void**)&B.progress, E * 4);
   rc |= balloc(b, (void**)&B.qerr, 8);  // [0] queue timeout, [1] the overflow kernel's finished workgroups
+  if (getenv("DX_QPARK") && atoi(getenv("DX_QPARK"))) rc |= balloc(b, (void**)&B.qpark, (DX_QPARK_SLOTS + 1) * 4);
   B.hand_stride = (d.nq + 2 * d.nv + 4 + 31) / 32 * 32;
   rc |= balloc(b, (void**)&B.hand, E * B.hand_stride * 4);
   B.epoch = 0;
@@ -1020,7 +1021,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
   B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
   B.defer_at = getenv("DX_DEFER_AT") ? atoi(getenv("DX_DEFER_AT")) : DX_NCON_MAX;  // (tests / probes)
-  B.order_last = getenv("DX_ORDER_LAST") ? atoi(getenv("DX_ORDER_LAST")) : 0;
+  B.order_last = getenv("DX_ORDER_LAST") ? atoi(getenv("DX_ORDER_LAST")) : 1;
   b->hi_grid = getenv("DX_HI_GRID") ? std::max(1, atoi(getenv("DX_HI_GRID"))) : DX_HI_GRID;
   {
     int ncu = 0;
@@ -1957,6 +1958,7 @@ extern "C" int dx_env_sample_actions(dx_env* e, uint64_t seed, int32_t step) {
 struct TimingState {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
   bool on = false;
+  unsigned n = 0, every = 1;
 };
 static std::map<const dx_batch*, TimingState> g_timing;
 
@@ -1964,6 +1966,7 @@ static void timing_begin(dx_batch* b, hipEvent_t* start) {
   auto it = g_timing.find(b);
   *start = nullptr;
   if (it == g_timing.end() || !it->second.on) return;
+  if (it->second.n++ % it->second.every) return;  // (every every-th launch, dx_timing_enable)
   (void)hipEventCreate(start);
   (void)hipEventRecord(*start, b->stream);
 }
@@ -1977,7 +1980,10 @@ static void timing_end(dx_batch* b, hipEvent_t start) {
 
 extern "C" int dx_timing_enable(dx_batch* b, int enable) {
   if (!b) return fail(DX_EINVAL, "null batch");
-  g_timing[b].on = enable != 0;
+  auto& st = g_timing[b];
+  st.on = enable != 0;
+  st.every = (unsigned)std::max(1, enable);
+  st.n = 0;
   return 0;
 }
 

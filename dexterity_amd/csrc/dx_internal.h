@@ -37,9 +37,15 @@
 #define DX_MAX_NV 64      // dof bitmasks are uint64
 #define DX_QUEUES 8         // substep queues: one per XCD (MI355X: 8 XCDs)
 #define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
+#define DX_QPARK_SLOTS 64   // substep queue: parked tasks (one per lane of a wave-wide scan)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
 #ifndef DX_SEP_WT
 #define DX_SEP_WT 0       // 1: cache entries stored write-through (sc1), the round-2 form
+#endif
+// 1: a cached separating direction that still separates stays in the cache (0: the
+// round-3 code cleared it after every such verdict, so the cache hit every other substep)
+#ifndef DX_SEP_KEEP
+#define DX_SEP_KEEP 1
 #endif
 #define DX_LDL_SLOTS 16   // tree-sparse LDL^T items: at most 16 x 64 (dx_device.h tree_solve)
 #ifndef DX_SWEEP_PK
@@ -48,6 +54,10 @@
 #ifndef DX_SWEEP
 #define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)
 #endif
+#ifndef DX_SWEEP_LA
+#define DX_SWEEP_LA 1     // sweep: the next pivot pair's block computed while the MFMA runs
+#endif
+
 // narrowphase lane groups per wave: 8 of 8 lanes, or 16 of 4 lanes when a substep has
 // more than 8 candidates (dx_step.hip narrow_pass); the LDS layout reserves the portal
 // points of the larger count
@@ -153,6 +163,9 @@ struct DevBatch {
   // queues in use (1 or DX_QUEUES: one per XCD), timeout mark
   unsigned* qhead;
   unsigned* progress;
+  // DX_QPARK: tasks parked while their env's previous physics step still ran,
+  // [DX_QPARK_SLOTS] entries (s + 1) << 24 | env (0: free), then the parked count; null: off
+  unsigned* qpark;
   unsigned epoch;
   int nqueue;
   int* qerr;
@@ -191,7 +204,9 @@ struct DevBatch {
   int mid, mid_defer_at;
   unsigned mid_epoch;  // this launch's number among the mid tier's launches
   int defer_at;  // defer a physics step with more contacts than this (DX_NCON_MAX; DX_DEFER_AT for tests)
-  int order_last;  // longest-first key from the control step's last physics step (x nsub), not its sum
+  // longest-first key: 1 (default) the control step's last physics step's cost x nsub, 0
+  // the whole control step's cost (measured same-box: 1 is 0.4 % faster), 2 their mean
+  int order_last;
   // Task logic fused into the step kernel (dx_task.h; DevBatch::tp / ts): task_pre in the
   // env's first physics-step task, with ctrl = the action (`action`, [nenv][nu], or drawn
   // in the kernel by the random agent when act_random: dx_urand(act_seed, env0 + env,

@@ -159,8 +159,9 @@ int dx_sensor_enable(dx_batch* b, int enable);
  *   4 env-substeps that diverged (DX_DIVERGED) and reset their env
  *   5 the most contacts one env-substep found, when above 16 (else 0)
  *   6 env-substeps that found more than the 32 contacts the step kernel keeps in LDS and
- *     were therefore run by the overflow tier (the same physics with the 256-contact
- *     pool, a second small kernel behind every step launch): not a truncation
+ *     were therefore run by a larger pool -- the mid tier (64 contacts, beside a queued
+ *     step launch on a side stream) or the overflow tier (256, behind the launch), the
+ *     same physics: not a truncation
  * then, when the histogram is on (dx_ncon_histogram), out[16 .. 16 + 65): env-substeps
  * by contacts found (bins 0..63, then >= 64).  Synchronises the batch's stream. */
 #define DX_HEALTH_WORDS 16
@@ -238,8 +239,8 @@ int dx_env_goal_dim(const dx_env* e);
 int dx_env_reset(dx_env* e);
 /* One control step for every env; action is [nenv][nu] float32, device memory.  The
  * reorient task's before_step / after_step / reward / observation run inside the step
- * kernel: a control step is two kernel launches (the step kernel and the overflow tier's,
- * which also orders the next launch). */
+ * kernel: a control step is the step kernel, the mid contact tier beside it (a side
+ * stream) and the overflow tier's launch after it, which also orders the next launch. */
 int dx_env_step(dx_env* e, const float* action);
 /* composer.Environment's time_limit (manipulation/__init__.py:61,83): an episode also
  * ends (LAST, with the task's discount) once its physics time reaches `seconds`.
@@ -349,8 +350,10 @@ int dx_ik_solve(dx_batch* b, const dx_ik_options* opt, const int32_t* sites, int
                 int32_t* success, float* linear_err, int32_t* attempt, int32_t* steps);
 
 /* Timing ---------------------------------------------------------------- */
-/* When enabled, HIP events bracket every step-kernel launch on the batch stream;
- * dx_timing_read syncs, returns the summed kernel time and launch count, and clears. */
+/* When enabled, HIP events bracket the step-kernel launches on the batch stream -- every
+ * launch (enable = 1) or every enable-th one (enable > 1: the events' own packets cost
+ * ~5 us per bracketed launch); dx_timing_read syncs, returns the summed kernel time and
+ * the count of bracketed launches, and clears. */
 int dx_timing_enable(dx_batch* b, int enable);
 int dx_timing_read(dx_batch* b, double* total_ms, int32_t* count);
 /* Per-stage shader-clock accounting inside the fused step kernel (diagnostics):

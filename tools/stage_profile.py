@@ -57,6 +57,13 @@ for e in order[-4:][::-1]:
     cnts = {name: round(per_env[e, k] / (steps * 5), 1) for k, name in _lib.COUNTERS.items()
             if name in ("mpr", "mpr_support", "mpr_hit", "np_trips", "newton_iter", "linesearch_iter", "nefc")}
     print(f"  env {e}: {tot_env[e] / (steps * 5):.0f} cyc/substep;", ", ".join(f"{n} {v:.0f}" for v, n in parts), cnts)
+# substep queue: slot-time spent waiting for an env's previous physics step, against the
+# tasks' own cycles (both in s_memtime cycles; 2.39 GHz shader clock under the bench)
+wait = per_env[:, 35].sum()
+busy = per_env[:, stage_cols].sum()
+slots = 2047
+print(f"queue waits {wait / (B * steps * 5):.0f} cyc/env-substep = {100 * wait / (busy + wait):.1f}% of slot time in "
+      f"tasks; slot utilisation at 2.39 GHz ~ {(busy + wait) / (slots * dt / steps * 2.39e9 * steps):.3f}")
 niter = env.physics.get(_lib.NITER)[:, 0]
 ncon = env.physics.get(_lib.NCON)[:, 0]
 print("niter hist", np.bincount(niter), "ncon mean", ncon.mean(), "max", ncon.max())
