@@ -1013,7 +1013,6 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.qhead, DX_QUEUES * DX_QHEAD_STRIDE * 4);
   rc |= balloc(b, (void**)&B.progress, E * 4);
   rc |= balloc(b, (void**)&B.qerr, 8);  // [0] queue timeout, [1] the overflow kernel's finished workgroups
-  if (getenv("DX_QPARK") && atoi(getenv("DX_QPARK"))) rc |= balloc(b, (void**)&B.qpark, (DX_QPARK_SLOTS + 1) * 4);
   B.hand_stride = (d.nq + 2 * d.nv + 4 + 31) / 32 * 32;
   rc |= balloc(b, (void**)&B.hand, E * B.hand_stride * 4);
   B.epoch = 0;

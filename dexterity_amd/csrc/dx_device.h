@@ -986,43 +986,15 @@ __device__ __forceinline__ void mfma_sweep_solve30(const float* A, int n, float 
     if (j == 31 && i < n) e = xv[v];  // column 31: b_i
     C[v] = e;
   }
-#if DX_SWEEP_LA
-  // look-ahead: the next pair's 2 x 2 pivot block after this step's update is computed from
-  // this step's scalars (S'[a][b] = S[a][b] - sum_h S[k+h][a] (W V^T)[h][b], the entries the
-  // MFMA writes there) while the MFMA runs, so the chain between two MFMAs no longer holds
-  // the pivot readlanes and the divide
-  float q00, q10, q11;
-  {
-    const float r0 = half_dup(C[0], false), r1 = half_dup(C[1], false);
-    q00 = rl(r0, 0); q10 = rl(r1, 0); q11 = rl(r1, 1);
-  }
-#endif
 #pragma unroll
   for (int k = 0; k < 30; k += 2) {
     if (k >= n) continue;  // identity padding (a uniform branch; break would block the unroll)
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // S[k][j], S[k+1][j]
-#if DX_SWEEP_LA
-    const float p00 = q00, p10 = q10, p11 = q11;
-#else
     const float p00 = rl(rk, k), p10 = rl(rk1, k), p11 = rl(rk1, k + 1);
-#endif
     const float id = 1.0f / (p00 * p11 - p10 * p10);
     const float w00 = p11 * id, w01 = -p10 * id, w11 = p00 * id;
-#if DX_SWEEP_LA
-    if (k + 2 < 30 && k + 2 < n) {
-      const int k2 = k + 2, vk2 = 4 * (k2 >> 3) + (k2 & 3);
-      const bool up2 = (k2 & 7) >= 4;
-      const float r2 = half_dup(C[vk2], up2), r3 = half_dup(C[vk2 + 1], up2);  // S[k+2][j], S[k+3][j]
-      const float x0 = rl(rk, k2), x1 = rl(rk1, k2), y0 = rl(rk, k2 + 1), y1 = rl(rk1, k2 + 1);
-      const float wx0 = fmaf(w00, x0, w01 * x1), wx1 = fmaf(w01, x0, w11 * x1);
-      const float wy0 = fmaf(w00, y0, w01 * y1), wy1 = fmaf(w01, y0, w11 * y1);
-      q00 = rl(r2, k2) - fmaf(x0, wx0, x1 * wx1);
-      q10 = rl(r3, k2) - fmaf(y0, wx0, y1 * wx1);
-      q11 = rl(r3, k2 + 1) - fmaf(y0, wy0, y1 * wy1);
-    }
-#endif
     const bool pc = j == k || j == k + 1;  // a pivot column
     const float v0 = pc ? (j == k ? -1.f : 0.f) : rk;
     const float v1 = pc ? (j == k ? 0.f : -1.f) : rk1;

@@ -37,7 +37,6 @@
 #define DX_MAX_NV 64      // dof bitmasks are uint64
 #define DX_QUEUES 8         // substep queues: one per XCD (MI355X: 8 XCDs)
 #define DX_QHEAD_STRIDE 64  // words between two queue heads (each on its own 256-B span)
-#define DX_QPARK_SLOTS 64   // substep queue: parked tasks (one per lane of a wave-wide scan)
 #define DX_SEP_SLOTS 64   // per-env MPR separating-direction cache, slot = geom pair & 63
 #ifndef DX_SEP_WT
 #define DX_SEP_WT 0       // 1: cache entries stored write-through (sc1), the round-2 form
@@ -53,9 +52,6 @@
 #endif
 #ifndef DX_SWEEP
 #define DX_SWEEP 1        // dense solves n <= 30 by the MFMA sweep operator (else Cholesky)
-#endif
-#ifndef DX_SWEEP_LA
-#define DX_SWEEP_LA 1     // sweep: the next pivot pair's block computed while the MFMA runs
 #endif
 
 // narrowphase lane groups per wave: 8 of 8 lanes, or 16 of 4 lanes when a substep has
@@ -163,9 +159,6 @@ struct DevBatch {
   // queues in use (1 or DX_QUEUES: one per XCD), timeout mark
   unsigned* qhead;
   unsigned* progress;
-  // DX_QPARK: tasks parked while their env's previous physics step still ran,
-  // [DX_QPARK_SLOTS] entries (s + 1) << 24 | env (0: free), then the parked count; null: off
-  unsigned* qpark;
   unsigned epoch;
   int nqueue;
   int* qerr;

@@ -3504,93 +3504,20 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   int q = (int)((xcc & 7u) % (unsigned)nqueue);
   int empty = 0;  // queues found drained, in the order this workgroup visits them
-  unsigned park_spin = 0;
   for (;;) {
-    int s = -1, env = -1;
-    bool from_park = false;
-    // parked tasks first (DX_QPARK): a claimed task whose env's previous physics step was
-    // still running was parked instead of waited for; the first parked task whose
-    // predecessor has finished is taken (CAS on its slot), so no slot idles on a wait
-    if (B.qpark) {
-      const unsigned np = __builtin_amdgcn_readfirstlane(
-          LANE == 0 ? __hip_atomic_load(B.qpark + DX_QPARK_SLOTS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u);
-      if (np > 0) {
-        const unsigned v = __hip_atomic_load(B.qpark + LANE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        bool ready = false;
-        if (v) {
-          const unsigned tag = __hip_atomic_load(B.progress + (v & 0xffffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const int ps = (int)(v >> 24) - 1;
-          ready = tag == qtag(B.epoch, ps) || tag == qtag(B.epoch, DX_TAG_DEFER) || tag == qtag(B.epoch, DX_TAG_DONE);
-        }
-        const uint64_t rb = __ballot(ready);
-        if (rb) {
-          const int l = __builtin_ctzll(rb);
-          const unsigned vl = __shfl(v, l, 64);
-          unsigned won = 0;
-          if (LANE == 0) {
-            unsigned exp = vl;
-            won = __hip_atomic_compare_exchange_strong(B.qpark + l, &exp, 0u, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT);
-            if (won) __hip_atomic_fetch_sub(B.qpark + DX_QPARK_SLOTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-          if (__builtin_amdgcn_readfirstlane(won)) {
-            s = (int)(vl >> 24) - 1;
-            env = (int)(vl & 0xffffffu);
-            from_park = true;
-          } else {
-            continue;  // another workgroup took it: look again
-          }
-        } else if (empty >= nqueue) {
-          // queues drained, parked tasks not ready yet (bounded as the wait below is: a
-          // launch another task aborted ends here too)
-          __builtin_amdgcn_s_sleep(2);
-          unsigned bad = 0;
-          if (LANE == 0) {
-            bad = __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (++park_spin > (1u << 25)) {
-              __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              bad = 1;
-            }
-          }
-          if (__builtin_amdgcn_readfirstlane(bad)) break;
-          continue;
-        }
-      }
+    // queue q: order positions q + nqueue * j, j < nq
+    const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
+    unsigned t = 0;
+    if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __builtin_amdgcn_readfirstlane(t);
+    if (t >= nq * (unsigned)nsub) {
+      if (++empty >= nqueue) break;
+      q = q + 1 == nqueue ? 0 : q + 1;
+      continue;
     }
-    if (!from_park) {
-      if (empty >= nqueue) break;  // (with DX_QPARK: and no task parked)
-      // queue q: order positions q + nqueue * j, j < nq
-      const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
-      unsigned t = 0;
-      if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = __builtin_amdgcn_readfirstlane(t);
-      if (t >= nq * (unsigned)nsub) {
-        ++empty;
-        q = q + 1 == nqueue ? 0 : q + 1;
-        continue;
-      }
-      s = (int)(t / nq);
-      const int k = q + nqueue * (int)(t - (unsigned)s * nq);
-      env = B.order ? B.order[k] : k;
-      if (B.qpark && s > 0) {
-        // predecessor not finished: park the task in a free slot (else wait below)
-        unsigned parked = 0;
-        if (LANE == 0) {
-          const unsigned tag = __hip_atomic_load(B.progress + env, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (tag != qtag(B.epoch, s) && tag != qtag(B.epoch, DX_TAG_DEFER) && tag != qtag(B.epoch, DX_TAG_DONE)) {
-            const unsigned val = ((unsigned)(s + 1) << 24) | (unsigned)env;
-            for (int j = 0; j < DX_QPARK_SLOTS && !parked; j++) {
-              const int slot = (env + j) & (DX_QPARK_SLOTS - 1);
-              unsigned exp = 0u;
-              parked = __hip_atomic_compare_exchange_strong(B.qpark + slot, &exp, val, __ATOMIC_RELAXED,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            if (parked) __hip_atomic_fetch_add(B.qpark + DX_QPARK_SLOTS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        }
-        if (__builtin_amdgcn_readfirstlane(parked)) continue;
-      }
-    }
+    const int s = (int)(t / nq);
+    const int k = q + nqueue * (int)(t - (unsigned)s * nq);
+    const int env = B.order ? B.order[k] : k;
     if (s > 0) {
       int abort = 0;
       if (LANE == 0) {
