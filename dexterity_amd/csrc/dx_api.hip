@@ -935,10 +935,10 @@ struct dx_batch {
   float* sen_stash = nullptr;
   unsigned* ncon_hist = nullptr;  // dx_ncon_histogram
   // the mid tier beside queued launches (dx_step.hip dx_step_mid_kernel): its stream, the
-  // queued workgroups' exit count it waits for (DevBatch::qdone[0]) and its launch count
+  // queued workgroups' exit count it waits for (DevBatch::qdone[0])
   bool mid = false;
   hipStream_t side = nullptr;
-  unsigned qdone_target = 0, mid_epoch = 0;
+  unsigned qdone_target = 0;
 };
 
 #define DX_HI_GRID 32  // workgroups of the overflow tier (each loops over the deferred steps)
@@ -953,6 +953,7 @@ static int balloc(dx_batch* b, void** p, size_t bytes) {
 extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t device) {
   dx_model* m = const_cast<dx_model*>(mc);
   if (!m || nenv < 1) { fail(DX_EINVAL, "bad model or nenv"); return nullptr; }
+  if (nenv > (1 << DX_DEFER_ENV_BITS)) { fail(DX_ELIMIT, "nenv above 2^20 per batch (deferral entries)"); return nullptr; }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
     fail(DX_EHIP, "invalid HIP device (is a GPU visible?)");
@@ -1219,7 +1220,9 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   HIPCHK(hipSetDevice(b->device));
   size_t lds = (size_t)b->model->lds.total * 4;
   if (const char* pad = getenv("DX_LDS_PAD")) lds += (size_t)atol(pad);  // occupancy experiment
-  // (progress tags 30 and 31 are markers: dx_step.hip DX_QUEUE_NSUB)
+  // (progress tags 30 and 31 are markers: dx_step.hip DX_QUEUE_NSUB; a deferral entry
+  // holds the physics step in 8 bits)
+  if (b->db.defer && nsub > 255) return fail(DX_EINVAL, "at most 255 physics steps per call");
   const bool queued = mode == 0 && b->queue && nsub <= 29;
   // a mode-0 step builds the next launch's longest-first order, placed by the overflow
   // tier's launch (or, without one, by the order kernel)
@@ -1240,7 +1243,6 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
     b->qhead_zero = false;
   }
   Bo.mid = mid ? 1 : 0;
-  if (mid) Bo.mid_epoch = ++b->mid_epoch;
   hipEvent_t t0;
   timing_begin(b, &t0);
   hipError_t e = dx_launch_step(b->spec, grid, lds, b->stream, b->dm_dev, b->db, b->model->lds, nsub, queued ? 3 : mode);

@@ -183,19 +183,16 @@ struct DevBatch {
   // candidates, else eight 8-lane groups (DX_WAVE / 8; DX_NP_WIDE overrides it, the
   // group-size invisibility test forces either layout)
   int np_wide;
-  // physics steps deferred to the overflow tier (dx_step.hip dx_step_hi_kernel): [0] the
-  // count, [1] the overflow kernel's finished workgroups, [2 ..] entries env | substep
-  // << 24 | forward-only << 30, appended by the step kernel, emptied by the overflow
-  // kernel's last workgroup
+  // physics steps deferred by the step kernel (dx_step.hip env_defer): [0] the count, [1]
+  // unused, [2 ..] entries (DX_DEFER_*), emptied by the overflow kernel's last workgroup
   unsigned* defer;
   // with the mid tier running beside a queued launch (mid = 1): the step kernel publishes
   // each deferral (state in the env's hand-off record, entry | DX_DEFER_VALID stored after
   // it), its workgroups count themselves in qdone[0] as they exit, and the mid tier's own
   // deferrals go to defer2 (same layout, batch arrays) for the overflow tier
   unsigned* defer2;
-  unsigned* qdone;  // [0] exits of queued workgroups (never reset), [1] the last mid launch that finished
+  unsigned* qdone;  // [0] exits of queued workgroups (never reset), [1] deferral entries finished this launch
   int mid, mid_defer_at;
-  unsigned mid_epoch;  // this launch's number among the mid tier's launches
   int defer_at;  // defer a physics step with more contacts than this (DX_NCON_MAX; DX_DEFER_AT for tests)
   // longest-first key: 1 (default) the control step's last physics step's cost x nsub, 0
   // the whole control step's cost (measured same-box: 1 is 0.4 % faster), 2 their mean
@@ -216,8 +213,11 @@ struct DevBatch {
   unsigned *ohist, *okey;
   int opar, onext;
 };
-#define DX_DEFER_FWD (1u << 30)
-#define DX_DEFER_VALID (1u << 31)  // a published entry (mid tier: consumed entries are zeroed)
+// deferral entries: env (bits 0-19) | physics step << 20 (bits 20-27) | flags
+#define DX_DEFER_ENV_BITS 20
+#define DX_DEFER_FWD (1u << 28)      // forward only (dx_forward)
+#define DX_DEFER_CLAIMED (1u << 29)  // taken by the mid tier or the overflow tier (compare-and-swap)
+#define DX_DEFER_VALID (1u << 31)    // published (beside a mid-tier launch)
 #define DX_HEALTH_WORDS 16
 #define DX_NCON_HIST 65   // bins 0..63, and >= 64
 #define DX_MAXVAL 1e10f   // mjMAXVAL: |qacc| beyond this is a diverged state (mj_checkAcc)

@@ -3355,7 +3355,7 @@ __device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int e
                                           unsigned* list = nullptr) {
   const bool publish = B.mid && list == nullptr;
   if (!list) list = B.defer;
-  const unsigned val = (unsigned)env | ((unsigned)s << 24) | (fwd ? DX_DEFER_FWD : 0u);
+  const unsigned val = (unsigned)env | ((unsigned)s << DX_DEFER_ENV_BITS) | (fwd ? DX_DEFER_FWD : 0u);
   if (publish) {
     env_store_hand(c, B.hand + (size_t)env * B.hand_stride, B.hand_stride, time, 0u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3376,6 +3376,26 @@ __device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int e
   }
   if (!fwd && list == B.defer) order_key(B, env, 0xffffffffu);
 }
+
+// Deferral entries beside a mid-tier launch: either consumer -- the mid tier while the
+// launch runs, or the overflow tier after it, should the mid tier not have run (a
+// profiler or a shared hardware queue serialising the two streams) -- takes an entry by
+// compare-and-swap.  Lane 0: 1 taken (*e its value), 2 taken by the other consumer, 0 not
+// published yet.
+__device__ __forceinline__ int defer_claim(unsigned* list, unsigned i, unsigned* e) {
+  unsigned v = __hip_atomic_load(list + 2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (!(v & DX_DEFER_VALID)) return 0;
+    if (v & DX_DEFER_CLAIMED) return 2;
+    if (__hip_atomic_compare_exchange_strong(list + 2 + i, &v, v | DX_DEFER_CLAIMED, __ATOMIC_RELAXED,
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      *e = v;
+      return 1;
+    }
+  }
+}
+__device__ __forceinline__ int defer_env(unsigned e) { return (int)(e & ((1u << DX_DEFER_ENV_BITS) - 1u)); }
+__device__ __forceinline__ int defer_step(unsigned e) { return (int)((e >> DX_DEFER_ENV_BITS) & 255u); }
 
 // Fused task_pre (DevBatch::fuse) in the env's first physics-step task: before_step /
 // initialize_episode by lane 0, then ctrl = the action (zero after a reset), every lane,
@@ -3692,12 +3712,32 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
       if (e < e1) ((int*)B.order)[p + (key & 0xffffu)] = e;
     }
   }
-  // 2. the deferred physics steps (beside a mid-tier launch: those beyond its pool, once
-  // the mid tier has finished)
+  // 2. the deferred physics steps.  Beside a mid-tier launch: first the step kernel's
+  // deferrals the mid tier has not taken (it may not have run yet: a profiler or a shared
+  // hardware queue can serialise the streams), from their hand-off records; then, once
+  // every one of them has finished (the mid tier's too), those beyond the mid tier's pool
+  const unsigned n1 = B.mid ? B.defer[0] : 0u;
+  for (unsigned i = blockIdx.x; i < n1; i += gridDim.x) {
+    unsigned e = 0;
+    int got = 0;
+    if (LANE == 0) got = defer_claim(B.defer, i, &e);
+    if (__shfl(got, 0, 64) != 1) continue;
+    e = __shfl(e, 0, 64);
+    const int env = defer_env(e), s0 = defer_step(e);
+    CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
+    c.I = (int*)(smem + c.L.ints);
+    c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
+    c.np_wide = B.np_wide;
+    float time = env_begin(c, B, env, B.hand + (size_t)env * B.hand_stride, true);
+    for (int s = s0; s < nsub; s++) env_substep(c, B, time, env, s == nsub - 1);
+    env_finish(c, B, env, time);
+    if (B.fuse) fused_post(c, B, env, false);
+    if (LANE == 0) __hip_atomic_fetch_add(B.qdone + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (B.mid) {
     int ok = 1;
     if (LANE == 0) {
-      for (unsigned w = 0; (int)(__hip_atomic_load(B.qdone + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - B.mid_epoch) < 0; w++) {
+      for (unsigned w = 0; __hip_atomic_load(B.qdone + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n1; w++) {
         __builtin_amdgcn_s_sleep(4);
         if (w > (1u << 25)) { __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); ok = 0; break; }
       }
@@ -3709,8 +3749,7 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
   const unsigned n = list ? list[0] : 0u;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     const unsigned e = list[2 + i];
-    if (LANE == 0) list[2 + i] = 0u;
-    const int env = (int)(e & 0xffffffu), s0 = (int)((e >> 24) & 63u);
+    const int env = defer_env(e), s0 = defer_step(e);
     CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
     c.I = (int*)(smem + c.L.ints);
     c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
@@ -3735,8 +3774,13 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
   }
   if (__shfl(last, 0, 64)) {
     __threadfence();
-    if (B.defer && LANE < 2) B.defer[LANE] = 0u;          // the deferral lists
+    // the deferral lists: entries, counts, the finished count
+    for (unsigned i = LANE; B.defer && i < B.defer[0]; i += DX_WAVE) B.defer[2 + i] = 0u;
+    for (unsigned i = LANE; B.defer2 && i < B.defer2[0]; i += DX_WAVE) B.defer2[2 + i] = 0u;
+    SYNC();
+    if (B.defer && LANE < 2) B.defer[LANE] = 0u;
     if (B.defer2 && LANE < 2) B.defer2[LANE] = 0u;
+    if (B.qdone && LANE == 0) B.qdone[1] = 0u;
     if (B.onext)                                           // this launch's cost histogram
 #pragma unroll
       for (int k = 0; k < 4; k++) B.ohist[256 * B.opar + 4 * LANE + k] = 0u;
@@ -3764,21 +3808,21 @@ hipError_t dx_launch_step_hi(int grid, size_t lds, hipStream_t stream, const Dev
 // runs -- instead of after it, on an otherwise idle chip -- and runs each deferred env
 // from its hand-off record to the end of its control step with the DX_NCON_MID pool, with
 // the step kernel's outputs and task logic.  A physics step beyond this pool goes on to
-// the overflow tier's list (B.defer2).  Entries are consumed in order (workgroup w takes
-// entries w, w + grid, ...); consumed entries are zeroed, so a published entry is always
-// this launch's.  The launch's end is its workgroups' exit count (B.qdone[0], never reset)
-// reaching `target`; after it the count is this launch's (the overflow tier that reset it
-// ran before this launch on the batch stream) and every entry below it is taken.  No
-// stream event joins the two streams: the mid tier stores its launch number in
-// B.qdone[1] when it exits (release), and the overflow tier that follows the step kernel
-// waits for it (acquire).  The waits are bounded (B.qerr).
+// the overflow tier's list (B.defer2).  Entries are taken in order by compare-and-swap
+// (defer_claim), as the overflow tier takes any the mid tier has not when it runs after
+// the launch; the overflow tier's last workgroup zeroes them for the next launch.  The
+// launch's end is its workgroups' exit count (B.qdone[0], never reset) reaching `target`;
+// after it every entry below the count is taken.  No stream event joins the two streams:
+// each finished entry counts in B.qdone[1] (release), and the overflow tier waits until
+// every entry of the launch has finished (acquire) -- it never waits for the mid tier to
+// start, so a serialised order cannot deadlock.  The waits are bounded (B.qerr).
 // ------------------------------------------------------------------------ //
 static_assert(DX_NCON_MAX == DX_NCON_MID, "the mid tier is compiled with the DX_NCON_MID pool");
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2)))
 dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, unsigned target) {
   extern __shared__ float smem[];
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
-  for (unsigned i = blockIdx.x;; i += gridDim.x) {
+  for (unsigned i = 0;;) {
     unsigned e = 0;
     int got = 0;
     if (LANE == 0) {
@@ -3787,24 +3831,28 @@ dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned cnt = __hip_atomic_load(B.defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (i < cnt) {
-          e = __hip_atomic_load(B.defer + 2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (e & DX_DEFER_VALID) { got = 1; break; }
+          const int r = defer_claim(B.defer, i, &e);
+          if (r == 1) { got = 1; break; }
+          if (r == 2) { i++; continue; }  // the overflow tier took it
         } else if (done) {
           break;  // the launch is over and every deferral below cnt was taken
         }
         __builtin_amdgcn_s_sleep(4);
-        if (++n > (1u << 25) || ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-          __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Giving up is always safe -- the overflow tier takes every entry left -- so the
+        // wait is short and sets no error: it ends a mid tier that runs before its
+        // launch's step kernel (a profiler serialising the dispatches) or one whose
+        // launch aborted
+        if (++n > (1u << 17) || ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
           break;
-        }
       }
     }
+    i = __shfl(i, 0, 64);
     if (!__shfl(got, 0, 64)) break;
     e = __shfl(e, 0, 64);
+    i++;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (LANE == 0) B.defer[2 + i] = 0u;  // consumed (the next launch's entries start unpublished)
-    const int env = (int)(e & 0xffffffu), s0 = (int)((e >> 24) & 63u);
+    const int env = defer_env(e), s0 = defer_step(e);
     CtxT<SpecRT> c(m, L, smem, nullptr, nullptr);
     c.I = (int*)(smem + c.L.ints);
     c.sep = B.sepcache ? B.sepcache + (size_t)env * DX_SEP_SLOTS : nullptr;
@@ -3824,9 +3872,11 @@ dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub,
       env_finish(c, B, env, time);
       if (B.fuse) fused_post(c, B, env, false);
     }
+    // finished: its stores (and a deferral to the overflow tier's list) before the count
+    // the overflow tier waits for
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (LANE == 0) __hip_atomic_fetch_add(B.qdone + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // finished: every store above before the overflow tier's wait sees this launch's number
-  if (LANE == 0) __hip_atomic_store(B.qdone + 1, B.mid_epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 hipError_t dx_launch_step_mid(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B,

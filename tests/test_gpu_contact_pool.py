@@ -164,6 +164,48 @@ def test_steps_beyond_mid_tier_match_oracle(oracle_mod):
         ph.close()
 
 
+_SERIAL_SNIPPET = """
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+from dexterity_amd import _lib, physics
+from tests.test_gpu_contact_pool import box_field, _states
+cm = box_field(10)
+states = _states(cm, 16, np.random.RandomState(1), 4)
+ph = physics.BatchedPhysics(physics.Model(cm), len(states))
+ph.set(_lib.QPOS, np.stack([s[0] for s in states]))
+ph.set(_lib.QVEL, np.stack([s[1] for s in states]))
+for _ in range(3):
+    ph.step(5)
+np.save(sys.argv[1], np.concatenate([ph.qpos, ph.qvel], axis=1))
+print("deferred", ph.health()["contact_deferred"])
+"""
+
+
+def test_tiers_under_serialised_kernels(tmp_path):
+    """The mid tier and the overflow tier never wait for each other to start: with every
+    kernel serialised (AMD_SERIALIZE_KERNEL=3, as a profiler's counter collection does),
+    deferred physics steps still complete -- the overflow tier takes the entries the mid
+    tier has not -- and the results equal the concurrent run's bit for bit."""
+    import os
+    import subprocess
+    import sys
+
+    from tests.conftest import ROOT
+
+    outs = []
+    for serial in (False, True):
+        env = dict(os.environ)
+        if serial:
+            env["AMD_SERIALIZE_KERNEL"] = "3"
+        f = str(tmp_path / f"out_{int(serial)}.npy")
+        r = subprocess.run([sys.executable, "-c", _SERIAL_SNIPPET.format(root=ROOT), f], env=env, capture_output=True,
+                           text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert int(r.stdout.split()[-1]) >= 3
+        outs.append(np.load(f))
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
 def test_pool_cut_keeps_candidate_order(oracle_mod):
     """10 bars of 8 cubes on the ground: 320 contacts, beyond the 256-contact pool.  The
     first 256 in candidate order are kept -- the oracle's list, whose pool (256) fills

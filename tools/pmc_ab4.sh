@@ -13,7 +13,7 @@ run() {  # run <name> <counter> [ENV=VALUE ...]
     python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/$name.$ctr.log" 2>&1
   rc=$?; echo "$name $ctr rc=$rc"; return $rc
 }
-for cfg in "default" "noqueue DX_NO_QUEUE=1" "nofuse DX_NO_FUSE=1" "sepold DX_LIB=$R/variants/sepold/libdx.so"; do
+for cfg in "default" "noqueue DX_NO_QUEUE=1" "nofuse DX_NO_FUSE=1"; do
   set -- $cfg
   name=$1; shift
   run "$name" FETCH_SIZE "$@" || exit 1
@@ -22,7 +22,7 @@ done
 cd "$R" && python3 - <<'PY'
 import csv, glob, os, statistics
 root = "gpurun_out/pmc_ab4"
-for name in ("default", "noqueue", "nofuse", "sepold"):
+for name in ("default", "noqueue", "nofuse"):
     out = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         per = {}
