@@ -22,7 +22,7 @@ CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libdx.so")
 SPECS = os.path.join(CSRC, "dx_specs.inc")
 SOURCES = ("dx_step.hip", "dx_ik.hip", "dx_task.hip", "dx_sensor.hip", "dx_api.hip")
-HEADERS = ("dx_internal.h", "dx_device.h")
+HEADERS = ("dx_internal.h", "dx_device.h", "dx_task.h")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 DIMS = ("nq", "nv", "nbody", "njnt", "nu", "ntendon", "nsite", "nlevel", "nroot", "nfric", "nlimj", "nlimt",
         "nbpair", "any_damping", "disable_contact", "iterations")  # dx_step.hip DX_DIMS

@@ -271,8 +271,8 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
       if (P.prop_qadr >= 0) {
         if (e < 3) {
           val = q[P.prop_qadr + e];
-        } else if (e < 7) {
-          val = cur[e - 3] / n;
+        } else if (e < 7) {  // cur[e - 3], read from qpos: a lane-indexed cur[] would live in scratch
+          val = q[P.prop_qadr + e] / n;
         } else if (e < 10) {
           val = v[P.prop_dadr + e - 7];
         } else if (e < 13) {
