@@ -719,6 +719,9 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   layout(DX_NCON_HI, m->lds_hi);
   layout(DX_NCON_MID, m->lds_mid);
   if (m->lds_mid.nefc_max > 5 * 64) m->lds_mid.nefc_max = 0;  // (its line search keeps 5 register slots)
+  if (getenv("DX_PRINT_LDS"))
+    fprintf(stderr, "dx: LDS per env %d B (step kernel), %d B (mid tier), %d B (overflow tier)\n", m->lds.total * 4,
+            m->lds_mid.total * 4, m->lds_hi.total * 4);
   m->ncon_max = DX_NCON_HI;
   m->nefc_max = m->lds_hi.nefc_max;
   // line-search register slots (dx_step.hip DX_LS_SLOTS: 5 in the step kernel, 20 in the
