@@ -289,9 +289,8 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   d.ngpair = geti(m, "ngpair"); d.iterations = geti(m, "iterations");
   d.disable_contact = geti(m, "disable_contact");
   d.solver = geti(m, "solver", 2);  // absent in every reference scene: MuJoCo's default, Newton
-  if (d.solver != 1 && d.solver != 2) {
-    fail(DX_EMODEL, d.solver == 0 ? "solver PGS (the dual solver) is not supported: use CG or Newton"
-                                  : "unknown solver");
+  if (d.solver < 0 || d.solver > 2) {
+    fail(DX_EMODEL, "unknown solver");
     delete m;
     return nullptr;
   }
@@ -702,12 +701,13 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   // sensor stash right after the last one); never live at the same time
   L.cq = take(3 * cap);
   L.cw = L.cq;
-  // The solver's J dir (efc_jv) and CG's M^-1 grad: written only from the solve on, when
-  // the kinematic block is dead, so they go past the Newton Hessian when it has room
+  // The solver's J dir (efc_jv) and CG's M^-1 grad (PGS's M^-1 J_r'): written only from
+  // the solve on, when the kinematic block is dead, so they go past the Newton Hessian
+  // when it has room
   int spare = U0 + r4(ntri);
   if (spare + r4(L.nefc_max) <= B0) { L.efc_jv = spare; spare += r4(L.nefc_max); }
   else L.efc_jv = take(L.nefc_max);
-  if (d.solver != 1) L.cgv = 0;  // Newton: no CG scratch
+  if (d.solver == 2) L.cgv = 0;  // Newton: no CG / PGS scratch
   else if (spare + r4(nv) <= B0) L.cgv = spare;
   else L.cgv = take(nv);
   end = std::max(end, off);

@@ -2506,6 +2506,138 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
   SYNC();
 }
 
+// Dense row r of J into Jd (lane d: dof d), from the rows' compact forms (jac_rows).
+template <class Ctx>
+__device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
+  const DevModel& m = c.mdl();
+  const int nv = c.nv;
+  const int mt = ((const int*)c.f(c.L.efc_meta))[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
+  if (LANE < nv) {
+    const int d = LANE;
+    float v = 0.f;
+    if (type == DXR_FRIC) {
+      v = d == id ? 1.f : 0.f;
+    } else if (type == DXR_LIMJ) {
+      v = d == id ? (aux ? -1.f : 1.f) : 0.f;
+    } else if (type == DXR_LIMT) {
+      const float tj = m.tendon_J[id * nv + d];
+      v = aux ? -tj : tj;
+    } else {
+      const float* rc = c.f(c.L.con) + DX_CON_STRIDE * id;
+      const uint64_t sup = (uint64_t)(uint32_t)__float_as_int(rc[18]) | ((uint64_t)(uint32_t)__float_as_int(rc[19]) << 32);
+      const uint64_t bit = 1ull << d;
+      const int q = __popcll(sup & (bit - 1));
+      if ((sup & bit) && q < DX_DOFMAX) {
+        const float* cv = c.f(c.L.cj_val) + id * 3 * DX_DOFMAX + q;
+        v = cv[0];
+        if (type == DXR_CON) {
+          const int k = 1 + (aux >> 1);
+          v += rc[15 + k] * ((aux & 1) ? -1.f : 1.f) * cv[k * DX_DOFMAX];
+        }
+      }
+    }
+    Jd[d] = v;
+  }
+  SYNC();
+}
+
+// [3P] MuJoCo's PGS (mj_solPGS), <option solver="PGS">: projected Gauss-Seidel on the
+// dual, min_f 0.5 f'(A + R) f + f'b with A = J M^-1 J' and b = J qacc_smooth - aref;
+// friction-loss rows boxed to +-floss, limit and pyramidal contact rows f >= 0, rows in
+// order, each f_r -= res_r / AR_rr and projected.  Matrix-free: qacc = qacc_smooth +
+// M^-1 J'f is kept current, so res_r = J_r qacc - aref_r + R_r f_r and no nefc x nefc
+// matrix is held in LDS; M^-1 J_r' is one product with M^-1 (the sweep's inverse, nv <=
+// 30, as CG) or one Cholesky solve, only for a row whose force changed.  Warm start: the
+// primal forces at qacc_warmstart, kept when their dual cost is below zero's.  Stops
+// after `iterations` sweeps or when a sweep's scaled dual-cost decrease is below the
+// tolerance.  The forces go back as residuals jar_r = -R_r f_r, whose primal force
+// (row_cost) is f_r, so qfrc_constraint and the sensors read them unchanged.  Oracle:
+// dx_oracle.c solve_pgs.  Serial over rows: a scene option, not the reference's path.
+template <class Ctx>
+__device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) {
+  const int nv = c.nv, nefc = c.I[I_NEFC];
+  float* qacc = c.f(c.L.qacc);
+  const float* a0 = c.f(c.L.qacc_smooth);
+  float* g = c.f(c.L.v2);
+  float* Jd = c.f(c.L.v3);
+  float* u = c.f(c.L.cgv);
+  float* f = c.f(c.L.efc_jv);
+  float* jar = c.f(c.L.efc_jar);  // the warm start's residuals, then AR's diagonal
+  float* ard = jar;
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* Rf = c.f(c.L.efc_Rf);
+  const float* aref = c.f(c.L.efc_aref);
+  const float* M = c.f(c.L.M);
+  float* T = c.f(c.L.H);
+  const bool inv = DX_SWEEP && nv <= 30;
+  if (inv) mfma_sweep_inverse30(M, nv, T);
+  auto minv = [&](const float* x, float* y) {
+    if (inv) {
+      mat_vec(T, x, y, nv);
+      SYNC();
+    } else {
+      for (int i = LANE; i < nv; i += DX_WAVE) y[i] = x[i];
+      SYNC();
+      chol_solve(M, nv, y, T);
+    }
+  };
+  // warm start: jar holds J qacc_warmstart - aref (solve); g = J'f, u = M^-1 g
+  float dc = 0.f;
+  for (int r = LANE; r < nefc; r += DX_WAVE) {
+    const bool fr = r < c.nfric;
+    float fo, hw;
+    row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r], fo, hw);
+    f[r] = fo;
+    dc += 0.5f * fo * fo / D[r] - fo * aref[r];
+  }
+  jac_t_force(c, g);
+  minv(g, u);
+  for (int i = LANE; i < nv; i += DX_WAVE) dc += 0.5f * g[i] * u[i] + g[i] * a0[i];
+  const bool keep = wave_sum(dc) < 0.f;
+  for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = keep ? a0[i] + u[i] : a0[i];
+  if (!keep)
+    for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
+  SYNC();
+  // AR's diagonal: J_r M^-1 J_r' + R_r
+  for (int r = 0; r < nefc; r++) {
+    pgs_row(c, r, Jd);
+    minv(Jd, u);
+    const float s = wave_sum(LANE < nv ? Jd[LANE] * u[LANE] : 0.f);
+    if (LANE == 0) ard[r] = s + 1.0f / D[r];
+  }
+  SYNC();
+  int it = 0;
+  for (; it < c.iterations;) {
+    stage_count(c, CNT_NEWTON_IT);
+    float impr = 0.f;
+    for (int r = 0; r < nefc; r++) {
+      pgs_row(c, r, Jd);
+      const float jq = wave_sum(LANE < nv ? Jd[LANE] * qacc[LANE] : 0.f);
+      const float fo = f[r], ar = ard[r];
+      const float res = jq - aref[r] + fo / D[r];
+      float fn = fo - res / ar;
+      if ((meta[r] & 15) == DXR_FRIC) fn = fminf(fl[r], fmaxf(-fl[r], fn));
+      else fn = fmaxf(fn, 0.f);
+      const float dl = fn - fo;
+      if (dl != 0.f) {
+        minv(Jd, u);
+        if (LANE < nv) qacc[LANE] += dl * u[LANE];
+        if (LANE == 0) f[r] = fn;
+        impr -= 0.5f * ar * dl * dl + dl * res;
+        SYNC();
+      }
+    }
+    it++;
+    if (scale * impr < tol) break;
+  }
+  // the forces as residuals whose primal force is f_r
+  for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] = -f[r] / D[r];
+  if (LANE == 0) c.I[I_NITER] = it;
+  SYNC();
+}
+
 template <class Ctx>
 __device__ __forceinline__ void solve(const Ctx& c) {
   const DevModel& m = c.mdl();
@@ -2535,6 +2667,12 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   SYNC();
   float gw = 0.f;
   float cw = eval_cost(c, qacc, Ma, &gw);
+  if (m.solver == 0) {  // the dual solver starts from the warm start's forces
+    stage_count(c, CNT_SOLVE);
+    stage_count(c, CNT_NEFC, nefc);
+    solve_pgs(c, scale, tol);
+    return;
+  }
   jac_vec(c, a0, jvs);
   for (int r = LANE; r < nefc; r += DX_WAVE) jvs[r] -= aref[r];
   SYNC();

@@ -570,8 +570,8 @@ class CompiledModel:
                     tolerance: Optional[float] = None) -> "CompiledModel":
         """A copy with MuJoCo's `<option solver=... iterations=... tolerance=...>` set
         ([3P] mjOption; the reference sets none, so its scenes run Newton, 100
-        iterations, 1e-8).  "CG" and "Newton" run on the device; "PGS" (the dual
-        solver) is rejected by dx_model_load."""
+        iterations, 1e-8).  All three run on the device: "Newton" (the default) and
+        "CG" primal, "PGS" dual."""
         if solver not in self.SOLVERS:
             raise ValueError(f"unknown solver {solver!r}")
         arrays = dict(self.arrays)

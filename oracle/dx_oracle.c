@@ -12,7 +12,8 @@
  *   constraints ................ frictionloss/limits shadow_hand_series_e.xml:227, contacts
  *   smooth dynamics ............ actuators shadow_hand_position_actuators.xml:25-54,
  *                                gravity compensation utils/mujoco_utils.py:91-99
- *   Newton solver .............. [3P] MuJoCo default solver (no solver= in any reference XML)
+ *   Newton solver .............. [3P] MuJoCo default solver (no solver= in any reference XML);
+ *                                CG and PGS for <option solver=...> ([3P] mj_solCG, mj_solPGS)
  *   Euler (implicit damping) ... [3P] MuJoCo default integrator, dt from reorient.py:58 / reach.py:54
  * MuJoCo itself is third-party and absent: every [3P] semantic restated here is
  * listed in DESIGN.md §3 ("parity unpinned" against real MuJoCo).
@@ -154,12 +155,12 @@ dxo_model* dxo_model_load(const void* blob, size_t nbytes) {
     dxo_model_free(m);
     return NULL;
   }
-  /* optional <option solver>: 1 CG, 2 Newton (MuJoCo's default; absent in every
-     reference scene).  PGS (0, dual) is not restated. */
+  /* optional <option solver>: 0 PGS (dual), 1 CG, 2 Newton (MuJoCo's default; absent
+     in every reference scene) */
   s = (const int*)blob_find(m->blob, nbytes, "solver", 0, &cnt);
   m->solver = s ? s[0] : 2;
-  if (m->solver != 1 && m->solver != 2) {
-    fprintf(stderr, "dxo: solver %d not supported (CG = 1, Newton = 2)\n", m->solver);
+  if (m->solver < 0 || m->solver > 2) {
+    fprintf(stderr, "dxo: solver %d not supported (PGS = 0, CG = 1, Newton = 2)\n", m->solver);
     dxo_model_free(m);
     return NULL;
   }
@@ -1631,6 +1632,84 @@ static void solve_cg(const dxo_model* m, dxo_data* d) {
 #undef CG_GRAD
 }
 
+/* [3P] MuJoCo's PGS (mj_solPGS): projected Gauss-Seidel on the dual problem
+ *   min_f 0.5 f'(A + R) f + f'b,  A = J M^-1 J',  b = J qacc_smooth - aref,
+ * friction-loss rows boxed to [-floss, floss], limit and (pyramidal) contact rows
+ * f >= 0, rows visited in order, each a scalar update f_r -= res_r / AR_rr followed by
+ * its projection.  Restated matrix-free: qacc = qacc_smooth + M^-1 J'f is kept current
+ * (qacc += delta M^-1 J_r' per changed row), so res_r = J_r qacc - aref_r + R_r f_r and
+ * no nefc x nefc matrix is formed -- the same iterates as the AR form.  Warm start: the
+ * primal forces at qacc_warmstart, kept only when their dual cost is below that of
+ * f = 0 (zero).  Stops after `iterations` sweeps or when a sweep's scaled dual-cost
+ * decrease is below `tolerance`.  The oracle for dx_step.hip solve_pgs. */
+static void solve_pgs(const dxo_model* m, dxo_data* d) {
+  int nv = m->nv, nefc = d->nefc;
+  double* Ma = d->tmp1;
+  double* g = d->tmp2;
+  double* u = d->tmp4;
+  double* qacc = d->qacc;
+  double* f = d->efc_force;
+  double* ard = d->efc_jv;
+  const double* a0 = d->qacc_smooth;
+  double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
+  d->niter = 0;
+  if (nefc == 0) {
+    memcpy(qacc, a0, 8 * nv);
+    return;
+  }
+  /* warm start: primal forces at qacc_warmstart (eval_cost fills efc_force) */
+  eval_cost(m, d, d->qacc_warmstart, Ma);
+  memset(g, 0, 8 * nv);
+  double dc = 0;
+  for (int r = 0; r < nefc; r++) {
+    const double* J = d->efc_J + (size_t)r * nv;
+    for (int k = 0; k < nv; k++) g[k] += J[k] * f[r];
+    dc += 0.5 * d->efc_R[r] * f[r] * f[r] - f[r] * d->efc_aref[r];
+  }
+  chol_solve(d->L, u, g, nv, &d->flops[DXO_ST_SOLVE]);
+  for (int k = 0; k < nv; k++) dc += 0.5 * g[k] * u[k] + g[k] * a0[k];
+  if (dc < 0) {
+    for (int k = 0; k < nv; k++) qacc[k] = a0[k] + u[k];
+  } else {
+    memset(f, 0, 8 * nefc);
+    memcpy(qacc, a0, 8 * nv);
+  }
+  /* diagonal of AR */
+  for (int r = 0; r < nefc; r++) {
+    const double* J = d->efc_J + (size_t)r * nv;
+    chol_solve(d->L, u, J, nv, &d->flops[DXO_ST_SOLVE]);
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += J[k] * u[k];
+    ard[r] = s + d->efc_R[r];
+  }
+  for (int it = 0; it < m->iterations; it++) {
+    double impr = 0;
+    for (int r = 0; r < nefc; r++) {
+      const double* J = d->efc_J + (size_t)r * nv;
+      double jq = 0;
+      for (int k = 0; k < nv; k++) jq += J[k] * qacc[k];
+      double res = jq - d->efc_aref[r] + d->efc_R[r] * f[r];
+      double fn = f[r] - res / ard[r];
+      if (d->efc_type[r] == EFC_FRIC_DOF) {
+        double fl = d->efc_floss[r];
+        fn = fn < -fl ? -fl : (fn > fl ? fl : fn);
+      } else if (fn < 0) {
+        fn = 0;
+      }
+      double dl = fn - f[r];
+      if (dl != 0) {
+        chol_solve(d->L, u, J, nv, &d->flops[DXO_ST_SOLVE]);
+        for (int k = 0; k < nv; k++) qacc[k] += dl * u[k];
+        f[r] = fn;
+        impr -= 0.5 * ard[r] * dl * dl + dl * res;
+      }
+      d->flops[DXO_ST_SOLVE] += 4.0 * nv + 10;
+    }
+    d->niter++;
+    if (scale * impr < m->tolerance) break;
+  }
+}
+
 static void finish_constraint(const dxo_model* m, dxo_data* d) {
   int nv = m->nv;
   memset(d->qfrc_constraint, 0, 8 * nv);
@@ -1803,6 +1882,8 @@ int dxo_forward(const dxo_model* m, dxo_data* d) {
   /* constraint velocities were computed in make_constraint with current qvel */
   if (m->solver == 1)
     solve_cg(m, d);
+  else if (m->solver == 0)
+    solve_pgs(m, d);
   else
     solve_newton(m, d);
   finish_constraint(m, d);

@@ -1091,6 +1091,79 @@ def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):
         phys.close()
 
 
+def test_pgs_solver_parity(gpu, oracle_mod, reorient_setup):
+    """<option solver="PGS"> ([3P] MuJoCo's dual projected Gauss-Seidel): the kernel's
+    PGS (dx_step.hip solve_pgs) against the oracle's (dx_oracle.c solve_pgs) on the
+    contact-rich states -- run to convergence, both at the Newton optimum (the primal
+    problem's solution, the restatement's anchor); at MuJoCo's defaults (100 sweeps,
+    1e-8), kernel vs oracle at identical settings, one forward pass and 1 / 3 substeps."""
+    cm, xfrc, om, states, _ = reorient_setup
+    pg = cm.with_solver("PGS", iterations=3000, tolerance=1e-13)
+    om_pg = oracle_mod.OracleModel(blob.pack(pg.arrays))
+    phys = _load_states(gpu, gpu.Model(pg), xfrc, states)
+    phys.forward()
+    qacc = phys.qacc
+    e_pg, e_nt = [], []
+    for e, st in enumerate(states):
+        d_pg = _oracle_pair(oracle_mod, om_pg, pg, xfrc, st)
+        d_nt = _oracle_pair(oracle_mod, om, cm, xfrc, st)
+        scale = max(1.0, np.abs(d_nt[0].qacc_smooth).max())
+        e_pg.append(min(np.abs(qacc[e] - d.qacc).max() for d in d_pg) / scale)
+        e_nt.append(min(np.abs(qacc[e] - d.qacc).max() for d in d_nt) / scale)
+    phys.close()
+    e_pg, e_nt = np.array(e_pg), np.array(e_nt)
+    print(f"PGS converged: |qacc| err / scale vs oracle PGS max {e_pg.max():.2e}, vs Newton max {e_nt.max():.2e}")
+    assert e_pg.max() <= PGS_CONV_MAX and e_nt.max() <= PGS_CONV_MAX
+    # MuJoCo's defaults on both sides
+    pgd = cm.with_solver("PGS")
+    om_d = oracle_mod.OracleModel(blob.pack(pgd.arrays))
+    phys = _load_states(gpu, gpu.Model(pgd), xfrc, states)
+    phys.forward()
+    qacc = phys.qacc
+    ea = []
+    for e, st in enumerate(states):
+        d_pg = _oracle_pair(oracle_mod, om_d, pgd, xfrc, st)
+        scale = max(1.0, np.abs(d_pg[0].qacc_smooth).max())
+        ea.append(min(np.abs(qacc[e] - d.qacc).max() for d in d_pg) / scale)
+    phys.close()
+    ea = np.array(ea)
+    print(f"PGS defaults, forward: |qacc| err / scale median {np.median(ea):.2e} max {ea.max():.2e}")
+    assert np.median(ea) <= PGS_QACC_MED and ea.max() <= PGS_QACC_MAX
+    for nsub in (1, 3):
+        phys = _load_states(gpu, gpu.Model(pgd), xfrc, states)
+        phys.step(nsub)
+        qpos, qvel = phys.qpos, phys.qvel
+        assert np.all(np.isfinite(qpos)) and np.all(np.isfinite(qvel))
+        eq, ev = [], []
+        for e, st in enumerate(states):
+            best = None
+            for x, y in ((xfrc, st), (np.asarray(xfrc, dtype=np.float32).astype(np.float64), _f32(st))):
+                d = oracle_mod.OracleData(om_d)
+                d.xfrc_applied[:] = x.ravel()
+                d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = y
+                for _ in range(nsub):
+                    d.step()
+                sc = max(1.0, np.abs(d.qacc_smooth).max())
+                q, v = np.abs(qpos[e] - d.qpos).max(), np.abs(qvel[e] - d.qvel).max() / sc
+                best = (q, v) if best is None or q < best[0] else best
+            eq.append(best[0])
+            ev.append(best[1])
+        eq, ev = np.array(eq), np.array(ev)
+        print(f"PGS defaults, {nsub} substep(s): |qpos| err median {np.median(eq):.2e} max {eq.max():.2e}; "
+              f"|qvel|/scale median {np.median(ev):.2e} max {ev.max():.2e}")
+        assert eq.max() <= PGS_QPOS_MAX * nsub and ev.max() <= PGS_QVEL_MAX
+        phys.close()
+
+
+# PGS bounds.  Measured (r4) over the 12 states: converged (3000 sweeps, 1e-13) qacc
+# within 2.9e-4 x scale of both the oracle's PGS and the Newton optimum (fp32's floor
+# here, CG's bound); defaults, one forward: median 4.4e-5, max 1.9e-4; 1 / 3 substeps:
+# qpos max 9.3e-8 / 1.5e-7, qvel / scale max 9.2e-7 / 6.7e-7
+PGS_CONV_MAX = 5e-4
+PGS_QACC_MED, PGS_QACC_MAX = 2e-4, 1e-3
+PGS_QPOS_MAX, PGS_QVEL_MAX = 1e-6, 1e-5
+
+
 # CG at MuJoCo's defaults stops after 100 iterations or at 1e-8 on a linearly converging
 # path that fp32 and fp64 walk differently.  Measured (r3) over the contact-rich states:
 # qpos median 9e-8 / max 2.1e-6 (1 substep), 5.9e-5 (3 substeps); qvel / scale median

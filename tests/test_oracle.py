@@ -289,6 +289,49 @@ def test_oracle_cg_reaches_the_newton_optimum(oracle_mod, reorient_compiled):
     assert checked >= 3
 
 
+def test_oracle_pgs_reaches_the_newton_optimum(oracle_mod, reorient_compiled):
+    """`<option solver="PGS">` ([3P] MuJoCo's dual projected Gauss-Seidel) solves the
+    dual of the primal problem Newton minimises: run to convergence, its acceleration
+    qacc_smooth + M^-1 J'f is Newton's (the restatement's anchor: MuJoCo itself is not
+    in the reference, so PGS's iterates are pinned only through this optimum).  At
+    MuJoCo's defaults (100 sweeps, 1e-8) it stops within the sweep budget."""
+    from dexterity_amd import blob
+
+    cm = reorient_compiled
+    xfrc = gravity_compensation(cm, "shadow_hand_e/")
+    newton = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    pgs = oracle_mod.OracleModel(blob.pack(cm.with_solver("PGS", iterations=20000, tolerance=1e-15).arrays))
+    pgs_d = oracle_mod.OracleModel(blob.pack(cm.with_solver("PGS").arrays))
+    rng = np.random.RandomState(3)
+    d = oracle_mod.OracleData(newton)
+    d.xfrc_applied[:] = xfrc.ravel()
+    d.qpos[24:27] += [0.01, -0.01, 0]
+    lo, hi = cm.actuator_ctrlrange.T
+    checked = 0
+    for s in range(120):
+        d.ctrl[:] = 0.3 * rng.uniform(lo, hi)
+        d.step()
+        if s % 20 != 19:
+            continue
+        a = oracle_mod.OracleData(newton)
+        b = oracle_mod.OracleData(pgs)
+        c = oracle_mod.OracleData(pgs_d)
+        for x in (a, b, c):
+            x.xfrc_applied[:] = xfrc.ravel()
+            x.qpos[:], x.qvel[:], x.ctrl[:], x.qacc_warmstart[:] = d.qpos, d.qvel, d.ctrl, d.qacc_warmstart
+            x.forward()
+        assert a.nefc == b.nefc and a.nefc > 24
+        scale = max(1.0, np.abs(a.qacc_smooth).max())
+        assert np.abs(a.qacc - b.qacc).max() <= 1e-5 * scale, np.abs(a.qacc - b.qacc).max()
+        assert 1 <= b.niter < 20000
+        assert 1 <= c.niter <= 100
+        # (100 sweeps do not reach the optimum on the light cube's dofs: Gauss-Seidel's
+        # slow tail, which MuJoCo's PGS has as well)
+        assert np.all(np.isfinite(c.qacc))
+        checked += a.ncon > 0
+    assert checked >= 3
+
+
 @pytest.mark.parametrize("tilt", [5.0, 10.0, 15.0, 25.0, 30.0])
 def test_oracle_inclined_plane_friction_kat(oracle_mod, tilt):
     """Contact physics against a physical law rather than the restatement: a cube on a
