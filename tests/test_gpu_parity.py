@@ -986,6 +986,39 @@ def test_bimanual_forward_parity(gpu, oracle_mod, bimanual_setup):
     assert with_contacts >= 3
 
 
+def test_bimanual_pgs_forward(gpu, oracle_mod, bimanual_setup):
+    """PGS at MuJoCo's defaults on the two-hand scene (nv 54: M^-1 J_r' by the LDS
+    Cholesky, not the sweep's inverse): kernel vs the oracle's PGS, one forward pass.
+    A state whose contact set ties (MPR's choice under fp32 rounding) is held to the
+    same bound on the GPU's own contacts (dxo_set_contacts)."""
+    cm, xfrc, _, states, _ = bimanual_setup
+    pg = cm.with_solver("PGS")
+    om = oracle_mod.OracleModel(blob.pack(pg.arrays))
+    phys = _load_states(gpu, gpu.Model(pg), xfrc, states)
+    phys.debug(True)
+    phys.forward()
+    phys.sync()
+    con = phys.debug_get("contact")
+    qacc = phys.qacc
+    phys.close()
+    errs = []
+    for e, st in enumerate(states):
+        ds = _oracle_pair(oracle_mod, om, pg, xfrc, st)
+        sc = max(1.0, np.abs(ds[0].qacc_smooth).max())
+        err = min((np.abs(qacc[e] - d.qacc) for d in ds), key=lambda x: x.max())
+        if err.max() > PGS_BIMANUAL_HAND * sc:
+            gc = con[e, : (con[e, :, 15] != 0).sum()]
+            err = np.abs(qacc[e] - _qacc_on_gpu_contacts(oracle_mod, om, xfrc, st, gc))
+        errs.append((err[:48].max() / sc, err[48:].max() / sc))
+    errs = np.array(errs)
+    print(f"bimanual PGS: |qacc| err / scale, hands max {errs[:, 0].max():.2e}, cube max {errs[:, 1].max():.2e}")
+    assert errs[:, 0].max() <= PGS_BIMANUAL_HAND and errs[:, 1].max() <= PGS_BIMANUAL_CUBE
+
+
+# measured (r4): hands max 4.0e-6, cube max 9.6e-4 of the scale (the cube's contact
+# points, as Newton's bimanual bound)
+PGS_BIMANUAL_HAND, PGS_BIMANUAL_CUBE = 5e-5, 3e-3
+
 BIMANUAL_TIE_ERR = []
 
 
