@@ -111,6 +111,8 @@ def main():
         env_config("3 reorient.state_dense", "reorient", "state_dense", 4096),
         env_config("3' reorient.state_dense, CG solver at MuJoCo's defaults", "reorient", "state_dense", 4096,
                    solver="CG"),
+        env_config("3'' reorient.state_dense, PGS solver at MuJoCo's defaults", "reorient", "state_dense", 4096,
+                   solver="PGS"),
         bimanual(),
     ]
     for o in out:
