@@ -2506,15 +2506,15 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
   SYNC();
 }
 
-// Dense row r of J into Jd (lane d: dof d), from the rows' compact forms (jac_rows).
+// Entry (r, LANE) of J (lane d: dof d, 0 past nv), from the rows' compact forms (jac_rows).
 template <class Ctx>
-__device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
+__device__ __forceinline__ float pgs_jrow(const Ctx& c, int r) {
   const DevModel& m = c.mdl();
   const int nv = c.nv;
   const int mt = ((const int*)c.f(c.L.efc_meta))[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
+  float v = 0.f;
   if (LANE < nv) {
     const int d = LANE;
-    float v = 0.f;
     if (type == DXR_FRIC) {
       v = d == id ? 1.f : 0.f;
     } else if (type == DXR_LIMJ) {
@@ -2536,8 +2536,14 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
         }
       }
     }
-    Jd[d] = v;
   }
+  return v;
+}
+// Dense row r of J into Jd (LDS)
+template <class Ctx>
+__device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
+  const float v = pgs_jrow(c, r);
+  if (LANE < c.nv) Jd[LANE] = v;
   SYNC();
 }
 
@@ -2600,6 +2606,62 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
   if (!keep)
     for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
   SYNC();
+  if (inv) {
+    // nv <= 30: the sweep's M^-1 row of dof d in lane d's registers, qacc[d] in lane d,
+    // J_r built in registers (lane d: entry d), so a row update is a DPP dot product, a
+    // few scalars and, for a changed force, M^-1 J_r' from 30 readlanes -- no LDS round
+    // trip on the chain from one row to the next
+    float mi[30];
+    const int d = min(LANE, nv - 1);
+#pragma unroll
+    for (int k = 0; k < 30; k++) {
+      const int kc = min(k, nv - 1);
+      const float t = T[ti(max(d, kc)) + min(d, kc)];
+      mi[k] = LANE < nv && k < nv ? t : 0.f;
+    }
+    float qa = LANE < nv ? qacc[LANE] : 0.f;
+    auto minv_row = [&](float jr) {
+      float u0 = 0.f, u1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < 30; k += 2) {
+        u0 = fmaf(mi[k], rl(jr, k), u0);
+        u1 = fmaf(mi[k + 1], rl(jr, k + 1), u1);
+      }
+      return u0 + u1;
+    };
+    for (int r = 0; r < nefc; r++) {
+      const float jr = pgs_jrow(c, r);
+      const float sr = wave_sum(jr * minv_row(jr));
+      if (LANE == 0) ard[r] = sr + 1.0f / D[r];
+    }
+    SYNC();
+    int it = 0;
+    for (; it < c.iterations;) {
+      stage_count(c, CNT_NEWTON_IT);
+      float impr = 0.f;
+      for (int r = 0; r < nefc; r++) {
+        const float jr = pgs_jrow(c, r);
+        const int ty = meta[r] & 15;
+        const float fo = f[r], ar = ard[r], ra = aref[r], dr = D[r], fr = ty == DXR_FRIC ? fl[r] : 0.f;
+        const float res = wave_sum(jr * qa) - ra + fo / dr;
+        float fn = fo - res / ar;
+        fn = ty == DXR_FRIC ? fminf(fr, fmaxf(-fr, fn)) : fmaxf(fn, 0.f);
+        const float dl = fn - fo;
+        if (dl != 0.f) {
+          qa = fmaf(dl, minv_row(jr), qa);
+          if (LANE == 0) f[r] = fn;
+          impr -= 0.5f * ar * dl * dl + dl * res;
+        }
+      }
+      it++;
+      if (scale * impr < tol) break;
+    }
+    if (LANE < nv) qacc[LANE] = qa;
+    for (int r = LANE; r < nefc; r += DX_WAVE) jar[r] = -f[r] / D[r];
+    if (LANE == 0) c.I[I_NITER] = it;
+    SYNC();
+    return;
+  }
   // AR's diagonal: J_r M^-1 J_r' + R_r
   for (int r = 0; r < nefc; r++) {
     pgs_row(c, r, Jd);
