@@ -278,8 +278,9 @@ def main():
             "data": "synthetic: random actions within ctrlrange, device RNG; cube spawn/goals per reorient.py",
             "config": {
                 "workload": "reorient.state_dense, Shadow hand + cube, full contact + Newton solver",
-                # MuJoCo's default and the only solver the reference's scenes run; CG is
-                # tools/bench_configs.py's config 3' line; PGS is not built
+                # MuJoCo's default and the only solver the reference's scenes run (no
+                # solver= anywhere in their MJCF); CG and PGS (config 3' / 3'') are
+                # tools/bench_configs.py lines, each with its own kernel specialization
                 "solver": "Newton",
                 "envs_per_gpu": B,
                 "global_envs": world * B,

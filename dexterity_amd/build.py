@@ -25,7 +25,7 @@ SOURCES = ("dx_step.hip", "dx_ik.hip", "dx_task.hip", "dx_sensor.hip", "dx_api.h
 HEADERS = ("dx_internal.h", "dx_device.h", "dx_task.h")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 DIMS = ("nq", "nv", "nbody", "njnt", "nu", "ntendon", "nsite", "nlevel", "nroot", "nfric", "nlimj", "nlimt",
-        "nbpair", "any_damping", "disable_contact", "iterations")  # dx_step.hip DX_DIMS
+        "nbpair", "any_damping", "disable_contact", "iterations", "solver")  # dx_device.h DX_DIMS
 
 
 def _stale() -> bool:
@@ -50,6 +50,7 @@ FLAGS = (
     "-fno-slp-vectorize", "-fgpu-flush-denormals-to-zero",
 )
 OBJ = os.path.join(ROOT, "build", "obj")
+SOLVER_SPECS = ("shadow_reorient",)  # scenes specialised for CG and PGS too (spec_text)
 
 
 def _spec_names() -> list:
@@ -119,8 +120,10 @@ def _compile_locked(out: str, verbose: bool) -> None:
             os.remove(old)
 
 
-def spec_text(lib_path: str) -> str:
+def spec_text(lib_path: str, dims: tuple = DIMS, solver_specs: tuple = None) -> str:
     """dx_specs.inc for every asset, from the layout the library at lib_path computes."""
+    if solver_specs is None:
+        solver_specs = SOLVER_SPECS
     import ctypes
 
     import numpy as np
@@ -135,9 +138,18 @@ def spec_text(lib_path: str) -> str:
     L.dx_model_free.argtypes = [ctypes.c_void_p]
     L.dx_model_layout.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32]
     seen = {}
+    models = []
     for path in sorted(glob.glob(os.path.join(ROOT, "assets", "*.npz"))):
         name = os.path.splitext(os.path.basename(path))[0]
-        data = blob_mod.pack(CompiledModel.load(path).arrays)
+        cm = CompiledModel.load(path)
+        models.append((name, cm))
+        # the headline scene also with the two other solvers at MuJoCo's defaults
+        # (BASELINE config 3 names "PGS"; <option solver=...>): their own kernels, so the
+        # Newton kernel carries neither (the solver is a specialization dimension)
+        if name in solver_specs:
+            models += [(f"{name}_{sv.lower()}", cm.with_solver(sv)) for sv in ("CG", "PGS")]
+    for name, cm in models:
+        data = blob_mod.pack(cm.arrays)
         m = L.dx_model_load(data, len(data))
         if not m:
             continue
@@ -151,12 +163,14 @@ def spec_text(lib_path: str) -> str:
     lines = ["// generated by dexterity_amd/build.py from assets/*.npz -- do not edit"]
     names = []
     for key, name in seen.items():
-        nl = len(key) - len(DIMS)
+        nl = len(key) - len(dims)
         ident = "DxSpec_" + "".join(ch if ch.isalnum() else "_" for ch in name)
         names.append(ident)
         lines.append(f"struct {ident} {{")
         lines.append(f"  static constexpr Lds L = {{{', '.join(str(v) for v in key[:nl])}}};")
-        lines.append("  static constexpr int " + ", ".join(f"{d} = {v}" for d, v in zip(DIMS, key[nl:])) + ";")
+        lines.append("  static constexpr int " + ", ".join(f"{d} = {v}" for d, v in zip(dims, key[nl:])) + ";")
+        # a reach scene's kernel carries the reach sampling pass (dx_step.hip fused_reach_prep)
+        lines.append(f"  static constexpr bool reach_task = {'true' if 'reach' in name else 'false'};")
         lines.append("};")
     lines.append("#define DX_SPECS(X) " + " ".join(f"X({n})" for n in names))
     del np
@@ -172,7 +186,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     # process: this one may load libdx.so afterwards)
     text = subprocess.run(
         [sys.executable, "-c", f"import sys; sys.path.insert(0, {ROOT!r}); "
-         f"from dexterity_amd.build import spec_text; sys.stdout.write(spec_text({tmp!r}))"],
+         f"from dexterity_amd.build import spec_text; sys.stdout.write(spec_text({tmp!r}, {DIMS!r}, {SOLVER_SPECS!r}))"],
         check=True, capture_output=True, text=True).stdout
     old = open(SPECS).read() if os.path.exists(SPECS) else ""
     if text != old:

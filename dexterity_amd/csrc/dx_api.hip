@@ -722,16 +722,20 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   if (getenv("DX_PRINT_LDS"))
     fprintf(stderr, "dx: LDS per env %d B (step kernel), %d B (mid tier), %d B (overflow tier)\n", m->lds.total * 4,
             m->lds_mid.total * 4, m->lds_hi.total * 4);
-  m->ncon_max = DX_NCON_HI;
-  m->nefc_max = m->lds_hi.nefc_max;
+  // the contact tiers exist only for a model that can have contacts (dx_batch_create
+  // allocates the deferral lists and launches the tiers for those only): a contact-free
+  // model is held to the step kernel's layout alone
+  const bool tiers = !d.disable_contact && d.ngpair > 0;
+  m->ncon_max = tiers ? DX_NCON_HI : DX_NCON_MAX;
+  m->nefc_max = tiers ? m->lds_hi.nefc_max : m->lds.nefc_max;
   // line-search register slots (dx_step.hip DX_LS_SLOTS: 5 in the step kernel, 20 in the
   // overflow tier)
-  if (m->lds.nefc_max > 5 * 64 || m->lds_hi.nefc_max > 20 * 64) {
+  if (m->lds.nefc_max > 5 * 64 || (tiers && m->lds_hi.nefc_max > 20 * 64)) {
     fail(DX_ELIMIT, "constraint row capacity exceeds the line search's register slots");
     delete m;
     return nullptr;
   }
-  if (m->lds.total * 4 > 160 * 1024 || m->lds_hi.total * 4 > 160 * 1024) {
+  if (m->lds.total * 4 > 160 * 1024 || (tiers && m->lds_hi.total * 4 > 160 * 1024)) {
     fail(DX_ELIMIT, "per-env LDS footprint exceeds 160 KiB");
     delete m;
     return nullptr;
@@ -812,17 +816,17 @@ extern "C" int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[
 }
 
 // Layout export for build.py's kernel specialization: the Lds struct (words, in
-// declaration order) followed by the 16 dimensions of dx_step.hip DX_DIMS.
+// declaration order) followed by the 17 dimensions of dx_device.h DX_DIMS.
 extern "C" int dx_model_layout(const dx_model* m, int32_t* out, int32_t n) {
   if (!m || !out) return fail(DX_EINVAL, "null argument");
   const int nl = (int)(sizeof(Lds) / sizeof(int));
   const DevModel& d = m->dm;
-  int dims[16] = {d.nq, d.nv, d.nbody, d.njnt, d.nu, d.ntendon, d.nsite, d.nlevel, d.nroot,
-                  d.nfric, d.nlimj, d.nlimt, d.nbpair, d.any_damping, d.disable_contact, d.iterations};
-  if (n < nl + 16) return fail(DX_EINVAL, "output too small");
+  int dims[17] = {d.nq, d.nv, d.nbody, d.njnt, d.nu, d.ntendon, d.nsite, d.nlevel, d.nroot,
+                  d.nfric, d.nlimj, d.nlimt, d.nbpair, d.any_damping, d.disable_contact, d.iterations, d.solver};
+  if (n < nl + 17) return fail(DX_EINVAL, "output too small");
   memcpy(out, &m->lds, sizeof(Lds));
   memcpy(out + nl, dims, sizeof(dims));
-  return nl + 16;
+  return nl + 17;
 }
 
 extern "C" int dx_model_lds_bytes(const dx_model* m) {
@@ -1022,6 +1026,7 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   B.epoch = 0;
   // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
+  B.xcd_local = B.nqueue == DX_QUEUES && getenv("DX_XCD_LOCAL") ? atoi(getenv("DX_XCD_LOCAL")) : 0;
   B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
   B.defer_at = getenv("DX_DEFER_AT") ? atoi(getenv("DX_DEFER_AT")) : DX_NCON_MAX;  // (tests / probes)
   B.order_last = getenv("DX_ORDER_LAST") ? atoi(getenv("DX_ORDER_LAST")) : 1;
@@ -1736,15 +1741,20 @@ extern "C" int dx_env_obs_dim(const dx_env* e) { return e ? e->P.obs_dim : fail(
 extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const float* ctrlrange, uint64_t seed,
                                                     int step, int env0, float* out);
 
-// One control step.  Reorient runs its task logic fused into the step kernel (task_pre
-// in each env's first physics-step task, task_post in its last; dx_task.h), so a control
-// step is the step kernel plus the overflow tier's launch.  Reach keeps the task kernels
-// around its sampling pass (DX_NO_FUSE=1 selects them for reorient too).
+// One control step.  The task logic runs fused into the step kernel (task_pre in each
+// env's first physics-step task, task_post in its last; dx_task.h): a reorient control step
+// is the step kernel plus the overflow tier's launch.  Reach (a reach scene's
+// specialization) also runs its sampling pass -- goal rollouts, joint sampling -- in the
+// env's first task (dx_step.hip fused_reach_prep): the step kernel plus the order kernel
+// (contact-free Shadow reach) or the overflow tier (Adroit).  DX_NO_FUSE=1 selects the
+// task kernels and the separate sampling launch instead.
 // random: actions drawn in the kernel by the random agent (seed, step) instead of read.
 static int env_run(dx_env* e, const float* action, bool random = false, uint64_t seed = 0, int step = 0) {
   dx_batch* b = e->batch;
   HIPCHK(hipSetDevice(b->device));
-  if (e->P.kind == DX_KIND_REORIENT && !getenv("DX_NO_FUSE") && b->db.defer) {
+  const bool fuse = !getenv("DX_NO_FUSE") && ((e->P.kind == DX_KIND_REORIENT && b->db.defer) ||
+                                              (e->P.kind == DX_KIND_REACH && b->spec >= 0 && dx_spec_reach(b->spec)));
+  if (fuse) {
     DevBatch& B = b->db;
     const int* skip = B.skip;
     B.fuse = 1;

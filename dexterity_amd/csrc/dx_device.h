@@ -198,8 +198,10 @@ __device__ __forceinline__ float dot6(const float* a, const float* b) {
 // bounds are constants, and far fewer scalar registers stay live (the generic
 // kernel spills its ~60 layout/dimension scalars into VGPR lanes).
 #define DX_DIMS(X) X(nq) X(nv) X(nbody) X(njnt) X(nu) X(ntendon) X(nsite) X(nlevel) X(nroot) \
-  X(nfric) X(nlimj) X(nlimt) X(nbpair) X(any_damping) X(disable_contact) X(iterations)
-struct SpecRT {};
+  X(nfric) X(nlimj) X(nlimt) X(nbpair) X(any_damping) X(disable_contact) X(iterations) X(solver)
+struct SpecRT {
+  static constexpr bool reach_task = false;  // (the generic kernel: no fused reach sampling pass)
+};
 // Stages take the model through c.mdl().  (Laundering that reference per stage, so
 // each stage re-loads its table pointers instead of the kernel keeping ~100 of them
 // live, cut the SGPR spills 408 -> 331 but not the step time; it is a plain

@@ -76,7 +76,7 @@ enum { DXR_FRIC = 0, DXR_LIMJ = 1, DXR_LIMT = 2, DXR_CON = 3, DXR_CONFL = 4 };
 struct DevModel {
   int nq, nv, nbody, njnt, ngeom, nsite, nu, ntendon, nwrap, nbpair, ngpair;
   int iterations, disable_contact, any_damping, nlevel, nroot, nfric, nlimj, nlimt;
-  int solver;  // [3P] mjtSolver: 1 CG, 2 Newton (default)
+  int solver;  // [3P] mjtSolver: 0 PGS, 1 CG, 2 Newton (default)
   float timestep, tolerance, impratio, meaninertia;
   float gravity[3];
   // bodies
@@ -162,6 +162,11 @@ struct DevBatch {
   unsigned epoch;
   int nqueue;
   int* qerr;
+  // XCD-local queues (DX_XCD_LOCAL): a workgroup claims only from its own XCD's queue (no
+  // stealing), so every task of an env runs under one L2 and the hand-off record and the
+  // task logic's stores between an env's tasks are plain (L2-resident) instead of
+  // write-through.  Deferrals to the mid tier stay write-through (it may run on any XCD).
+  int xcd_local;
   // the state an env's task hands to its next substep's task: [nenv][hand_stride]
   // floats = qpos | qvel | warm start | time | cost so far | nstep | flags, each record on
   // whole 128-B lines (hand_stride a multiple of 32), so a hand-off writes back and reads
@@ -184,7 +189,8 @@ struct DevBatch {
   // group-size invisibility test forces either layout)
   int np_wide;
   // physics steps deferred by the step kernel (dx_step.hip env_defer): [0] the count, [1]
-  // unused, [2 ..] entries (DX_DEFER_*), emptied by the overflow kernel's last workgroup
+  // the epoch of the queued launch that published the entries (the mid tier claims only its
+  // own launch's), [2 ..] entries (DX_DEFER_*), emptied by the overflow kernel's last workgroup
   unsigned* defer;
   // with the mid tier running beside a queued launch (mid = 1): the step kernel publishes
   // each deferral (state in the env's hand-off record, entry | DX_DEFER_VALID stored after
@@ -207,12 +213,13 @@ struct DevBatch {
   uint64_t act_seed;
   // Longest-first dispatch order for the next launch, built without a kernel of its own:
   // an env's last task of a launch that sets onext counts its cost bucket in
-  // ohist[opar][256] (descending cost) and keeps its rank in okey[env] (bucket << 16 |
-  // rank); the overflow tier's launch then places every env at its bucket's prefix +
+  // ohist[opar][256] (descending cost) and keeps its rank in okey[env] (bucket <<
+  // DX_OKEY_RANK_BITS | rank); the overflow tier's launch then places every env at its bucket's prefix +
   // rank in `order` and its last workgroup zeroes ohist[opar] and the queue heads.
   unsigned *ohist, *okey;
   int opar, onext;
 };
+#define DX_OKEY_RANK_BITS 24  // rank within a cost bucket: a whole batch (nenv <= 2^20) fits one bucket
 // deferral entries: env (bits 0-19) | physics step << 20 (bits 20-27) | flags
 #define DX_DEFER_ENV_BITS 20
 #define DX_DEFER_FWD (1u << 28)      // forward only (dx_forward)
@@ -384,6 +391,7 @@ __device__ __forceinline__ float dx_urand(uint64_t seed, int env, int episode, i
 
 // dx_step.hip: specialized-kernel lookup and launch (host side)
 int dx_spec_find(const DevModel& d, const Lds& L);
+bool dx_spec_reach(int spec);  // the specialization fuses the reach sampling pass
 int dx_step_occupancy(int spec, size_t lds);
 hipError_t dx_launch_step(int spec, int grid, size_t lds, hipStream_t stream, const DevModel* mdev, const DevBatch& B,
                           const Lds& L, int nsub, int mode);

@@ -2729,7 +2729,9 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   SYNC();
   float gw = 0.f;
   float cw = eval_cost(c, qacc, Ma, &gw);
-  if (m.solver == 0) {  // the dual solver starts from the warm start's forces
+  // c.solver is a compile-time constant in a scene specialization (DX_DIMS), so a Newton
+  // kernel carries no CG / PGS code
+  if (c.solver == 0) {  // the dual solver starts from the warm start's forces
     stage_count(c, CNT_SOLVE);
     stage_count(c, CNT_NEFC, nefc);
     solve_pgs(c, scale, tol);
@@ -2751,7 +2753,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   stage_mark(c, ST_NEWTON_EVAL);
   stage_count(c, CNT_SOLVE);
   stage_count(c, CNT_NEFC, nefc);
-  if (m.solver == 1) {
+  if (c.solver == 1) {
     solve_cg(c, scale, tol);
     return;
   }
@@ -3160,8 +3162,11 @@ __device__ __forceinline__ double mtw_normal(MtWave& w, int n, double loc, doubl
 // one environment, with the reference's side effects on the physics state: after a
 // goal draw qpos and ctrl are restored, qvel / warm start keep the last rollout's
 // values, time advances by the accepted rollout (a rejected one restores it).
-template <class Ctx>
+// WT: fused into the queued step kernel (fused_reach_prep), where the task state this
+// writes is read by the env's last task, which may run on another XCD: write-through.
+template <bool WT = false, class Ctx>
 __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int env, float& time) {
+  using W = TaskStore<WT>;
   const TaskParams& P = *B.tp;
   const TaskState& T = *B.ts;
   float* qpos = c.f(c.L.qpos);
@@ -3244,22 +3249,22 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       gc = tip_coord(c, P);
       // fingertip_position.py:99-103: the accepted goal's joints are the state after
       // the two steps (kept as FingertipCartesianPosition.qpos; the last draw if none)
-      if (T.goal_qpos && LANE < nq) T.goal_qpos[(size_t)env * nq + LANE] = qpos[LANE];
+      if (T.goal_qpos && LANE < nq) W::st(T.goal_qpos, (size_t)env * nq + LANE, qpos[LANE]);
       if (!contact_now(c)) { ok = true; break; }
       time = t0;
       SYNC();
       if (LANE == 0) c.I[I_NSTEP] = n0;
     }
-    if (LANE < 3 * P.ntips) T.goal[(size_t)env * P.goal_dim + LANE] = gc;
+    if (LANE < 3 * P.ntips) W::st(T.goal, (size_t)env * P.goal_dim + LANE, gc);
     if (LANE == 0) {
-      T.goalnum[env] = g + 1;
-      T.goalfail[env] += fails + (ok ? 0 : 1);  // GoalInitializationErrors the reference raised (and retried)
+      W::st(T.goalnum, env, g + 1);
+      W::st(T.goalfail, env, T.goalfail[env] + fails + (ok ? 0 : 1));  // GoalInitializationErrors the reference raised (and retried)
       // GoalTask.initialize_episode / before_step bookkeeping (task.py:137-165)
-      T.counter[env] = 0;
-      T.exceeded[env] = 0;
-      T.registered[env] = 0;
-      T.solve_start[env] = time;
-      T.solve_n[env] = c.I[I_NSTEP];  // the fp64 start (task_post): the goal's physics step
+      W::st(T.counter, env, 0);
+      W::st(T.exceeded, env, 0);
+      W::st(T.registered, env, 0);
+      W::st(T.solve_start, env, time);
+      W::st(T.solve_n, env, c.I[I_NSTEP]);  // the fp64 start (task_post): the goal's physics step
     }
     if (LANE < nq) qpos[LANE] = q_init;
     if (LANE < nu) ctrl[LANE] = c_init;
@@ -3284,7 +3289,7 @@ __device__ __forceinline__ void reach_prep(const Ctx& c, const DevBatch& B, int 
       if (!contact_now(c)) break;
     }
   }
-  if (LANE == 0) T.need[env] = 0;
+  if (LANE == 0) W::st(T.need, env, 0);
   SYNC();
 }
 
@@ -3365,7 +3370,8 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
 // The hand-off record (DevBatch::hand) of a task whose env has substeps left: lane t
 // gathers words 4t .. 4t + 3 from LDS and writes them with one 16-byte sc1 store.
 template <class Ctx>
-__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int stride, float time, unsigned cost) {
+__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int stride, float time, unsigned cost,
+                                               bool wt = true) {
   const float* qpos = c.f(c.L.qpos);
   const float* qvel = c.f(c.L.qvel);
   const float* ws = c.f(c.L.v5);
@@ -3382,7 +3388,8 @@ __device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int str
            : m < c.nq + 2 * c.nv ? ws[m - c.nq - c.nv]
            : k == 0 ? time : k == 1 ? __uint_as_float(cost) : k == 2 ? __int_as_float(nstep) : __int_as_float(flags);
     }
-    st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
+    if (wt) st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
+    else *(float4*)(rec + 4 * t) = make_float4(w[0], w[1], w[2], w[3]);  // XCD-local queue: L2-resident
   }
 }
 
@@ -3535,7 +3542,7 @@ __device__ __forceinline__ void order_key(const DevBatch& B, int env, unsigned c
   if (B.onext && LANE == 0) {
     const unsigned b = 255u - min(cost >> 4, 255u);
     const unsigned r = atomicAdd(B.ohist + 256 * B.opar + b, 1u);
-    B.okey[env] = b << 16 | r;
+    B.okey[env] = b << DX_OKEY_RANK_BITS | r;  // 24-bit rank: every env of a batch (<= 2^20) in one bucket
   }
 }
 
@@ -3563,6 +3570,13 @@ __device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int e
     env_store_state(c, B, env, rl(time, 0));
   }
   if (LANE == 0) {
+    // the launch that owns the list's entries (list[1]): the mid tier claims only its own
+    // launch's (defer_claim), so a mid tier that starts while an earlier launch's step
+    // kernel still publishes leaves those entries to that launch's overflow tier
+    if (publish) {
+      __hip_atomic_store(list + 1, B.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const unsigned k = atomicAdd(list, 1u);
     if (publish)
       __hip_atomic_store(list + 2 + k, val | DX_DEFER_VALID, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3581,9 +3595,16 @@ __device__ __forceinline__ void env_defer(const Ctx& c, const DevBatch& B, int e
 // launch runs, or the overflow tier after it, should the mid tier not have run (a
 // profiler or a shared hardware queue serialising the two streams) -- takes an entry by
 // compare-and-swap.  Lane 0: 1 taken (*e its value), 2 taken by the other consumer, 0 not
-// published yet.
-__device__ __forceinline__ int defer_claim(unsigned* list, unsigned i, unsigned* e) {
+// published yet (or, epoch != 0: published by another launch than `epoch`, list[1] --
+// the mid tier runs only its own launch's entries, with its own launch's arguments).
+// The claim compares the whole entry, so an entry read before the overflow tier reset the
+// list and republished by the next launch is taken only if it is that launch's same entry.
+__device__ __forceinline__ int defer_claim(unsigned* list, unsigned i, unsigned* e, unsigned epoch = 0u) {
   unsigned v = __hip_atomic_load(list + 2 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (epoch && (v & DX_DEFER_VALID)) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__hip_atomic_load(list + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) return 0;
+  }
   for (;;) {
     if (!(v & DX_DEFER_VALID)) return 0;
     if (v & DX_DEFER_CLAIMED) return 2;
@@ -3632,6 +3653,28 @@ __device__ __forceinline__ void fused_post(const Ctx& c, const DevBatch& B, int 
   task_post(P, S, B, env, LANE, skip, (c.I[I_FLAGS] & 1) != 0, c.I[I_NSTEP]);
 }
 
+// Fused reach (DevBatch::fuse, a reach scene's specialization): after task_pre, an env
+// that requested a goal or initial joints (S.need, set by task_pre) runs the sampling pass
+// (reach_prep: goal rollouts, joint sampling) right here, in its first physics-step task,
+// instead of in a mode-2 launch of its own; the state it leaves goes through the batch
+// arrays and is reloaded into a zeroed LDS block, as the separate pass hands it to the
+// step kernel, so the result is the unfused one bit for bit.  Returns the env's time.
+template <class Ctx>
+__device__ __forceinline__ float fused_reach_prep(Ctx& c, const DevBatch& B, int env, float time) {
+  const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
+  int need = 0;
+  if (LANE == 0) need = S.need[env];
+  if (!__builtin_amdgcn_readfirstlane(need)) return time;
+  const bool defer = c.defer;
+  c.defer = false;  // (the sampling pass keeps its pool and cuts it, as mode 2 does)
+  reach_prep<true>(c, B, env, time);
+  c.defer = defer;
+  env_store_state(c, B, env, rl(time, 0));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  return env_begin(c, B, env);
+}
+
 // mode 0: nsub x (forward + Euler), then observe;  mode 1: forward only (+observe)
 // mode 2: reach sampling pass (goal rollouts / joint sampling), state out only
 template <class SP>
@@ -3660,6 +3703,8 @@ __device__ __forceinline__ void step_body(const DevModel& m, const DevBatch& B, 
   const bool fuse = B.fuse && mode == 0;
   int skip = fuse ? fused_pre(c, B, env) : (B.skip && B.skip[env]);
   float time = env_begin(c, B, env);
+  if constexpr (SP::reach_task)
+    if (fuse) time = fused_reach_prep(c, B, env, time);
   const int steps = skip ? 0 : mode == 0 ? nsub : 1;  // a freshly reset env is only observed
   for (int s = 0; s < steps; s++) {
     if (mode == 0) {
@@ -3731,7 +3776,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= nq * (unsigned)nsub) {
-      if (++empty >= nqueue) break;
+      if (B.xcd_local || ++empty >= nqueue) break;  // (XCD-local: no claims from other XCDs' queues)
       q = q + 1 == nqueue ? 0 : q + 1;
       continue;
     }
@@ -3784,6 +3829,8 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       skip = B.fuse ? fused_pre(c, B, env) : (B.skip && B.skip[env]);
     }
     float time = env_begin(c, B, env, s > 0 ? rec : nullptr);
+    if constexpr (SP::reach_task)
+      if (s == 0 && B.fuse) time = fused_reach_prep(c, B, env, time);
     if (!skip && !(s > 0 && !B.fuse && B.skip && B.skip[env])) env_substep(c, B, time, env, s == nsub - 1);
     if (c.I[I_DEFER]) {
       env_defer(c, B, env, s, false, time);
@@ -3803,7 +3850,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       const unsigned lcost = tcost * (unsigned)nsub;
       order_key(B, env, skip || !B.order_last ? cost : B.order_last == 1 ? lcost : (cost >> 1) + (lcost >> 1));
     } else {
-      env_store_hand(c, rec, B.hand_stride, time, cost);
+      env_store_hand(c, rec, B.hand_stride, time, cost, !B.xcd_local);
     }
     // publish: the bytes the env's next task must read (the hand-off record) were
     // stored write-through (sc1), so a drained vmcnt suffices and no release fence (a
@@ -3905,11 +3952,11 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
     for (int base = e0; base < e1; base += DX_WAVE) {  // uniform trip count (the shuffles)
       const int e = base + LANE;
       const unsigned key = e < e1 ? B.okey[e] : 0u;
-      const int b = (int)(key >> 16);
+      const int b = (int)(key >> DX_OKEY_RANK_BITS);
       const unsigned p0 = __shfl(pre[0], b >> 2, 64), p1 = __shfl(pre[1], b >> 2, 64);
       const unsigned p2 = __shfl(pre[2], b >> 2, 64), p3 = __shfl(pre[3], b >> 2, 64);
       const unsigned p = (b & 3) == 0 ? p0 : (b & 3) == 1 ? p1 : (b & 3) == 2 ? p2 : p3;
-      if (e < e1) ((int*)B.order)[p + (key & 0xffffu)] = e;
+      if (e < e1) ((int*)B.order)[p + (key & ((1u << DX_OKEY_RANK_BITS) - 1u))] = e;
     }
   }
   // 2. the deferred physics steps.  Beside a mid-tier launch: first the step kernel's
@@ -3934,8 +3981,8 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
     if (B.fuse) fused_post(c, B, env, false);
     if (LANE == 0) __hip_atomic_fetch_add(B.qdone + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
+  int ok = 1;
   if (B.mid) {
-    int ok = 1;
     if (LANE == 0) {
       for (unsigned w = 0; __hip_atomic_load(B.qdone + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < n1; w++) {
         __builtin_amdgcn_s_sleep(4);
@@ -3943,10 +3990,13 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (!__shfl(ok, 0, 64)) return;
+    ok = __shfl(ok, 0, 64);
   }
+  // (a timed-out wait skips the second list -- its entries may not be complete; qerr[0]
+  // reports the launch -- but still counts this workgroup below, so the last one resets
+  // the launch-to-launch state and later launches start from clean lists)
   unsigned* list = B.mid ? B.defer2 : B.defer;
-  const unsigned n = list ? list[0] : 0u;
+  const unsigned n = list && ok ? list[0] : 0u;
   for (unsigned i = blockIdx.x; i < n; i += gridDim.x) {
     const unsigned e = list[2 + i];
     const int env = defer_env(e), s0 = defer_step(e);
@@ -4031,7 +4081,7 @@ dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned cnt = __hip_atomic_load(B.defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (i < cnt) {
-          const int r = defer_claim(B.defer, i, &e);
+          const int r = defer_claim(B.defer, i, &e, B.epoch);
           if (r == 1) { got = 1; break; }
           if (r == 2) { i++; continue; }  // the overflow tier took it
         } else if (done) {
@@ -4130,6 +4180,16 @@ int dx_step_occupancy(int spec, size_t lds) {
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dx_step_kernel, 64, lds) != hipSuccess) n = 0;
   return n;
+}
+
+// Whether specialization `spec` carries the fused reach sampling pass (fused_reach_prep).
+bool dx_spec_reach(int spec) {
+  int k = 0;
+#define DX_REACH(SP) if (spec == k) return SP::reach_task; k++;
+  DX_SPECS(DX_REACH)
+#undef DX_REACH
+  (void)k;
+  return false;
 }
 
 // Index of the specialization whose layout and dimensions equal the model's, or -1.

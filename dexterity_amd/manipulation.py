@@ -371,10 +371,13 @@ class GoalEnvironment:
             arrays[name] = a.reshape(self.num_envs, -1) if name not in ("mt_env", "mt_goal") else a.reshape(-1, self.num_envs)
         meta = np.array([self.num_envs, self.model.nq, self.model.nv, self.model.nu, self.obs_dim, self.env_offset],
                         dtype=np.int64)
-        np.savez(path, __meta__=meta, **arrays)
+        # the random agent's key (dx_env_step_random / sample_actions draw from it), so a
+        # load into an env created with another seed continues the same action stream
+        np.savez(path, __meta__=meta, __agent_seed__=np.array([self._seed], dtype=np.int64), **arrays)
 
     def load(self, path: str) -> None:
-        """Restores a checkpoint written by `save` (same task, model and num_envs)."""
+        """Restores a checkpoint written by `save` (same task, model and num_envs),
+        including the random agent's key."""
         L = _lib.load()
         with np.load(path, allow_pickle=False) as z:
             meta = z["__meta__"]
@@ -382,6 +385,8 @@ class GoalEnvironment:
             if list(meta) != want:
                 raise ValueError(f"checkpoint is for (num_envs, nq, nv, nu, obs_dim, env_offset) = {list(meta)}, "
                                  f"this env is {want}")
+            if "__agent_seed__" in z.files:
+                self._seed = int(z["__agent_seed__"][0])
             fields = self._state_fields()
             nbytes = sum(nb for _, _, nb in fields)
             buf = np.empty(nbytes, dtype=np.uint8)

@@ -292,6 +292,45 @@ def test_fused_task_logic_matches_task_kernels(built, monkeypatch):
             np.testing.assert_array_equal(a, b)
 
 
+@pytest.mark.parametrize("domain", ["reach_shadow", "reach"])
+def test_fused_reach_matches_task_kernels(built, domain, monkeypatch):
+    """Reach with its task logic and sampling pass fused into the step kernel (task_pre,
+    goal rollouts / joint sampling in an env's first physics-step task, task_post in its
+    last: dx_step.hip fused_reach_prep) equals the task kernels around a separate sampling
+    launch (DX_NO_FUSE=1) bit for bit -- resets with their goal and initial-joint draws,
+    goal changes, rewards, observations and the physics state -- over 512 envs x 40
+    control steps, for the contact-free Shadow reach (BASELINE config 2: the step kernel
+    and the order kernel, 2 launches per control step) and the Adroit reach (contacts,
+    the overflow tier).  A 0.3 s time limit ends every episode after 12 control steps, so
+    the sampling pass also runs inside later control steps (auto-resets), not only at
+    the first."""
+    from dexterity_amd import _lib, manipulation
+
+    n = 512
+    outs = []
+    for variant in ("kernels", "fused"):
+        if variant == "kernels":
+            monkeypatch.setenv("DX_NO_FUSE", "1")
+        else:
+            monkeypatch.delenv("DX_NO_FUSE", raising=False)
+        env = manipulation.load(domain, "state_dense", seed=17, num_envs=n, time_limit=0.3)
+        env.reset()
+        sts = []
+        for i in range(40):
+            env.step_random(i)
+            sts.append(env._read(_lib.OUT_STEP_TYPE, np.int32, 1)[:, 0])
+        ts = env.timestep()
+        outs.append((np.stack(sts), ts.reward, ts.discount,
+                     np.concatenate([v.reshape(n, -1) for v in ts.observation.values()], axis=1),
+                     env.physics.qpos, env.physics.qvel, env.physics.get(_lib.TIME), env.goals(), env.successes(),
+                     env.goal_failures()))
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        env.close()
+    assert (outs[0][0] == 2).sum() >= n and (outs[0][0] == 0).sum() >= n  # episodes ended and restarted
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("domain", ["reorient", "reach"])
 def test_checkpoint_resume_is_bit_exact(built, domain, tmp_path):
     """Checkpoint / resume: a run saved after control step 10 and resumed
@@ -328,8 +367,8 @@ def test_checkpoint_resume_is_bit_exact(built, domain, tmp_path):
     a.close()
     b = manipulation.load(domain, task, seed=99, num_envs=n)
     b.reset()
-    b._seed = 21  # the random agent's key (dx_env_step_random) is the caller's, as in the run
-    b.load(path)
+    b.load(path)  # restores the random agent's key (seed 21) too
+    assert b._seed == 21
     sb = run(b, range(10, 25))
     got = outputs(b)
     b.close()

@@ -516,24 +516,32 @@ def _contact_lists_agree(d, recs, cm=None, deep=None):
     normal of a shallow or rounded contact is not pinned tighter than this.  Returns
     (None or the first disagreement, tie contacts).
 
-    Deep mesh-mesh contacts (|dist| > 1 mm; `cm` and the list `deep` given): MPR stops on a
-    portal within its tolerance of the Minkowski boundary, and for a deep overlap of two
-    rounded hulls fp32 and fp64 can stop on different portals, either closer to the true
-    minimum penetration.  Such a contact is accepted, and appended to `deep`, when its
+    Deep mesh-mesh contacts (|dist| > 0.1 mm; `cm` and the list `deep` given): MPR stops
+    on a portal within its tolerance of the Minkowski boundary, and for a deep overlap of
+    two rounded hulls fp32 and fp64 can stop on different portals, either closer to the
+    true minimum penetration.  Such a contact is accepted, and appended to `deep`, when its
     depth is within 3 % of the geoms' minimum penetration depth (_min_penetration, fp64),
-    i.e. when it is as good an answer as MPR gives."""
+    i.e. when it is as good an answer as MPR gives -- or when its portal lies on the
+    Minkowski boundary: the fp64 separation of the two hulls along the GPU's own normal
+    equals the GPU's depth (within max(2e-5 m, 3 %)), i.e. the GPU's (normal, depth) is
+    an exact support-based answer, a terminal portal of MPR from another start (deep
+    finger-finger overlaps of the two-hand scene, where MPR's answer is discontinuous)."""
     oc = d.contacts()
     ties = 0
 
     def deep_ok(r, o):
-        if cm is None or deep is None or abs(o[12]) <= 1e-3:
+        if cm is None or deep is None or abs(o[12]) <= 1e-4:
             return False
         g1, g2 = int(o[13]), int(o[14])
         if int(cm.geom_type[g1]) != 7 or int(cm.geom_type[g2]) != 7:
             return False
         pen = _min_penetration(cm, d, g1, g2, (r[3:6], o[3:6]))
         if abs(r[12] - pen) <= 0.03 * abs(pen):
-            deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(pen)))
+            deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(pen), "min"))
+            return True
+        sep = _separation(cm, d, g1, g2, r[3:6])
+        if abs(sep - r[12]) <= max(2e-5, 0.03 * abs(r[12])):
+            deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(sep), "boundary"))
             return True
         return False
 
@@ -583,6 +591,60 @@ def _oracle_on_contacts(oracle_mod, om, x32, st, recs, gqacc):
     d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = (np.asarray(x, dtype=np.float64) for x in st)
     d.step()
     return d.qpos.copy(), d.qvel.copy(), excess
+
+
+def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label):
+    """The full-batch accounting of test_full_batch_parity: every env's GPU step (gq, gv)
+    against the oracle's from the same fp32 state (oq, ov); a state outside the tight bound
+    (qpos 1e-6, qvel 5e-4 of the scale) must be explained as an MPR discontinuity, contact
+    geometry or solver resolution.  Returns (tight mask, category counts, tie contacts,
+    deep mesh-mesh contacts, unexplained states)."""
+    qpos, qvel, ws, ctrl = states
+    gq, gv, gqacc, con, scale, oq, ov = gpu_out
+    eq = np.abs(gq - oq).max(axis=1)
+    ev = np.abs(gv - ov).max(axis=1) / scale
+    tight = (eq <= 1e-6) & (ev <= 5e-4)
+    kinds = {"perturbed": 0, "geometry": 0, "solver": 0}
+    ties = 0
+    deep = []  # deep mesh-mesh contacts judged on geometry (_contact_lists_agree)
+    unexplained = []
+    for e in np.flatnonzero(~tight):
+        st = (qpos[e], qvel[e], ws[e], ctrl[e])
+        pq, pv = _nearest_perturbed(oracle_mod, om, x32, st, 1, gq[e], gv[e], scale[e])
+        if pq <= 1e-6 and pv <= 5e-4:
+            kinds["perturbed"] += 1
+            continue
+        recs = con[e][con[e][:, 15] != 0]
+        cq, cv, excess = _oracle_on_contacts(oracle_mod, om, x32, st, recs, gqacc[e])
+        sq, sv = np.abs(cq - gq[e]).max(), np.abs(cv - gv[e]).max() / scale[e]
+        # the oracle's contacts at the state, else at one of its perturbations at fp32
+        # resolution -- of the input (6e-8) and of the fp32 forward kinematics that places
+        # the geoms (1e-6: seven-level chains of fp32 transforms) -- since MPR's path, and
+        # so its normal and depth, is discontinuous in the input
+        rng = np.random.RandomState(int(e))
+        for p in range(33):
+            rel = 6e-8 if p <= 16 else 1e-6
+            pst = st if p == 0 else (qpos[e] * (1 + rng.standard_normal(qpos.shape[1]) * rel),
+                                     qvel[e] * (1 + rng.standard_normal(qvel.shape[1]) * rel), ws[e], ctrl[e])
+            why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, pst), recs)
+            if why is None:
+                break
+        if why is not None:  # at the state itself, with deep mesh-mesh contacts judged on geometry
+            dp = []
+            why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, compiled, dp)
+            deep += dp
+        if why is None and sq <= 1e-6 and sv <= 5e-4:
+            kinds["geometry"] += 1
+            ties += t
+        elif why is None and excess <= 1e-7 and sv <= 5e-4 and sq <= h * 5e-4 * scale[e]:
+            kinds["solver"] += 1
+        else:
+            unexplained.append((int(e), float(eq[e]), float(sq), float(sv), float(excess), why))
+    print(f"{label} full batch: {(~tight).sum()} of {len(qpos)} states outside the tight bound (max qpos err {eq.max():.2e}, "
+          f"max qvel err / scale {ev.max():.2e}; tight set {eq[tight].max():.2e} / {ev[tight].max():.2e}); {kinds}, "
+          f"{ties} tie contacts; deep mesh-mesh contacts on geometry (pair, GPU dist, oracle dist, fp64 minimum "
+          f"penetration or separation along the GPU normal, rule) {deep}; unexplained {unexplained[:10]}")
+    return tight, kinds, ties, deep, unexplained
 
 
 def test_full_batch_parity(gpu, oracle_mod):
@@ -647,50 +709,13 @@ def test_full_batch_parity(gpu, oracle_mod):
     rc, oq, ov, _ = oracle_mod.batch_step(om, qpos.astype(np.float64), qvel.astype(np.float64),
                                           ctrl.astype(np.float64), ws.astype(np.float64), x32, nsub=1)
     assert rc == 0
-    eq = np.abs(gq - oq).max(axis=1)
-    ev = np.abs(gv - ov).max(axis=1) / scale
-    tight = (eq <= 1e-6) & (ev <= 5e-4)
-    kinds = {"perturbed": 0, "geometry": 0, "solver": 0}
-    ties = 0
-    deep = []  # deep mesh-mesh contacts judged on geometry (_contact_lists_agree)
-    unexplained = []
-    for e in np.flatnonzero(~tight):
-        st = (qpos[e], qvel[e], ws[e], ctrl[e])
-        pq, pv = _nearest_perturbed(oracle_mod, om, x32, st, 1, gq[e], gv[e], scale[e])
-        if pq <= 1e-6 and pv <= 5e-4:
-            kinds["perturbed"] += 1
-            continue
-        recs = con[e][con[e][:, 15] != 0]
-        cq, cv, excess = _oracle_on_contacts(oracle_mod, om, x32, st, recs, gqacc[e])
-        sq, sv = np.abs(cq - gq[e]).max(), np.abs(cv - gv[e]).max() / scale[e]
-        # the oracle's contacts at the state, else at one of its perturbations at fp32
-        # resolution -- of the input (6e-8) and of the fp32 forward kinematics that places
-        # the geoms (1e-6: seven-level chains of fp32 transforms) -- since MPR's path, and
-        # so its normal and depth, is discontinuous in the input
-        rng = np.random.RandomState(int(e))
-        for p in range(33):
-            rel = 6e-8 if p <= 16 else 1e-6
-            pst = st if p == 0 else (qpos[e] * (1 + rng.standard_normal(qpos.shape[1]) * rel),
-                                     qvel[e] * (1 + rng.standard_normal(qvel.shape[1]) * rel), ws[e], ctrl[e])
-            why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, pst), recs)
-            if why is None:
-                break
-        if why is not None:  # at the state itself, with deep mesh-mesh contacts judged on geometry
-            dp = []
-            why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, model.compiled, dp)
-            deep += dp
-        if why is None and sq <= 1e-6 and sv <= 5e-4:
-            kinds["geometry"] += 1
-            ties += t
-        elif why is None and excess <= 1e-7 and sv <= 5e-4 and sq <= h * 5e-4 * scale[e]:
-            kinds["solver"] += 1
-        else:
-            unexplained.append((int(e), float(eq[e]), float(sq), float(sv), float(excess), why))
-    print(f"full batch: {(~tight).sum()} of {n} states outside the tight bound (max qpos err {eq.max():.2e}, "
-          f"max qvel err / scale {ev.max():.2e}; tight set {eq[tight].max():.2e} / {ev[tight].max():.2e}); {kinds}, "
-          f"{ties} tie contacts; deep mesh-mesh contacts on geometry (pair, GPU dist, oracle dist, fp64 minimum "
-          f"penetration) {deep}; unexplained {unexplained[:10]}")
-    assert (~tight).mean() <= 0.1
+    tight, kinds, ties, deep, unexplained = _account_full_batch(
+        oracle_mod, om, model.compiled, x32, h, (qpos, qvel, ws, ctrl), (gq, gv, gqacc, con, scale, oq, ov), "reorient")
+    # pinned near the measured rates (round 4, this state mix: 212 of 4096 outside the
+    # tight bound -- 172 perturbed, 38 geometry, 2 solver, 0 unexplained), so a regression
+    # in any category shows
+    assert (~tight).mean() <= 0.07
+    assert kinds["perturbed"] <= 240 and kinds["geometry"] <= 60 and kinds["solver"] <= 8, kinds
     assert not unexplained
     assert len(deep) <= max(2, n // 1000)
 
@@ -829,6 +854,60 @@ def test_contact_tiers_are_invisible(gpu, monkeypatch):
         for a, b in zip(outs[0], o):
             differ |= (np.asarray(a).reshape(1024, -1) != np.asarray(b).reshape(1024, -1)).any(axis=1)
         assert differ.sum() == 0, np.flatnonzero(differ)
+
+
+def test_mixed_launches_with_deferrals(gpu, monkeypatch):
+    """Deferral entries belong to their launch (list[1] = the launch's epoch; the mid tier
+    claims only its own launch's entries, with its own nsub and task-logic mode): fused
+    5-substep control steps alternating with raw 1- and 3-substep physics launches, every
+    contact step deferred (DX_DEFER_AT=0), are bit-identical with and without the mid tier
+    (DX_NO_MID=1: every entry run by its own launch's overflow tier)."""
+    from dexterity_amd import manipulation
+
+    n = 512
+    outs = []
+    for env_vars in ({"DX_DEFER_AT": "0"}, {"DX_DEFER_AT": "0", "DX_NO_MID": "1"}):
+        monkeypatch.delenv("DX_NO_MID", raising=False)
+        for k, v in env_vars.items():
+            monkeypatch.setenv(k, v)
+        env = manipulation.load("reorient", "state_dense", seed=8, num_envs=n)
+        env.reset()
+        for step in range(9):
+            env.step_random(step)
+            env.physics.step(1 + 2 * (step % 2))  # no task logic, another nsub
+        env.physics.sync()
+        h = env.physics.health()
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        assert h["contact_overflow"] == 0 and h["diverged"] == 0
+        assert h["contact_deferred"] > 500, h
+        outs.append((env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART),
+                     env.timestep().reward, env.physics.get(_lib.TIME)))
+        env.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_order_key_beyond_16_bit_rank(gpu):
+    """The longest-first order keeps an env's rank within its cost bucket in 24 bits: after
+    a reset every env of a 70,000-env batch is an observe-only env of about the same cost
+    (one bucket, > 65,536 ranks), and the next launches must still run every env exactly
+    once.  Env e's trajectory does not depend on the batch size or the order, so the first
+    1,024 envs equal a 1,024-env batch of the same seed bit for bit."""
+    from dexterity_amd import manipulation
+
+    outs = []
+    for n in (70000, 1024):
+        env = manipulation.load("reorient", "state_dense", seed=13, num_envs=n)
+        env.reset()
+        for step in range(4):
+            env.step_random(step)
+        env.physics.sync()
+        assert env.physics.debug_get("queue_timeouts")[0] == 0
+        outs.append((env.physics.qpos[:1024], env.physics.qvel[:1024], env.timestep().reward[:1024],
+                     env.physics.get(_lib.TIME)[:1024]))
+        env.close()
+    for a, b in zip(*outs):
+        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
 
 
 def _check_reach_rewards(env, ts, dense):
@@ -1036,9 +1115,8 @@ def test_bimanual_forward_parity_wide_sample(gpu, oracle_mod, bimanual_setup):
     assert ties <= 1
 
 
-def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
-    """One substep vs the oracle (qpos 1e-6), then BASELINE config 5 at full size:
-    4096 envs x 20 control steps of random actions stay finite and in contact."""
+def test_bimanual_substep(gpu, oracle_mod, bimanual_setup):
+    """One substep vs the oracle (qpos 1e-5)."""
     cm, xfrc, om, states, model = bimanual_setup
     phys = _load_states(gpu, model, xfrc, states)
     phys.step(1)
@@ -1049,6 +1127,16 @@ def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
         d.qpos[:], d.qvel[:], d.qacc_warmstart[:], d.ctrl[:] = st
         d.step()
         assert np.abs(qpos[e] - d.qpos).max() < 1e-5
+
+
+def test_bimanual_full_batch_parity(gpu, oracle_mod, bimanual_setup):
+    """BASELINE config 5 at full size with test_full_batch_parity's accounting: 4096
+    two-hand envs (nv 54: the LDS Cholesky path; the 64- and 256-contact tiers at the
+    scene's contact counts) after 20 control steps of random actions from randomised cube
+    positions; every env's fp32 state then takes one physics step on the GPU and in the
+    fp64 oracle, and every state outside the tight bound is explained (MPR discontinuity,
+    contact geometry or solver resolution), none left."""
+    cm, xfrc, om, _, model = bimanual_setup
     n = 4096
     big = gpu.BatchedPhysics(model, n)
     big.set_xfrc(xfrc)
@@ -1060,8 +1148,37 @@ def test_bimanual_substep_and_batch(gpu, oracle_mod, bimanual_setup):
     for step in range(20):
         big.set(_lib.CTRL, rng.uniform(lo, hi, size=(n, cm.nu)).astype(np.float32))
         big.step(5)
-    assert np.all(np.isfinite(big.qpos)) and np.all(np.isfinite(big.qvel))
+    qpos, qvel = big.qpos, big.qvel
+    ws, ctrl = big.get(_lib.QACC_WARMSTART), big.get(_lib.CTRL)
+    assert np.all(np.isfinite(qpos)) and np.all(np.isfinite(qvel))
     assert (big.get(_lib.NCON)[:, 0] > 0).mean() > 0.5
+    h = big.health()
+    assert h["contact_overflow"] == 0 and h["diverged"] == 0, h
+    assert big.debug_get("queue_timeouts")[0] == 0
+    big.debug(True)
+    big.forward()
+    scale = np.maximum(1.0, np.abs(big.debug_get("qacc_smooth")).max(axis=1))
+    con = big.debug_get("contact").astype(np.float64)
+    gqacc = big.qacc.astype(np.float64)
+    for f, v in ((_lib.QPOS, qpos), (_lib.QVEL, qvel), (_lib.QACC_WARMSTART, ws)):
+        big.set(f, v)
+    big.debug(False)
+    big.step(1)
+    gq, gv = big.qpos, big.qvel
+    big.close()
+    x32 = np.asarray(xfrc, dtype=np.float32).astype(np.float64).ravel()
+    rc, oq, ov, _ = oracle_mod.batch_step(om, qpos.astype(np.float64), qvel.astype(np.float64),
+                                          ctrl.astype(np.float64), ws.astype(np.float64), x32, nsub=1)
+    assert rc == 0
+    tight, kinds, ties, deep, unexplained = _account_full_batch(
+        oracle_mod, om, cm, x32, float(cm.timestep), (qpos, qvel, ws, ctrl), (gq, gv, gqacc, con, scale, oq, ov),
+        "bimanual")
+    # measured (round 5): 275 of 4096 outside the tight bound -- 234 perturbed, 34
+    # geometry, 3 solver -- with 9 deep finger-finger contacts judged on geometry
+    assert (~tight).mean() <= 0.09
+    assert kinds["perturbed"] <= 320 and kinds["geometry"] <= 60 and kinds["solver"] <= 8, kinds
+    assert not unexplained
+    assert len(deep) <= 16
 
 
 def test_cg_solver_parity(gpu, oracle_mod, reorient_setup):

@@ -99,24 +99,27 @@ def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
 
 
 def main():
+    """Every config, or (arguments) only those whose key is given: 1 1' 2 2' 3 3' 3'' 5."""
     import torch  # noqa: F401  (one HIP runtime for torch and libdx)
 
     from bench import cpu_baseline_reach_1env
 
-    out = [
-        {"config": "1 reach (Shadow hand, contacts disabled), 1 env, CPU", **cpu_baseline_reach_1env(4.0, "shadow")},
-        {"config": "1' reach (Adroit hand), 1 env, CPU", **cpu_baseline_reach_1env(4.0, "adroit")},
-        env_config("2 reach_shadow.state_dense (no contacts)", "reach_shadow", "state_dense", 1024),
-        env_config("2' reach.state_dense (Adroit)", "reach", "state_dense", 1024),
-        env_config("3 reorient.state_dense", "reorient", "state_dense", 4096),
-        env_config("3' reorient.state_dense, CG solver at MuJoCo's defaults", "reorient", "state_dense", 4096,
-                   solver="CG"),
-        env_config("3'' reorient.state_dense, PGS solver at MuJoCo's defaults", "reorient", "state_dense", 4096,
-                   solver="PGS"),
-        bimanual(),
-    ]
-    for o in out:
-        print(json.dumps(o), flush=True)
+    runs = {
+        "1": lambda: {"config": "1 reach (Shadow hand, contacts disabled), 1 env, CPU",
+                      **cpu_baseline_reach_1env(4.0, "shadow")},
+        "1'": lambda: {"config": "1' reach (Adroit hand), 1 env, CPU", **cpu_baseline_reach_1env(4.0, "adroit")},
+        "2": lambda: env_config("2 reach_shadow.state_dense (no contacts)", "reach_shadow", "state_dense", 1024,
+                                steps=400, warmup=40),
+        "2'": lambda: env_config("2' reach.state_dense (Adroit)", "reach", "state_dense", 1024, steps=200),
+        "3": lambda: env_config("3 reorient.state_dense", "reorient", "state_dense", 4096),
+        "3'": lambda: env_config("3' reorient.state_dense, CG solver at MuJoCo's defaults", "reorient",
+                                 "state_dense", 4096, solver="CG"),
+        "3''": lambda: env_config("3'' reorient.state_dense, PGS solver at MuJoCo's defaults", "reorient",
+                                  "state_dense", 4096, solver="PGS"),
+        "5": bimanual,
+    }
+    for k in (sys.argv[1:] or list(runs)):
+        print(json.dumps(runs[k]()), flush=True)
 
 
 if __name__ == "__main__":

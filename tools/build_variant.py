@@ -34,6 +34,10 @@ if rev:
         open(os.path.join(src, f), "wb").write(data)
 else:
     shutil.copytree(B.CSRC, src)
+# a revision from before the solver became a specialization dimension (round 5)
+if "X(solver)" not in open(os.path.join(src, "dx_device.h")).read():
+    B.DIMS = tuple(d for d in B.DIMS if d != "solver")
+    B.SOLVER_SPECS = ()
 # csrc includes "../../include/dx.h"
 os.makedirs(os.path.join(ROOT, "variants", "include"), exist_ok=True)
 shutil.copy(os.path.join(ROOT, "include", "dx.h"), os.path.join(ROOT, "variants", "include", "dx.h"))
