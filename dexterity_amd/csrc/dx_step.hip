@@ -19,6 +19,7 @@
 // parity-tested against) and DESIGN.md §3.
 #include "dx_device.h"
 #include "dx_task.h"
+#include <utility>
 
 // 16-byte write-through (sc1) store into a per-env block whose base is wave-uniform:
 // the substep queue hands these bytes to the env's next task without a release fence
@@ -122,40 +123,45 @@ __device__ __forceinline__ void expand_portal(const MPoint& P0, MPoint& P1, MPoi
   msel(P2, v4, to2);
   msel(P3, v4, to3);
 }
-__device__ __forceinline__ float tri_origin_dist2(const float* a, const float* b, const float* c, float* q) {
-  float ab[3], ac[3], ap[3];
-  sub3(ab, b, a); sub3(ac, c, a);
-  ap[0] = -a[0]; ap[1] = -a[1]; ap[2] = -a[2];
-  float d1 = dot3(ab, ap), d2 = dot3(ac, ap);
-  if (d1 <= 0 && d2 <= 0) { q[0] = a[0]; q[1] = a[1]; q[2] = a[2]; return dot3(q, q); }
-  float bp[3] = {-b[0], -b[1], -b[2]};
-  float d3 = dot3(ab, bp), d4 = dot3(ac, bp);
-  if (d3 >= 0 && d4 <= d3) { q[0] = b[0]; q[1] = b[1]; q[2] = b[2]; return dot3(q, q); }
-  float vc = d1 * d4 - d3 * d2;
-  if (vc <= 0 && d1 >= 0 && d3 <= 0) {
-    float v = d1 / (d1 - d3);
+// Closest point q of triangle abc to the origin and its squared distance (Ericson 5.1.5,
+// the oracle's tri_point_dist2), computed in T.  MPR's final portal at a deep overlap
+// can be a sliver whose Voronoi-region tests (d1 d4 - d3 d2, ...) cancel in fp32 and pick
+// an edge or vertex over the face: a wrong normal and a depth past the closest point
+// (bimanual finger-finger contacts at 2-6 mm, test_bimanual_full_batch_parity).  The
+// exit runs once per penetrating pair, so it runs in fp64.
+template <class T>
+__device__ __forceinline__ float tri_origin_dist2_t(const float* af, const float* bf, const float* cf, float* qf) {
+  const T a[3] = {af[0], af[1], af[2]}, b[3] = {bf[0], bf[1], bf[2]}, c[3] = {cf[0], cf[1], cf[2]};
+  T q[3];
+  const T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+  auto dot = [](const T* x, const T* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+  const T ap[3] = {-a[0], -a[1], -a[2]}, bp[3] = {-b[0], -b[1], -b[2]}, cp[3] = {-c[0], -c[1], -c[2]};
+  const T d1 = dot(ab, ap), d2 = dot(ac, ap);
+  const T d3 = dot(ab, bp), d4 = dot(ac, bp);
+  const T d5 = dot(ab, cp), d6 = dot(ac, cp);
+  const T vc = d1 * d4 - d3 * d2, vb = d5 * d2 - d1 * d6, va = d3 * d6 - d5 * d4;
+  if (d1 <= 0 && d2 <= 0) {
+    q[0] = a[0]; q[1] = a[1]; q[2] = a[2];
+  } else if (d3 >= 0 && d4 <= d3) {
+    q[0] = b[0]; q[1] = b[1]; q[2] = b[2];
+  } else if (vc <= 0 && d1 >= 0 && d3 <= 0) {
+    const T v = d1 / (d1 - d3);
     for (int k = 0; k < 3; k++) q[k] = a[k] + v * ab[k];
-    return dot3(q, q);
-  }
-  float cp[3] = {-c[0], -c[1], -c[2]};
-  float d5 = dot3(ab, cp), d6 = dot3(ac, cp);
-  if (d6 >= 0 && d5 <= d6) { q[0] = c[0]; q[1] = c[1]; q[2] = c[2]; return dot3(q, q); }
-  float vb = d5 * d2 - d1 * d6;
-  if (vb <= 0 && d2 >= 0 && d6 <= 0) {
-    float w = d2 / (d2 - d6);
+  } else if (d6 >= 0 && d5 <= d6) {
+    q[0] = c[0]; q[1] = c[1]; q[2] = c[2];
+  } else if (vb <= 0 && d2 >= 0 && d6 <= 0) {
+    const T w = d2 / (d2 - d6);
     for (int k = 0; k < 3; k++) q[k] = a[k] + w * ac[k];
-    return dot3(q, q);
-  }
-  float va = d3 * d6 - d5 * d4;
-  if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
-    float w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+  } else if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) {
+    const T w = (d4 - d3) / ((d4 - d3) + (d5 - d6));
     for (int k = 0; k < 3; k++) q[k] = b[k] + w * (c[k] - b[k]);
-    return dot3(q, q);
+  } else {
+    const T denom = T(1) / (va + vb + vc);
+    const T v = vb * denom, w = vc * denom;
+    for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
   }
-  float denom = 1.0f / (va + vb + vc);
-  float v = vb * denom, w = vc * denom;
-  for (int k = 0; k < 3; k++) q[k] = a[k] + ab[k] * v + ac[k] * w;
-  return dot3(q, q);
+  for (int k = 0; k < 3; k++) qf[k] = (float)q[k];
+  return (float)dot(q, q);
 }
 __device__ __forceinline__ void find_pos(const MPoint& P0, const MPoint& P1, const MPoint& P2, const MPoint& P3,
                                          float* pos) {
@@ -609,7 +615,7 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
     return 1;
   if (ph == 4 && stop) {
     float cl[3];
-    float d2 = tri_origin_dist2(v1, v2, v3, cl);
+    float d2 = tri_origin_dist2_t<double>(v1, v2, v3, cl);
     depth = sqrtf(d2);
     if (depth > 1e-20f) {
       float sc = 1.0f / depth;
@@ -2547,6 +2553,15 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
   SYNC();
 }
 
+#ifndef DX_PGS_AR
+#define DX_PGS_AR 64  // PGS on AR in registers (one column per lane) up to this many rows
+#endif
+// f(std::integral_constant<int, I>) for I in the sequence, unrolled: a register array
+// indexed by I stays in registers
+template <class F, int... I>
+__device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
 // [3P] MuJoCo's PGS (mj_solPGS), <option solver="PGS">: projected Gauss-Seidel on the
 // dual, min_f 0.5 f'(A + R) f + f'b with A = J M^-1 J' and b = J qacc_smooth - aref;
 // friction-loss rows boxed to +-floss, limit and pyramidal contact rows f >= 0, rows in
@@ -2629,6 +2644,72 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       }
       return u0 + u1;
     };
+    if (nefc <= DX_PGS_AR) {
+      // MuJoCo's own form (mj_solPGS on efc_AR): AR = J M^-1 J' + R, lane k holding
+      // column k (a[r] = AR[r][k] = AR[k][r]) and the residual res_k = (AR f)_k + b_k
+      // (b = J qacc_smooth - aref).  A row update is then a readlane of res_r, a few
+      // uniform scalars and, for a changed force, one FMA of every lane's residual with
+      // its AR entry -- no J row, no M^-1 J_r' and no reduction on the chain from one
+      // row to the next.  The loop over rows is unrolled (AR's column index is a
+      // register name), with a uniform exit past nefc.
+      float a[DX_PGS_AR];
+      constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
+      static_for([&](auto K) { a[K.value] = 0.f; }, rows);
+      jac_vec(c, a0, jar);  // J qacc_smooth (jar's warm-start residuals were consumed above)
+      const float bk = LANE < nefc ? jar[LANE] - aref[LANE] : 0.f;
+      float fk = LANE < nefc ? f[LANE] : 0.f;
+      const float rk = LANE < nefc ? 1.0f / D[LANE] : 0.f;
+      float dg = 1.f;
+      for (int r = 0; r < nefc; r++) {
+        // column r: J (M^-1 J_r') for every row, + R_r on the diagonal
+        const float y = minv_row(pgs_jrow(c, r));
+        if (LANE < nv) u[LANE] = y;
+        SYNC();
+        jac_vec(c, u, jar);
+        float v = LANE < nefc ? jar[LANE] : 0.f;
+        if (LANE == r) { v += rk; dg = v; }
+        static_for([&](auto K) { a[K.value] = K.value == r ? v : a[K.value]; }, rows);
+      }
+      const float idg = 1.0f / dg;
+      const int mk = LANE < nefc ? meta[LANE] & 15 : 0;
+      const float flk = LANE < nefc && LANE < c.nfric ? fl[LANE] : 0.f;
+      float res = bk;
+      static_for([&](auto K) { res = K.value < nefc ? fmaf(a[K.value], rl(fk, K.value), res) : res; }, rows);
+      int it = 0;
+      for (; it < c.iterations;) {
+        stage_count(c, CNT_NEWTON_IT);
+        float impr = 0.f;
+        static_for([&](auto R) {
+          constexpr int r = R.value;
+          if (r < nefc) {
+            const float rr = rl(res, r), fo = rl(fk, r), ir = rl(idg, r);
+            const float ar = rl(dg, r), fr = rl(flk, r);
+            float fn = fo - rr * ir;
+            fn = __builtin_amdgcn_readlane(mk, r) == DXR_FRIC ? fminf(fr, fmaxf(-fr, fn)) : fmaxf(fn, 0.f);
+            const float dl = fn - fo;
+            if (dl != 0.f) {
+              res = fmaf(dl, a[r], res);
+              fk = LANE == r ? fn : fk;
+              impr -= 0.5f * ar * dl * dl + dl * rr;
+            }
+          }
+        }, rows);
+        it++;
+        if (scale * impr < tol) break;
+      }
+      // the forces, as residuals whose primal force is f_r; qacc = qacc_smooth + M^-1 J'f
+      if (LANE < nefc) {
+        f[LANE] = fk;
+        jar[LANE] = -fk / D[LANE];
+      }
+      SYNC();
+      jac_t_force(c, g);
+      minv(g, u);
+      for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i] + u[i];
+      if (LANE == 0) c.I[I_NITER] = it;
+      SYNC();
+      return;
+    }
     for (int r = 0; r < nefc; r++) {
       const float jr = pgs_jrow(c, r);
       const float sr = wave_sum(jr * minv_row(jr));

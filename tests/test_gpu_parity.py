@@ -640,6 +640,11 @@ def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label
             kinds["solver"] += 1
         else:
             unexplained.append((int(e), float(eq[e]), float(sq), float(sv), float(excess), why))
+    if unexplained:  # the states and the GPU's contacts, for a CPU-side look with the oracle
+        os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+        ids = np.array([u[0] for u in unexplained])
+        np.savez(os.path.join(ROOT, "gpurun_out", f"fullbatch_{label}_unexplained.npz"), ids=ids, qpos=qpos[ids],
+                 qvel=qvel[ids], ws=ws[ids], ctrl=ctrl[ids], con=con[ids], gq=gq[ids], gv=gv[ids], x32=x32)
     print(f"{label} full batch: {(~tight).sum()} of {len(qpos)} states outside the tight bound (max qpos err {eq.max():.2e}, "
           f"max qvel err / scale {ev.max():.2e}; tight set {eq[tight].max():.2e} / {ev[tight].max():.2e}); {kinds}, "
           f"{ties} tie contacts; deep mesh-mesh contacts on geometry (pair, GPU dist, oracle dist, fp64 minimum "

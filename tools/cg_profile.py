@@ -4,7 +4,7 @@ iteration counts per env beside the fp64 oracle's CG -- and both solvers' Newton
 same states (diagnostics for VERDICT r3 item 5: is CG's cost its iteration count, or the
 kernel's cost per iteration?).
 
-usage: python tools/cg_profile.py [nenv] [oracle_sample]   -> gpurun_out/cg_profile.log / .json
+usage: python tools/cg_profile.py [nenv] [oracle_sample] [CG|PGS]   -> gpurun_out/<solver>_profile.json
 """
 import ctypes
 import json
@@ -21,6 +21,7 @@ from oracle import oracle as O  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 NS = int(sys.argv[2]) if len(sys.argv) > 2 else 512
+SOLVER = sys.argv[3] if len(sys.argv) > 3 else "CG"
 L = _lib.load()
 out = {}
 
@@ -63,7 +64,7 @@ def stage_profile(solver, steps=5):
 
 
 log = []
-for solver in ("CG", None):
+for solver in (SOLVER, None):
     prof, st, xfrc, cm = stage_profile(solver)
     out["profile_" + (solver or "Newton")] = prof
     log.append(f"[{solver or 'Newton'}] {prof['ms_per_step']:.3f} ms/step, "
@@ -72,20 +73,24 @@ for solver in ("CG", None):
                f"{prof['counters']['newton_iter']:.2f} iterations x {prof['solver_cycles_per_iteration']:.0f} cyc, "
                f"line-search iterations {prof['counters']['linesearch_iter']:.2f}, nefc {prof['counters']['nefc']:.1f}")
     log.append("   stages: " + ", ".join(f"{k} {v:.0f}" for k, v in sorted(prof["stages"].items(), key=lambda x: -x[1])[:10]))
-    if solver == "CG":
+    if solver == SOLVER:
         states, xfrc_cg, cm_cg = st, xfrc, cm
 
 # iteration counts on the same states (the CG env's state mix): one forward (= one solve)
 qpos, qvel, ws, ctrl = states
 cm_newton = manipulation.ReOrient().compiled
 res = {}
-for name, cm in (("CG", cm_cg), ("Newton", cm_newton)):
+for name, cm in ((SOLVER, cm_cg), ("Newton", cm_newton)):
     model = physics.Model(cm)
     ph = physics.BatchedPhysics(model, B)
     ph.set_xfrc(xfrc_cg)
     for f, v in ((_lib.QPOS, qpos), (_lib.QVEL, qvel), (_lib.QACC_WARMSTART, ws), (_lib.CTRL, ctrl)):
         ph.set(f, v)
+    ph.debug(True)
     ph.forward()
+    nefc = ph.debug_get("efc_count")[:, 0]
+    log.append(f"[{name} state mix] nefc mean {nefc.mean():.1f} p50 {np.median(nefc):.0f} p99 "
+               f"{np.percentile(nefc, 99):.0f} max {nefc.max()}; > 64 rows: {(nefc > 64).mean():.4f} of the envs")
     gpu_it = ph.get(_lib.NITER)[:, 0].copy()
     gpu_qacc = ph.qacc
     ph.close()
@@ -114,4 +119,4 @@ for name, cm in (("CG", cm_cg), ("Newton", cm_newton)):
 out["iterations"] = res
 print("\n".join(log), flush=True)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-json.dump(out, open(os.path.join(ROOT, "gpurun_out", "cg_profile.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"{SOLVER.lower()}_profile.json"), "w"), indent=1)

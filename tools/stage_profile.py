@@ -12,7 +12,8 @@ from dexterity_amd import _lib, manipulation  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
-env = manipulation.load("reorient", "state_dense", seed=3, num_envs=B)
+domain = sys.argv[3] if len(sys.argv) > 3 else "reorient"  # e.g. reach_shadow (BASELINE config 2)
+env = manipulation.load(domain, "state_dense", seed=3, num_envs=B)
 L = _lib.load()
 env.reset()
 for i in range(10):
