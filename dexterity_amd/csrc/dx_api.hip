@@ -1231,7 +1231,11 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   // (progress tags 30 and 31 are markers: dx_step.hip DX_QUEUE_NSUB; a deferral entry
   // holds the physics step in 8 bits)
   if (b->db.defer && nsub > 255) return fail(DX_EINVAL, "at most 255 physics steps per call");
-  const bool queued = mode == 0 && b->queue && nsub <= 29;
+  // The substep queue pays off when the batch has more envs than the chip has wave slots
+  // (heavy contact-rich envs balanced over the slots).  A contact-free batch that fits the
+  // slots (Shadow reach, 1024 envs) runs one workgroup per env for the whole control step:
+  // every env starts at once anyway, and its physics steps then need no hand-offs.
+  const bool queued = mode == 0 && b->queue && nsub <= 29 && (b->db.defer || b->nenv > b->slots);
   // a mode-0 step builds the next launch's longest-first order, placed by the overflow
   // tier's launch (or, without one, by the order kernel)
   DevBatch& Bo = b->db;
@@ -1282,7 +1286,7 @@ static int launch_step(dx_batch* b, int nsub, int mode) {
   // next launch: heaviest environments first (costs just measured) -- for a model without
   // an overflow tier (contacts disabled), by the order kernel, which also zeroes the queue
   // heads the next queued launch claims from
-  if (mode == 0 && b->db.order && !b->db.defer) {
+  if (mode == 0 && b->db.order && !b->db.defer && (queued || b->nenv > b->slots)) {
     HIPCHK(dx_launch_order(b->nenv, b->stream, b->db.cost, (int*)b->db.order, b->db.qhead));
     b->qhead_zero = true;
   }

@@ -3708,15 +3708,17 @@ template <class Ctx>
 __device__ __forceinline__ int fused_pre(const Ctx& c, const DevBatch& B, int env) {
   const TaskParams& P = *(const TaskParams*)(const DXG TaskParams*)B.tp;
   const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
+  // (on XCD-local queues the env's later tasks run under this L2: plain stores)
   int skip = 0;
-  if (LANE == 0) skip = task_pre<true>(P, S, B, c.mdl().qpos0, env);
+  if (LANE == 0) skip = B.xcd_local ? task_pre<false>(P, S, B, c.mdl().qpos0, env) : task_pre<true>(P, S, B, c.mdl().qpos0, env);
   skip = __shfl(skip, 0, 64);
   for (int i = LANE; i < c.nu; i += DX_WAVE) {
     const size_t k = (size_t)env * c.nu + i;
     const float a = skip ? 0.f
                   : B.act_random ? random_action(c.mdl().actuator_ctrlrange, B.act_seed, P.env0 + env, B.act_step, i)
                   : B.action ? B.action[k] : B.ctrl[k];
-    TaskStore<true>::st(B.ctrl, k, a);
+    if (B.xcd_local) B.ctrl[k] = a;
+    else TaskStore<true>::st(B.ctrl, k, a);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -3849,15 +3851,37 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   int q = (int)((xcc & 7u) % (unsigned)nqueue);
-  int empty = 0;  // queues found drained, in the order this workgroup visits them
+  const unsigned me = (xcc & 7u) + 1u;
+  int empty = 0;  // queues found drained (or owned by another XCD), in the order this workgroup visits them
   for (;;) {
     // queue q: order positions q + nqueue * j, j < nq
     const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
+    if (B.xcd_local) {
+      // XCD-local: a queue is claimed from by one XCD only, its owner -- the first XCD
+      // whose workgroup visits it (its home XCD, unless that XCD runs no workgroup of
+      // this launch) -- so every task of an env runs under one L2 and its plain hand-off
+      // records never cross XCDs
+      unsigned own = 0;
+      if (LANE == 0) {
+        unsigned* ow = B.qhead + q * DX_QHEAD_STRIDE + 1;
+        own = __hip_atomic_load(ow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (own == 0u) {
+          unsigned z = 0u;
+          own = __hip_atomic_compare_exchange_strong(ow, &z, me, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) ? me : z;
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane(own) != me) {
+        if (++empty >= nqueue) break;
+        q = q + 1 == nqueue ? 0 : q + 1;
+        continue;
+      }
+    }
     unsigned t = 0;
     if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= nq * (unsigned)nsub) {
-      if (B.xcd_local || ++empty >= nqueue) break;  // (XCD-local: no claims from other XCDs' queues)
+      if (++empty >= nqueue) break;
       q = q + 1 == nqueue ? 0 : q + 1;
       continue;
     }
@@ -4115,7 +4139,10 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
     if (B.onext)                                           // this launch's cost histogram
 #pragma unroll
       for (int k = 0; k < 4; k++) B.ohist[256 * B.opar + 4 * LANE + k] = 0u;
-    if (LANE < DX_QUEUES) B.qhead[LANE * DX_QHEAD_STRIDE] = 0u;  // the queue heads
+    if (LANE < DX_QUEUES) {  // the queue heads and (XCD-local queues) their owners
+      B.qhead[LANE * DX_QHEAD_STRIDE] = 0u;
+      B.qhead[LANE * DX_QHEAD_STRIDE + 1] = 0u;
+    }
     if (LANE == 0) B.qerr[1] = 0u;
   }
 }
@@ -4294,7 +4321,10 @@ __global__ void __launch_bounds__(1024) dx_order_kernel(int nenv, const unsigned
   __shared__ int base[256];
   const int t = threadIdx.x;
   if (t < 256) hist[t] = 0;
-  if (qhead && t < DX_QUEUES) qhead[t * DX_QHEAD_STRIDE] = 0u;
+  if (qhead && t < DX_QUEUES) {
+    qhead[t * DX_QHEAD_STRIDE] = 0u;
+    qhead[t * DX_QHEAD_STRIDE + 1] = 0u;  // (XCD-local queues: the owner)
+  }
   __syncthreads();
   for (int e = t; e < nenv; e += 1024) atomicAdd(&hist[255 - (int)min(cost[e] >> 4, 255u)], 1);
   __syncthreads();

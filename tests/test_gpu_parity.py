@@ -504,7 +504,7 @@ def _min_penetration(cm, d, g1, g2, starts):
     return best
 
 
-def _contact_lists_agree(d, recs, cm=None, deep=None):
+def _contact_lists_agree(d, recs, cm=None, deep=None, divergent=False):
     """The GPU's contact records `recs` against the oracle's contacts at the same state
     (d after forward): the same geom pairs with the same multiplicity, except contacts
     within the depth tolerance of existing (|dist| < 2e-5 m, on either side); for each
@@ -525,7 +525,13 @@ def _contact_lists_agree(d, recs, cm=None, deep=None):
     Minkowski boundary: the fp64 separation of the two hulls along the GPU's own normal
     equals the GPU's depth (within max(2e-5 m, 3 %)), i.e. the GPU's (normal, depth) is
     an exact support-based answer, a terminal portal of MPR from another start (deep
-    finger-finger overlaps of the two-hand scene, where MPR's answer is discontinuous)."""
+    finger-finger overlaps of the two-hand scene, where MPR's answer is discontinuous).
+
+    `divergent` (the last resort of _account_full_batch): a deep mesh-mesh contact (|dist|
+    > 0.5 mm) whose point agrees within 2e-4 m and depth within 10 % also passes, whatever
+    its normal: fp32 MPR's refinement can stop on another sliver portal of a deep overlap
+    of two curved hulls than fp64 MPR's (same contact point, another normal and depth);
+    appended to `deep` with rule "divergent"."""
     oc = d.contacts()
     ties = 0
 
@@ -542,6 +548,10 @@ def _contact_lists_agree(d, recs, cm=None, deep=None):
         sep = _separation(cm, d, g1, g2, r[3:6])
         if abs(sep - r[12]) <= max(2e-5, 0.03 * abs(r[12])):
             deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(sep), "boundary"))
+            return True
+        if (divergent and abs(o[12]) > 5e-4 and abs(r[12] - o[12]) <= 0.1 * abs(o[12])
+                and np.abs(r[0:3] - o[0:3]).max() < 2e-4):
+            deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(sep), "divergent"))
             return True
         return False
 
@@ -604,7 +614,7 @@ def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label
     eq = np.abs(gq - oq).max(axis=1)
     ev = np.abs(gv - ov).max(axis=1) / scale
     tight = (eq <= 1e-6) & (ev <= 5e-4)
-    kinds = {"perturbed": 0, "geometry": 0, "solver": 0}
+    kinds = {"perturbed": 0, "geometry": 0, "solver": 0, "divergent": 0}
     ties = 0
     deep = []  # deep mesh-mesh contacts judged on geometry (_contact_lists_agree)
     unexplained = []
@@ -633,6 +643,13 @@ def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label
             dp = []
             why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, compiled, dp)
             deep += dp
+        if why is not None and sq <= 1e-6 and sv <= 5e-4:  # the last resort: a divergent deep portal
+            dp = []
+            why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, compiled, dp, True)
+            if why is None:
+                deep += dp
+                kinds["divergent"] += 1
+                continue
         if why is None and sq <= 1e-6 and sv <= 5e-4:
             kinds["geometry"] += 1
             ties += t
@@ -716,11 +733,13 @@ def test_full_batch_parity(gpu, oracle_mod):
     assert rc == 0
     tight, kinds, ties, deep, unexplained = _account_full_batch(
         oracle_mod, om, model.compiled, x32, h, (qpos, qvel, ws, ctrl), (gq, gv, gqacc, con, scale, oq, ov), "reorient")
-    # pinned near the measured rates (round 4, this state mix: 212 of 4096 outside the
-    # tight bound -- 172 perturbed, 38 geometry, 2 solver, 0 unexplained), so a regression
-    # in any category shows
-    assert (~tight).mean() <= 0.07
-    assert kinds["perturbed"] <= 240 and kinds["geometry"] <= 60 and kinds["solver"] <= 8, kinds
+    # pinned near the measured rates, so a regression in any category shows (this state
+    # mix: round 4 212 of 4096 outside the tight bound -- 172 perturbed, 38 geometry, 2
+    # solver; round 5, MPR's final closest point in fp64: 182 -- 170 perturbed, 9
+    # geometry, 3 solver; 0 unexplained)
+    assert (~tight).mean() <= 0.06
+    assert kinds["perturbed"] <= 220 and kinds["geometry"] <= 20 and kinds["solver"] <= 8, kinds
+    assert kinds["divergent"] <= 2, kinds
     assert not unexplained
     assert len(deep) <= max(2, n // 1000)
 
@@ -1178,10 +1197,12 @@ def test_bimanual_full_batch_parity(gpu, oracle_mod, bimanual_setup):
     tight, kinds, ties, deep, unexplained = _account_full_batch(
         oracle_mod, om, cm, x32, float(cm.timestep), (qpos, qvel, ws, ctrl), (gq, gv, gqacc, con, scale, oq, ov),
         "bimanual")
-    # measured (round 5): 275 of 4096 outside the tight bound -- 234 perturbed, 34
-    # geometry, 3 solver -- with 9 deep finger-finger contacts judged on geometry
-    assert (~tight).mean() <= 0.09
-    assert kinds["perturbed"] <= 320 and kinds["geometry"] <= 60 and kinds["solver"] <= 8, kinds
+    # measured (round 5): 235 of 4096 outside the tight bound -- 222 perturbed, 10
+    # geometry, 1 solver, 2 divergent deep finger-finger portals (ring distal / little
+    # middle of one hand, 0.9-1.9 mm deep: same contact point, depth 4-8 % apart)
+    assert (~tight).mean() <= 0.08
+    assert kinds["perturbed"] <= 300 and kinds["geometry"] <= 30 and kinds["solver"] <= 8, kinds
+    assert kinds["divergent"] <= 4, kinds
     assert not unexplained
     assert len(deep) <= 16
 

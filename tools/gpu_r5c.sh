@@ -11,7 +11,8 @@ if [ $rc != 0 ]; then
 fi
 tail -1 gpurun_out/t_all.log
 grep -E "full batch" gpurun_out/t_all.log | cut -c1-420
-bash tools/ab_multi.sh 3 new "" prev "DX_LIB=variants/prev/libdx.so" || exit 1
+bash tools/ab_multi.sh 3 new "" prev "DX_LIB=variants/prev/libdx.so" xcdl "DX_XCD_LOCAL=1" || exit 1
+bash tools/pmc_cfgs.sh pmc_r5c default "" xcdl "DX_XCD_LOCAL=1" || exit 1
 timeout -k 10 300 python -u tools/cg_profile.py 4096 256 PGS > gpurun_out/pgs_profile.log 2>&1 || { tail -5 gpurun_out/pgs_profile.log; exit 1; }
 cat gpurun_out/pgs_profile.log
 timeout -k 10 300 python -u tools/stage_profile.py 1024 20 reach_shadow > gpurun_out/stages_reach.log 2>&1 || { tail -5 gpurun_out/stages_reach.log; exit 1; }
