@@ -19,13 +19,14 @@ def built():
     build.build()
 
 
-def test_allgather_world1(built):
+@pytest.mark.parametrize("n", [64, 4096])
+def test_allgather_world1(built, n):
     """dx_allgather_obs over a one-rank RCCL communicator returns exactly the packed
     [obs | reward | discount | step_type] rows of the env (the in-place gather puts
-    rank 0's rows at offset 0)."""
+    rank 0's rows at offset 0) -- also at BASELINE config 4's shard size, 4096 x 126."""
     from dexterity_amd import distributed, manipulation
 
-    env = manipulation.load("reorient", "state_dense", seed=3, num_envs=64, device=0)
+    env = manipulation.load("reorient", "state_dense", seed=3, num_envs=n, device=0)
     comm = distributed.Comm(0, 1, 0, key=f"gputest_{os.getpid()}")
     col = distributed.OutputCollator(env, comm)
     env.reset()
@@ -35,7 +36,7 @@ def test_allgather_world1(built):
     got = col.read()
     ts = env.timestep()
     obs = np.concatenate([ts.observation[k] for k in ts.observation], axis=1).astype(np.float32)
-    assert got.shape == (64, env.obs_dim + 3)
+    assert got.shape == (n, env.obs_dim + 3)
     np.testing.assert_array_equal(got[:, : env.obs_dim], obs)
     np.testing.assert_array_equal(got[:, env.obs_dim], ts.reward.astype(np.float32))
     np.testing.assert_array_equal(got[:, env.obs_dim + 1], ts.discount.astype(np.float32))
@@ -717,15 +718,22 @@ def _shard_worker(rank, world, n, seed, steps, q):
     env.close()
 
 
-def test_sharded_job_two_processes(built):
+@pytest.mark.parametrize("n", [64, 4096])
+def test_sharded_job_two_processes(built, n, monkeypatch):
     """The sharded job of bench.py on one GPU: two processes step their own shards
     (env_offset from distributed.env_shard); their rows, placed at
-    distributed.gathered_rows, equal one process stepping the whole job."""
+    distributed.gathered_rows, equal one process stepping the whole job.  At BASELINE
+    config 4's shard size (4096 envs per rank, an 8192-env job, env_offset 4096) with
+    physics steps past 20 contacts deferred to the mid tier and past 24 to the overflow
+    tier (DX_DEFER_AT / DX_MID_DEFER_AT), so both tiers run in every rank."""
     import multiprocessing as mp
 
     from dexterity_amd import distributed, manipulation
 
-    world, n, seed, steps = 2, 64, 12345, 8
+    world, seed, steps = 2, 12345, 8
+    if n >= 4096:
+        monkeypatch.setenv("DX_DEFER_AT", "20")
+        monkeypatch.setenv("DX_MID_DEFER_AT", "24")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_shard_worker, args=(r, world, n, seed, steps, q)) for r in range(world)]
@@ -744,6 +752,9 @@ def test_sharded_job_two_processes(built):
         sl = distributed.gathered_rows(r, n)
         for k in ref:
             np.testing.assert_array_equal(ref[k][sl], got[r][k], err_msg=f"rank {r} {k}")
+    if n >= 4096:
+        h = whole.physics.health()
+        assert h["contact_deferred"] > 0 and h["contact_overflow"] == 0, h
     whole.close()
 
 
