@@ -2622,6 +2622,126 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
     for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
   SYNC();
   if (inv) {
+    if (nefc <= 2 * DX_PGS_AR) {
+      // MuJoCo's own form (mj_solPGS on efc_AR): AR = J M^-1 J' + R, lane k holding
+      // column k (a[r] = AR[r][k] = AR[k][r]) and the residual res_k = (AR f)_k + b_k
+      // (b = J qacc_smooth - aref).  A row update is then a readlane of res_r, a few
+      // uniform scalars and, for a changed force, one FMA of every lane's residual with
+      // its AR entry -- no J row, no M^-1 J_r' and no reduction on the chain from one
+      // row to the next.  The loop over rows is unrolled (AR's column index is a
+      // register name), with a uniform exit past nefc.  Past 64 rows the rows form two
+      // blocks (lane k: rows k and 64 + k), each holding its own diagonal block of AR
+      // (a[], b[]); the coupling between the blocks enters when a block's sweep starts,
+      // through its residuals recomputed from the current forces matrix-free (J (qacc_smooth
+      // + M^-1 J'f) - aref + R f) -- exactly the Gauss-Seidel sweep in row order.
+      const bool two = nefc > DX_PGS_AR;
+      float a[DX_PGS_AR], b[DX_PGS_AR];
+      constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
+      static_for([&](auto K) { a[K.value] = 0.f; b[K.value] = 0.f; }, rows);
+      const int k1 = DX_PGS_AR + LANE;  // this lane's row of the second block
+      jac_vec(c, a0, jar);  // J qacc_smooth (jar's warm-start residuals were consumed above)
+      const float bk = LANE < nefc ? jar[LANE] - aref[LANE] : 0.f;
+      float fk = LANE < nefc ? f[LANE] : 0.f, fk1 = k1 < nefc ? f[k1] : 0.f;
+      const float rk = LANE < nefc ? 1.0f / D[LANE] : 0.f, rk1 = k1 < nefc ? 1.0f / D[k1] : 0.f;
+      float dg = 1.f, dg1 = 1.f;
+      for (int r = 0; r < nefc; r++) {
+        // column r: J (M^-1 J_r') for every row, + R_r on the diagonal; kept for the rows
+        // of r's block
+        pgs_row(c, r, Jd);
+        minv(Jd, u);
+        jac_vec(c, u, jar);
+        if (r < DX_PGS_AR) {
+          float v = LANE < nefc ? jar[LANE] : 0.f;
+          if (LANE == r) { v += rk; dg = v; }
+          static_for([&](auto K) { a[K.value] = K.value == r ? v : a[K.value]; }, rows);
+        } else {
+          float v = k1 < nefc ? jar[k1] : 0.f;
+          if (k1 == r) { v += rk1; dg1 = v; }
+          static_for([&](auto K) { b[K.value] = K.value + DX_PGS_AR == r ? v : b[K.value]; }, rows);
+        }
+      }
+      const float idg = 1.0f / dg, idg1 = 1.0f / dg1;
+      // each row's projection as a box [lo, hi]: friction loss [-floss, floss], limits and
+      // pyramid edges [0, inf)
+      // (a padding row past nefc has the box [0, 0], force 0 and residual 0: its update
+      // changes nothing, so the rows go in groups of 8 with one test per group)
+      auto box = [&](int k, float& lo, float& hi) {
+        const int kc = min(k, nefc - 1);
+        const bool fr = (meta[kc] & 15) == DXR_FRIC;
+        hi = k >= nefc ? 0.f : fr ? fl[kc] : __builtin_inff();
+        lo = fr && k < nefc ? -hi : 0.f;
+      };
+      float lok, hik, lok1, hik1;
+      box(LANE, lok, hik);
+      box(k1, lok1, hik1);
+      float res = bk, res1 = 0.f;
+      // both blocks' residuals from the current forces, matrix-free
+      auto resid = [&]() {
+        if (LANE < nefc) { f[LANE] = fk; jar[LANE] = -fk / D[LANE]; }
+        if (k1 < nefc) { f[k1] = fk1; jar[k1] = -fk1 / D[k1]; }
+        SYNC();
+        jac_t_force(c, g);
+        minv(g, u);
+        for (int i = LANE; i < nv; i += DX_WAVE) u[i] += a0[i];
+        SYNC();
+        jac_vec(c, u, jar);
+        res = LANE < nefc ? jar[LANE] - aref[LANE] + fk * rk : 0.f;
+        res1 = k1 < nefc ? jar[k1] - aref[k1] + fk1 * rk1 : 0.f;
+      };
+      if (!two) static_for([&](auto K) { res = K.value < nefc ? fmaf(a[K.value], rl(fk, K.value), res) : res; }, rows);
+      // one row update (q static: a register name of a[] / b[])
+// (branch-free: an unchanged force gives dl = 0, and fma(0, x, res) = res, so the
+// residuals, the force and the improvement are those of the branch that skips it)
+#define DX_PGS_ROW(q, col, rs, fv, dgv, idgv, lov, hiv)                                                       \
+  {                                                                                                        \
+    const float rr = rl(rs, q), fo = rl(fv, q), ir = rl(idgv, q);                                          \
+    const float ar = rl(dgv, q), lo = rl(lov, q), hi = rl(hiv, q);                                         \
+    const float fn = __builtin_amdgcn_fmed3f(fo - rr * ir, lo, hi); /* min(hi, max(lo, .)), lo <= hi */   \
+    const float dl = fn - fo;                                                                              \
+    rs = fmaf(dl, col[q], rs);                                                                             \
+    fv = LANE == (q) ? fn : fv;                                                                            \
+    impr -= 0.5f * ar * dl * dl + dl * rr;                                                                 \
+  }
+      constexpr auto groups = std::make_integer_sequence<int, DX_PGS_AR / 8>{};
+      constexpr auto eight = std::make_integer_sequence<int, 8>{};
+      float impr = 0.f;
+      int it = 0;
+      for (; it < c.iterations;) {
+        stage_count(c, CNT_NEWTON_IT);
+        impr = 0.f;
+        if (two) resid();  // block 0 after the last sweep's block 1
+        static_for([&](auto G) {
+          if (8 * G.value < nefc)
+            static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, a, res, fk, dg, idg, lok, hik) }, eight);
+        }, groups);
+        if (two) {
+          resid();  // block 1 after this sweep's block 0
+          static_for([&](auto G) {
+            if (DX_PGS_AR + 8 * G.value < nefc)
+              static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, b, res1, fk1, dg1, idg1, lok1, hik1) }, eight);
+          }, groups);
+        }
+#undef DX_PGS_ROW
+        it++;
+        if (scale * impr < tol) break;
+      }
+      // the forces, as residuals whose primal force is f_r; qacc = qacc_smooth + M^-1 J'f
+      if (LANE < nefc) {
+        f[LANE] = fk;
+        jar[LANE] = -fk / D[LANE];
+      }
+      if (k1 < nefc) {
+        f[k1] = fk1;
+        jar[k1] = -fk1 / D[k1];
+      }
+      SYNC();
+      jac_t_force(c, g);
+      minv(g, u);
+      for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i] + u[i];
+      if (LANE == 0) c.I[I_NITER] = it;
+      SYNC();
+      return;
+    }
     // nv <= 30: the sweep's M^-1 row of dof d in lane d's registers, qacc[d] in lane d,
     // J_r built in registers (lane d: entry d), so a row update is a DPP dot product, a
     // few scalars and, for a changed force, M^-1 J_r' from 30 readlanes -- no LDS round
@@ -2644,72 +2764,6 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       }
       return u0 + u1;
     };
-    if (nefc <= DX_PGS_AR) {
-      // MuJoCo's own form (mj_solPGS on efc_AR): AR = J M^-1 J' + R, lane k holding
-      // column k (a[r] = AR[r][k] = AR[k][r]) and the residual res_k = (AR f)_k + b_k
-      // (b = J qacc_smooth - aref).  A row update is then a readlane of res_r, a few
-      // uniform scalars and, for a changed force, one FMA of every lane's residual with
-      // its AR entry -- no J row, no M^-1 J_r' and no reduction on the chain from one
-      // row to the next.  The loop over rows is unrolled (AR's column index is a
-      // register name), with a uniform exit past nefc.
-      float a[DX_PGS_AR];
-      constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
-      static_for([&](auto K) { a[K.value] = 0.f; }, rows);
-      jac_vec(c, a0, jar);  // J qacc_smooth (jar's warm-start residuals were consumed above)
-      const float bk = LANE < nefc ? jar[LANE] - aref[LANE] : 0.f;
-      float fk = LANE < nefc ? f[LANE] : 0.f;
-      const float rk = LANE < nefc ? 1.0f / D[LANE] : 0.f;
-      float dg = 1.f;
-      for (int r = 0; r < nefc; r++) {
-        // column r: J (M^-1 J_r') for every row, + R_r on the diagonal
-        const float y = minv_row(pgs_jrow(c, r));
-        if (LANE < nv) u[LANE] = y;
-        SYNC();
-        jac_vec(c, u, jar);
-        float v = LANE < nefc ? jar[LANE] : 0.f;
-        if (LANE == r) { v += rk; dg = v; }
-        static_for([&](auto K) { a[K.value] = K.value == r ? v : a[K.value]; }, rows);
-      }
-      const float idg = 1.0f / dg;
-      const int mk = LANE < nefc ? meta[LANE] & 15 : 0;
-      const float flk = LANE < nefc && LANE < c.nfric ? fl[LANE] : 0.f;
-      float res = bk;
-      static_for([&](auto K) { res = K.value < nefc ? fmaf(a[K.value], rl(fk, K.value), res) : res; }, rows);
-      int it = 0;
-      for (; it < c.iterations;) {
-        stage_count(c, CNT_NEWTON_IT);
-        float impr = 0.f;
-        static_for([&](auto R) {
-          constexpr int r = R.value;
-          if (r < nefc) {
-            const float rr = rl(res, r), fo = rl(fk, r), ir = rl(idg, r);
-            const float ar = rl(dg, r), fr = rl(flk, r);
-            float fn = fo - rr * ir;
-            fn = __builtin_amdgcn_readlane(mk, r) == DXR_FRIC ? fminf(fr, fmaxf(-fr, fn)) : fmaxf(fn, 0.f);
-            const float dl = fn - fo;
-            if (dl != 0.f) {
-              res = fmaf(dl, a[r], res);
-              fk = LANE == r ? fn : fk;
-              impr -= 0.5f * ar * dl * dl + dl * rr;
-            }
-          }
-        }, rows);
-        it++;
-        if (scale * impr < tol) break;
-      }
-      // the forces, as residuals whose primal force is f_r; qacc = qacc_smooth + M^-1 J'f
-      if (LANE < nefc) {
-        f[LANE] = fk;
-        jar[LANE] = -fk / D[LANE];
-      }
-      SYNC();
-      jac_t_force(c, g);
-      minv(g, u);
-      for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i] + u[i];
-      if (LANE == 0) c.I[I_NITER] = it;
-      SYNC();
-      return;
-    }
     for (int r = 0; r < nefc; r++) {
       const float jr = pgs_jrow(c, r);
       const float sr = wave_sum(jr * minv_row(jr));
@@ -3994,12 +4048,21 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
 #ifndef DX_STEP_WAVES
 #define DX_STEP_WAVES 2  // waves per SIMD the VGPR budget is set for (3: <= 168 VGPRs, measured slower)
 #endif
+// The substep queue (mode 3) is a kernel of its own: the step kernel's code -- every stage
+// inlined -- is ~0.4 MB per entry point, and one kernel holding both the queue and the
+// one-workgroup-per-env path doubled what the wave slots of a CU fetch into their shared
+// instruction cache.
 template <class SP>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DX_STEP_WAVES)))
 dx_step_kernel_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub, int mode) {
   const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
-  if (mode == 3) step_queue<SP>(m, B, L, nsub);
-  else step_body<SP>(m, B, L, nsub, mode);
+  step_body<SP>(m, B, L, nsub, mode);
+}
+template <class SP>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(DX_STEP_WAVES)))
+dx_step_kernel_queue_spec(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) {
+  const DevModel& m = *(const DevModel*)(const DXG DevModel*)mp;
+  step_queue<SP>(m, B, L, nsub);
 }
 // Mode 2 (reach goal rollouts / joint sampling) is its own kernel, so the rarely-run
 // sampling code does not share the step kernel's register allocation.
@@ -4247,13 +4310,15 @@ hipError_t dx_launch_step_mid(int grid, size_t lds, hipStream_t stream, const De
   bool dx_match_##SP(const DevModel& d, const Lds& L) { return spec_matches<SP>(d, L); }             \
   int dx_occ_##SP(size_t lds) {                                                                       \
     int n = 0;                                                                                        \
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dx_step_kernel_spec<SP>, 64, lds) != hipSuccess) n = 0; \
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, dx_step_kernel_queue_spec<SP>, 64, lds) != hipSuccess) n = 0; \
     return n;                                                                                         \
   }                                                                                                   \
   hipError_t dx_launch_##SP(int grid, size_t lds, hipStream_t stream, const DevModel* m, const DevBatch& B, \
                             const Lds& L, int nsub, int mode) {                                       \
     if (mode == 2)                                                                                    \
       hipLaunchKernelGGL(dx_prep_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L);         \
+    else if (mode == 3)                                                                               \
+      hipLaunchKernelGGL(dx_step_kernel_queue_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub);  \
     else                                                                                              \
       hipLaunchKernelGGL(dx_step_kernel_spec<SP>, dim3(grid), dim3(64), lds, stream, m, B, L, nsub, mode); \
     return hipGetLastError();                                                                         \

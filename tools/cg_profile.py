@@ -55,6 +55,12 @@ def stage_profile(solver, steps=5):
                                          "newton_linesearch", "matvec", "jacvec"))
     # the state mix the solvers are compared on
     ph = env.physics
+    cost = ph.get(_lib.STEP_COST)[:, 0].astype(np.float64) * 1024
+    ncon = ph.get(_lib.NCON)[:, 0]
+    top = np.argsort(-cost)[:12]
+    log.append(f"[{solver or 'Newton'} last step] per-env cycles p50 {np.median(cost):.3e} p99 {np.percentile(cost, 99):.3e} "
+               f"max {cost.max():.3e}; heaviest envs (cycles, ncon, niter): "
+               + ", ".join(f"({cost[e]:.2e}, {ncon[e]}, {ph.get(_lib.NITER)[e, 0]})" for e in top))
     st = (ph.qpos, ph.qvel, ph.get(_lib.QACC_WARMSTART), ph.get(_lib.CTRL))
     xfrc = t.gravity_compensation
     env.close()
