@@ -1001,7 +1001,8 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   rc |= balloc(b, (void**)&B.watch, E * 4);
   rc |= balloc(b, (void**)&B.niter, E * 4);
   rc |= balloc(b, (void**)&B.ncand, E * 4);
-  rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
+  if (!getenv("DX_NO_SEPCACHE"))  // (A/B and traffic attribution: MPR without the separating-direction cache)
+    rc |= balloc(b, (void**)&B.sepcache, E * DX_SEP_SLOTS * 16);
   rc |= balloc(b, (void**)&B.health, DX_HEALTH_WORDS * 4);
   rc |= balloc(b, (void**)&B.bad, E * 4);
   rc |= balloc(b, (void**)&B.nstep, E * 4);

@@ -3762,17 +3762,15 @@ template <class Ctx>
 __device__ __forceinline__ int fused_pre(const Ctx& c, const DevBatch& B, int env) {
   const TaskParams& P = *(const TaskParams*)(const DXG TaskParams*)B.tp;
   const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
-  // (on XCD-local queues the env's later tasks run under this L2: plain stores)
   int skip = 0;
-  if (LANE == 0) skip = B.xcd_local ? task_pre<false>(P, S, B, c.mdl().qpos0, env) : task_pre<true>(P, S, B, c.mdl().qpos0, env);
+  if (LANE == 0) skip = task_pre<true>(P, S, B, c.mdl().qpos0, env);
   skip = __shfl(skip, 0, 64);
   for (int i = LANE; i < c.nu; i += DX_WAVE) {
     const size_t k = (size_t)env * c.nu + i;
     const float a = skip ? 0.f
                   : B.act_random ? random_action(c.mdl().actuator_ctrlrange, B.act_seed, P.env0 + env, B.act_step, i)
                   : B.action ? B.action[k] : B.ctrl[k];
-    if (B.xcd_local) B.ctrl[k] = a;
-    else TaskStore<true>::st(B.ctrl, k, a);
+    TaskStore<true>::st(B.ctrl, k, a);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -3906,16 +3904,26 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   int q = (int)((xcc & 7u) % (unsigned)nqueue);
   const unsigned me = (xcc & 7u) + 1u;
-  int empty = 0;  // queues found drained (or owned by another XCD), in the order this workgroup visits them
+  const unsigned all = (1u << nqueue) - 1u;
+  unsigned gone = 0u;  // queues found drained
+  int idle = 0;        // (XCD-local) queues visited in a row without a task to take
+  unsigned naps = 0;   // (XCD-local) full passes without one, bounded like the waits below
   for (;;) {
+    if (gone == all) break;
+    if ((gone >> q) & 1u) {
+      q = q + 1 == nqueue ? 0 : q + 1;
+      continue;
+    }
     // queue q: order positions q + nqueue * j, j < nq
     const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
     if (B.xcd_local) {
-      // XCD-local: a queue is claimed from by one XCD only, its owner -- the first XCD
-      // whose workgroup visits it (its home XCD, unless that XCD runs no workgroup of
-      // this launch) -- so every task of an env runs under one L2 and its plain hand-off
-      // records never cross XCDs
-      unsigned own = 0;
+      // XCD-local: a queue has an owner XCD -- the first whose workgroup visits it (its
+      // home XCD, unless that XCD runs no workgroup of this launch) -- whose workgroups
+      // take its tasks, so an env's tasks run under one L2 and its hand-off records stay
+      // plain (L2-resident).  Only the record the last round reads is written through:
+      // once a queue is in its last round (head past (nsub - 1) rounds), workgroups of
+      // other XCDs may take its tasks too, as the tail of a launch needs
+      unsigned own = 0, late = 0;
       if (LANE == 0) {
         unsigned* ow = B.qhead + q * DX_QHEAD_STRIDE + 1;
         own = __hip_atomic_load(ow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3924,10 +3932,21 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
           own = __hip_atomic_compare_exchange_strong(ow, &z, me, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT) ? me : z;
         }
+        late = __hip_atomic_load(B.qhead + q * DX_QHEAD_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+               nq * (unsigned)(nsub - 1);
       }
-      if (__builtin_amdgcn_readfirstlane(own) != me) {
-        if (++empty >= nqueue) break;
+      if (__builtin_amdgcn_readfirstlane(own) != me && !__builtin_amdgcn_readfirstlane(late)) {
+        // another XCD's queue before its last round: come back later (every queue's owner
+        // is running, so each one reaches its last round and drains)
         q = q + 1 == nqueue ? 0 : q + 1;
+        if (++idle >= nqueue) {
+          __builtin_amdgcn_s_sleep(8);
+          idle = 0;
+          if (++naps > (1u << 22) || __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            if (LANE == 0) __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+          }
+        }
         continue;
       }
     }
@@ -3935,10 +3954,11 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
     if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= nq * (unsigned)nsub) {
-      if (++empty >= nqueue) break;
+      gone |= 1u << q;
       q = q + 1 == nqueue ? 0 : q + 1;
       continue;
     }
+    idle = 0;
     const int s = (int)(t / nq);
     const int k = q + nqueue * (int)(t - (unsigned)s * nq);
     const int env = B.order ? B.order[k] : k;
@@ -4009,7 +4029,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       const unsigned lcost = tcost * (unsigned)nsub;
       order_key(B, env, skip || !B.order_last ? cost : B.order_last == 1 ? lcost : (cost >> 1) + (lcost >> 1));
     } else {
-      env_store_hand(c, rec, B.hand_stride, time, cost, !B.xcd_local);
+      env_store_hand(c, rec, B.hand_stride, time, cost, !B.xcd_local || s == nsub - 2);
     }
     // publish: the bytes the env's next task must read (the hand-off record) were
     // stored write-through (sc1), so a drained vmcnt suffices and no release fence (a

@@ -16,8 +16,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dexterity_amd import _lib, manipulation  # noqa: E402
 
 
-def main(nenv=4096, steps=60):
-    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=nenv, device=0)
+def main(nenv=4096, steps=60, domain="reorient"):
+    env = manipulation.load(domain, "state_dense", seed=1, num_envs=nenv, device=0)
     env.reset()
     costs = []
     L = _lib.load()
@@ -35,7 +35,7 @@ def main(nenv=4096, steps=60):
     c = np.array(costs)
     os.makedirs("gpurun_out", exist_ok=True)
     np.save("gpurun_out/costs.npy", c.astype(np.float32))
-    slots = 256 * 8
+    slots = 256 * 8  # (the queued reorient batch; a contact-free batch that fits runs one workgroup per env)
     per = c.mean(axis=0)
     print(f"cycles per env-step: mean {c.mean():.3e} p50 {np.median(c):.3e} p90 {np.percentile(c, 90):.3e} "
           f"p99 {np.percentile(c, 99):.3e} max {c.max():.3e}")
@@ -60,4 +60,5 @@ def main(nenv=4096, steps=60):
 
 
 if __name__ == "__main__":
-    main(*[int(a) for a in sys.argv[1:]])
+    # cost_probe.py [nenv] [steps] [domain]
+    main(*[int(a) for a in sys.argv[1:3]], *sys.argv[3:4])
