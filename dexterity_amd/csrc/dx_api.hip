@@ -1027,7 +1027,6 @@ extern "C" dx_batch* dx_batch_create(const dx_model* mc, int32_t nenv, int32_t d
   B.epoch = 0;
   // one queue per XCD (DX_ONE_QUEUE=1: a single queue for the whole chip)
   B.nqueue = getenv("DX_ONE_QUEUE") ? 1 : DX_QUEUES;
-  B.xcd_local = B.nqueue == DX_QUEUES && getenv("DX_XCD_LOCAL") ? atoi(getenv("DX_XCD_LOCAL")) : 0;
   B.np_wide = getenv("DX_NP_WIDE") ? atoi(getenv("DX_NP_WIDE")) : DX_WAVE / 8;
   B.defer_at = getenv("DX_DEFER_AT") ? atoi(getenv("DX_DEFER_AT")) : DX_NCON_MAX;  // (tests / probes)
   B.order_last = getenv("DX_ORDER_LAST") ? atoi(getenv("DX_ORDER_LAST")) : 1;

@@ -162,11 +162,6 @@ struct DevBatch {
   unsigned epoch;
   int nqueue;
   int* qerr;
-  // XCD-local queues (DX_XCD_LOCAL): a workgroup claims only from its own XCD's queue (no
-  // stealing), so every task of an env runs under one L2 and the hand-off record and the
-  // task logic's stores between an env's tasks are plain (L2-resident) instead of
-  // write-through.  Deferrals to the mid tier stay write-through (it may run on any XCD).
-  int xcd_local;
   // the state an env's task hands to its next substep's task: [nenv][hand_stride]
   // floats = qpos | qvel | warm start | time | cost so far | nstep | flags, each record on
   // whole 128-B lines (hand_stride a multiple of 32), so a hand-off writes back and reads

@@ -2556,6 +2556,47 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
 #ifndef DX_PGS_AR
 #define DX_PGS_AR 64  // PGS on AR in registers (one column per lane) up to this many rows
 #endif
+// y = M^-1 J_k' for constraint row k of this lane (k < 0: zero), nv <= 30, from the row's
+// compact form (jac_rows / pgs_jrow) and Minv, the sweep's inverse as a packed lower
+// triangle in LDS: y[d] = sum over the row's nonzeros (e, v) of Minv[d][e] v.
+template <class Ctx>
+__device__ __forceinline__ void pgs_minv_row(const Ctx& c, int k, const float* Minv, float (&y)[30]) {
+  const DevModel& m = c.mdl();
+  const int nv = c.nv;
+#pragma unroll
+  for (int d = 0; d < 30; d++) y[d] = 0.f;
+  const int mt = k >= 0 ? ((const int*)c.f(c.L.efc_meta))[k] : 0;
+  const int type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
+  const bool on = k >= 0;
+  // the row's nonzeros: one dof (friction loss, joint limit), a tendon's dofs, or a
+  // contact row's support dofs
+  const bool con = on && (type == DXR_CON || type == DXR_CONFL);
+  const float* rc = c.f(c.L.con) + DX_CON_STRIDE * (con ? id : 0);
+  uint64_t sup = con ? ((uint64_t)(uint32_t)__float_as_int(rc[18]) | ((uint64_t)(uint32_t)__float_as_int(rc[19]) << 32)) : 0ull;
+  const int kk = 1 + (aux >> 1);
+  const float mu = type == DXR_CON ? rc[15 + kk] * ((aux & 1) ? -1.f : 1.f) : 0.f;
+  const float* cv = c.f(c.L.cj_val) + (con ? id : 0) * 3 * DX_DOFMAX;
+  auto add = [&](int e, float v) {  // y += Minv[:, e] v
+#pragma unroll
+    for (int d = 0; d < 30; d++) {
+      const int dc = min(d, nv - 1);
+      y[d] = fmaf(Minv[ti(max(dc, e)) + min(dc, e)], d < nv ? v : 0.f, y[d]);
+    }
+  };
+  if (on && (type == DXR_FRIC || type == DXR_LIMJ)) add(id, type == DXR_LIMJ && aux ? -1.f : 1.f);
+  if (c.nlimt > 0 && on && type == DXR_LIMT)
+    for (int e = 0; e < nv; e++) {
+      const float tj = m.tendon_J[id * nv + e];
+      add(e, aux ? -tj : tj);
+    }
+#pragma unroll 1
+  for (int q = 0; q < DX_DOFMAX; q++) {  // (not unrolled: y is what stays live)
+    const int e = sup ? (int)__builtin_ctzll(sup) : 0;
+    const float v = sup ? cv[q] + mu * cv[kk * DX_DOFMAX + q] : 0.f;
+    sup &= sup - 1;
+    if (__any(v != 0.f)) add(e, v);
+  }
+}
 // f(std::integral_constant<int, I>) for I in the sequence, unrolled: a register array
 // indexed by I stays in registers
 template <class F, int... I>
@@ -2637,24 +2678,42 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       const bool two = nefc > DX_PGS_AR;
       float a[DX_PGS_AR], b[DX_PGS_AR];
       constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
-      static_for([&](auto K) { a[K.value] = 0.f; b[K.value] = 0.f; }, rows);
+      static_for([&](auto K) { a[K.value] = 0.f; }, rows);
       const int k1 = DX_PGS_AR + LANE;  // this lane's row of the second block
       jac_vec(c, a0, jar);  // J qacc_smooth (jar's warm-start residuals were consumed above)
       const float bk = LANE < nefc ? jar[LANE] - aref[LANE] : 0.f;
       float fk = LANE < nefc ? f[LANE] : 0.f, fk1 = k1 < nefc ? f[k1] : 0.f;
       const float rk = LANE < nefc ? 1.0f / D[LANE] : 0.f, rk1 = k1 < nefc ? 1.0f / D[k1] : 0.f;
       float dg = 1.f, dg1 = 1.f;
-      for (int r = 0; r < nefc; r++) {
-        // column r: J (M^-1 J_r') for every row, + R_r on the diagonal; kept for the rows
-        // of r's block
-        pgs_row(c, r, Jd);
-        minv(Jd, u);
-        jac_vec(c, u, jar);
-        if (r < DX_PGS_AR) {
-          float v = LANE < nefc ? jar[LANE] : 0.f;
+      // AR's first diagonal block: lane k forms y_k = M^-1 J_k' for its row k (from the
+      // row's compact form and the sweep's M^-1 in LDS), then each column r is AR[k][r] =
+      // y_k . J_r (J_r lane-distributed by pgs_jrow, 30 readlanes), + R_r on the diagonal.
+      // The second block (two) goes column by column through LDS (J_r, M^-1 J_r' by the
+      // sweep's inverse, J (M^-1 J_r')): its registers are then the only ones live beside
+      // the first block's.
+      {
+        float y[30];
+        pgs_minv_row(c, LANE < nefc ? LANE : -1, T, y);
+        const int r1 = min(nefc, DX_PGS_AR);
+        for (int r = 0; r < r1; r++) {
+          const float jr = pgs_jrow(c, r);
+          float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+          for (int d = 0; d < 30; d += 2) {
+            v0 = fmaf(y[d], rl(jr, d), v0);
+            v1 = fmaf(y[d + 1], rl(jr, d + 1), v1);
+          }
+          float v = LANE < nefc ? v0 + v1 : 0.f;
           if (LANE == r) { v += rk; dg = v; }
           static_for([&](auto K) { a[K.value] = K.value == r ? v : a[K.value]; }, rows);
-        } else {
+        }
+      }
+      if (two) {
+        static_for([&](auto K) { b[K.value] = 0.f; }, rows);
+        for (int r = DX_PGS_AR; r < nefc; r++) {
+          pgs_row(c, r, Jd);
+          minv(Jd, u);
+          jac_vec(c, u, jar);
           float v = k1 < nefc ? jar[k1] : 0.f;
           if (k1 == r) { v += rk1; dg1 = v; }
           static_for([&](auto K) { b[K.value] = K.value + DX_PGS_AR == r ? v : b[K.value]; }, rows);
@@ -2689,6 +2748,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
         res1 = k1 < nefc ? jar[k1] - aref[k1] + fk1 * rk1 : 0.f;
       };
       if (!two) static_for([&](auto K) { res = K.value < nefc ? fmaf(a[K.value], rl(fk, K.value), res) : res; }, rows);
+      stage_mark(c, ST_NEWTON_HESS);
       // one row update (q static: a register name of a[] / b[])
 // (branch-free: an unchanged force gives dl = 0, and fma(0, x, res) = res, so the
 // residuals, the force and the improvement are those of the branch that skips it)
@@ -2709,17 +2769,25 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       for (; it < c.iterations;) {
         stage_count(c, CNT_NEWTON_IT);
         impr = 0.f;
-        if (two) resid();  // block 0 after the last sweep's block 1
+        // (profiling: the residual passes count as newton_grad, the row updates as
+        // newton_linesearch, the formation above as newton_hessian)
+        if (two) {
+          resid();  // block 0 after the last sweep's block 1
+          stage_mark(c, ST_NEWTON_GRAD);
+        }
         static_for([&](auto G) {
           if (8 * G.value < nefc)
             static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, a, res, fk, dg, idg, lok, hik) }, eight);
         }, groups);
+        stage_mark(c, ST_NEWTON_LS);
         if (two) {
           resid();  // block 1 after this sweep's block 0
+          stage_mark(c, ST_NEWTON_GRAD);
           static_for([&](auto G) {
             if (DX_PGS_AR + 8 * G.value < nefc)
               static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, b, res1, fk1, dg1, idg1, lok1, hik1) }, eight);
           }, groups);
+          stage_mark(c, ST_NEWTON_LS);
         }
 #undef DX_PGS_ROW
         it++;
@@ -3505,8 +3573,7 @@ __device__ __forceinline__ void env_store_state(const Ctx& c, const DevBatch& B,
 // The hand-off record (DevBatch::hand) of a task whose env has substeps left: lane t
 // gathers words 4t .. 4t + 3 from LDS and writes them with one 16-byte sc1 store.
 template <class Ctx>
-__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int stride, float time, unsigned cost,
-                                               bool wt = true) {
+__device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int stride, float time, unsigned cost) {
   const float* qpos = c.f(c.L.qpos);
   const float* qvel = c.f(c.L.qvel);
   const float* ws = c.f(c.L.v5);
@@ -3523,8 +3590,7 @@ __device__ __forceinline__ void env_store_hand(const Ctx& c, float* rec, int str
            : m < c.nq + 2 * c.nv ? ws[m - c.nq - c.nv]
            : k == 0 ? time : k == 1 ? __uint_as_float(cost) : k == 2 ? __int_as_float(nstep) : __int_as_float(flags);
     }
-    if (wt) st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
-    else *(float4*)(rec + 4 * t) = make_float4(w[0], w[1], w[2], w[3]);  // XCD-local queue: L2-resident
+    st_sc1_f4(rec, 4 * stride, 16 * t, make_float4(w[0], w[1], w[2], w[3]));
   }
 }
 
@@ -3903,62 +3969,18 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
   int q = (int)((xcc & 7u) % (unsigned)nqueue);
-  const unsigned me = (xcc & 7u) + 1u;
-  const unsigned all = (1u << nqueue) - 1u;
-  unsigned gone = 0u;  // queues found drained
-  int idle = 0;        // (XCD-local) queues visited in a row without a task to take
-  unsigned naps = 0;   // (XCD-local) full passes without one, bounded like the waits below
+  int empty = 0;  // queues found drained, in the order this workgroup visits them
   for (;;) {
-    if (gone == all) break;
-    if ((gone >> q) & 1u) {
-      q = q + 1 == nqueue ? 0 : q + 1;
-      continue;
-    }
     // queue q: order positions q + nqueue * j, j < nq
     const unsigned nq = B.nenv > q ? (unsigned)(B.nenv - q + nqueue - 1) / (unsigned)nqueue : 0u;
-    if (B.xcd_local) {
-      // XCD-local: a queue has an owner XCD -- the first whose workgroup visits it (its
-      // home XCD, unless that XCD runs no workgroup of this launch) -- whose workgroups
-      // take its tasks, so an env's tasks run under one L2 and its hand-off records stay
-      // plain (L2-resident).  Only the record the last round reads is written through:
-      // once a queue is in its last round (head past (nsub - 1) rounds), workgroups of
-      // other XCDs may take its tasks too, as the tail of a launch needs
-      unsigned own = 0, late = 0;
-      if (LANE == 0) {
-        unsigned* ow = B.qhead + q * DX_QHEAD_STRIDE + 1;
-        own = __hip_atomic_load(ow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (own == 0u) {
-          unsigned z = 0u;
-          own = __hip_atomic_compare_exchange_strong(ow, &z, me, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) ? me : z;
-        }
-        late = __hip_atomic_load(B.qhead + q * DX_QHEAD_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-               nq * (unsigned)(nsub - 1);
-      }
-      if (__builtin_amdgcn_readfirstlane(own) != me && !__builtin_amdgcn_readfirstlane(late)) {
-        // another XCD's queue before its last round: come back later (every queue's owner
-        // is running, so each one reaches its last round and drains)
-        q = q + 1 == nqueue ? 0 : q + 1;
-        if (++idle >= nqueue) {
-          __builtin_amdgcn_s_sleep(8);
-          idle = 0;
-          if (++naps > (1u << 22) || __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-            if (LANE == 0) __hip_atomic_store(B.qerr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            break;
-          }
-        }
-        continue;
-      }
-    }
     unsigned t = 0;
     if (LANE == 0) t = __hip_atomic_fetch_add(B.qhead + q * DX_QHEAD_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     t = __builtin_amdgcn_readfirstlane(t);
     if (t >= nq * (unsigned)nsub) {
-      gone |= 1u << q;
+      if (++empty >= nqueue) break;
       q = q + 1 == nqueue ? 0 : q + 1;
       continue;
     }
-    idle = 0;
     const int s = (int)(t / nq);
     const int k = q + nqueue * (int)(t - (unsigned)s * nq);
     const int env = B.order ? B.order[k] : k;
@@ -4029,7 +4051,7 @@ __device__ __forceinline__ void step_queue(const DevModel& m, const DevBatch& B,
       const unsigned lcost = tcost * (unsigned)nsub;
       order_key(B, env, skip || !B.order_last ? cost : B.order_last == 1 ? lcost : (cost >> 1) + (lcost >> 1));
     } else {
-      env_store_hand(c, rec, B.hand_stride, time, cost, !B.xcd_local || s == nsub - 2);
+      env_store_hand(c, rec, B.hand_stride, time, cost);
     }
     // publish: the bytes the env's next task must read (the hand-off record) were
     // stored write-through (sc1), so a drained vmcnt suffices and no release fence (a
@@ -4222,10 +4244,7 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
     if (B.onext)                                           // this launch's cost histogram
 #pragma unroll
       for (int k = 0; k < 4; k++) B.ohist[256 * B.opar + 4 * LANE + k] = 0u;
-    if (LANE < DX_QUEUES) {  // the queue heads and (XCD-local queues) their owners
-      B.qhead[LANE * DX_QHEAD_STRIDE] = 0u;
-      B.qhead[LANE * DX_QHEAD_STRIDE + 1] = 0u;
-    }
+    if (LANE < DX_QUEUES) B.qhead[LANE * DX_QHEAD_STRIDE] = 0u;  // the queue heads
     if (LANE == 0) B.qerr[1] = 0u;
   }
 }
@@ -4406,10 +4425,7 @@ __global__ void __launch_bounds__(1024) dx_order_kernel(int nenv, const unsigned
   __shared__ int base[256];
   const int t = threadIdx.x;
   if (t < 256) hist[t] = 0;
-  if (qhead && t < DX_QUEUES) {
-    qhead[t * DX_QHEAD_STRIDE] = 0u;
-    qhead[t * DX_QHEAD_STRIDE + 1] = 0u;  // (XCD-local queues: the owner)
-  }
+  if (qhead && t < DX_QUEUES) qhead[t * DX_QHEAD_STRIDE] = 0u;
   __syncthreads();
   for (int e = t; e < nenv; e += 1024) atomicAdd(&hist[255 - (int)min(cost[e] >> 4, 255u)], 1);
   __syncthreads();

@@ -880,31 +880,6 @@ def test_contact_tiers_are_invisible(gpu, monkeypatch):
         assert differ.sum() == 0, np.flatnonzero(differ)
 
 
-def test_xcd_local_queue_is_invisible(gpu, monkeypatch):
-    """The XCD-local substep queue (DX_XCD_LOCAL=1: each queue taken by its owner XCD,
-    plain hand-off records except the last round's, tail stealing in the last round)
-    gives the default queue's results bit for bit: 4096 reorient envs x 12 control
-    steps, outputs and task logic included."""
-    from dexterity_amd import manipulation
-
-    outs = []
-    for env_vars in ({}, {"DX_XCD_LOCAL": "1"}):
-        monkeypatch.delenv("DX_XCD_LOCAL", raising=False)
-        for k, v in env_vars.items():
-            monkeypatch.setenv(k, v)
-        env = manipulation.load("reorient", "state_dense", seed=6, num_envs=4096)
-        env.reset()
-        for step in range(12):
-            env.step_random(step)
-        ts = env.timestep()
-        assert env.physics.debug_get("queue_timeouts")[0] == 0
-        outs.append((env.physics.qpos, env.physics.qvel, env.physics.get(_lib.QACC_WARMSTART), ts.reward,
-                     ts.step_type, env.goals()))
-        env.close()
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
-
-
 def test_mixed_launches_with_deferrals(gpu, monkeypatch):
     """Deferral entries belong to their launch (list[1] = the launch's epoch; the mid tier
     claims only its own launch's entries, with its own nsub and task-logic mode): fused
