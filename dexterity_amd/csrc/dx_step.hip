@@ -2030,21 +2030,25 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
         break;  // contact rows are last
       }
     }
-    // Branch-free over the contacts (a skipped contact's loads are made and discarded),
-    // so the unrolled iterations' LDS reads overlap instead of waiting one by one; the
-    // sum keeps the contact order.
-    const uint64_t bit = 1ull << d;
-#pragma unroll 4
-    for (int ci = 0; ci < ncon; ci++) {
-      const float* r = con + DX_CON_STRIDE * ci;
-      const uint64_t sup = (uint64_t)(uint32_t)__float_as_int(r[18]) | ((uint64_t)(uint32_t)__float_as_int(r[19]) << 32);
-      const int q = __popcll(sup & (bit - 1));
-      const bool on = (sup & bit) && q < DX_DOFMAX;
-      const float* cv = cj_val + ci * 3 * DX_DOFMAX + min(q, DX_DOFMAX - 1);
-      const float t = cv[0] * cw[3 * ci] + cv[DX_DOFMAX] * cw[3 * ci + 1] + cv[2 * DX_DOFMAX] * cw[3 * ci + 2];
-      s = on ? s + t : s;
-    }
     out[d] = s;
+  }
+  SYNC();
+  // the contacts, over (contact, support slot) items (16 slots a contact): lane (ci, q)
+  // adds its slot's J^T f term to its dof with an LDS float atomic.  Within one atomic
+  // the lanes of a dof are applied in lane order, i.e. contact order, as the serial sum
+  // of each dof's contacts did (one lane per dof, a loop over the contacts: ncon
+  // dependent rounds of LDS reads, the bulk of the solvers' gradient stage).
+  const int nitem = 16 * ncon;
+  for (int base = 0; base < nitem; base += DX_WAVE) {
+    const int t = base + LANE;
+    const int ci = min(t >> 4, max(ncon - 1, 0)), q = t & 15;
+    const int nnz = __float_as_int(con[DX_CON_STRIDE * ci + 14]) & 255;
+    if (t < nitem && q < nnz) {
+      const int d = cj_idx[ci * DX_DOFMAX + q];
+      const float* cv = cj_val + ci * 3 * DX_DOFMAX + q;
+      const float tv = cv[0] * cw[3 * ci] + cv[DX_DOFMAX] * cw[3 * ci + 1] + cv[2 * DX_DOFMAX] * cw[3 * ci + 2];
+      atomicAdd(out + d, tv);
+    }
   }
   SYNC();
 }
