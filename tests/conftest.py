@@ -82,3 +82,66 @@ def inclined_box_scene(tilt_deg: float, mu: float = 0.4, dt: float = 0.002):
 
 # tilts used with it (mu = 0.4, tan^-1 0.4 = 21.8 deg): 5-15 deg stick, 25 and 30 deg
 # slide (steeper, the sliding cube starts to tip over its leading edge)
+
+
+def resting_box_scene(condim: int, mu: float = 1.0, solref=(0.02, 1.0), dt: float = 0.002):
+    """A free cube (half-size 2 cm, 0.064 kg) on a level plane, both geoms with the given
+    condim / friction / solref: the resting-contact known answer (resting_depth)."""
+    from dexterity_amd.mjcf.compiler import Scene
+
+    s = Scene(timestep=dt, gravity=(0.0, 0.0, -9.81))
+    kw = dict(condim=condim, friction=f"{mu} 0.005 0.0001", solref=f"{solref[0]} {solref[1]}")
+    s.add_world_geom("ground", "plane", (1, 1, 0.1), **kw)
+    s.add_free_box("box", 0.02, [0.0, 0.0, 0.0199], **kw)
+    return s.compile()
+
+
+def soft_impedance(r: float, solimp=(0.9, 0.95, 0.001, 0.5, 2.0)) -> float:
+    """MuJoCo's constraint impedance d(r) (documentation, Computation > Soft constraints:
+    the solimp sigmoid -- power `p` from dmin at 0 to dmax at `width`, joined at `mid`)."""
+    dmin, dmax, width, mid, p = solimp
+    x = min(r / width, 1.0)
+    if x >= 1.0:
+        y = 1.0
+    elif x <= mid:
+        y = x**p / mid ** (p - 1)
+    else:
+        y = 1.0 - (1.0 - x) ** p / (1.0 - mid) ** (p - 1)
+    return dmin + y * (dmax - dmin)
+
+
+def resting_depth(condim: int, mu: float = 1.0, solref=(0.02, 1.0), g: float = 9.81,
+                  solimp=(0.9, 0.95, 0.001, 0.5, 2.0), impratio: float = 1.0) -> float:
+    """Equilibrium penetration of resting_box_scene, from MuJoCo's published soft-contact
+    model alone (not the oracle): at rest qacc = 0 and v = 0, so each active row carries
+    f = aref / R with aref = K d(r) r, K = 1 / (dmax^2 timeconst^2 dampratio^2) and
+    R = (1 - d) / d * A, A = the box's translational inverse weight 1 / m (the world's is 0).
+    Frictionless (condim 1): one row per corner.  Pyramidal (condim 3): four edge rows
+    n +- mu t per corner, R_edge = 2 mu^2 R / impratio, whose tangential parts cancel, so a
+    corner's normal force is 2 impratio / mu^2 times the frictionless one.  The four
+    corners share m g; m cancels (A = 1 / m).  Solved for r by bisection."""
+    tc, dr = solref
+    K = 1.0 / (solimp[1] ** 2 * tc**2 * dr**2)
+    c = 1.0 if condim == 1 else 2.0 * impratio / mu**2
+    lo, hi = 0.0, 0.05
+    for _ in range(200):
+        r = 0.5 * (lo + hi)
+        d = soft_impedance(r, solimp)
+        if 4.0 * c * K * d * d * r / (1.0 - d) > g:
+            hi = r
+        else:
+            lo = r
+    return 0.5 * (lo + hi)
+
+
+# resting_box_scene cases: the impedance's power segment (r < mid * width), its upper
+# segment (mid * width < r < width) and its plateau (r > width); frictionless and
+# pyramidal rows, two friction coefficients, an underdamped solref
+RESTING_CASES = [
+    (1, 1.0, (0.02, 1.0)),
+    (1, 1.0, (0.07, 1.0)),
+    (1, 1.0, (0.1, 1.0)),
+    (3, 1.0, (0.02, 1.0)),
+    (3, 0.5, (0.02, 1.0)),
+    (3, 1.0, (0.05, 0.7)),
+]

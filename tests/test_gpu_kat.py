@@ -7,7 +7,10 @@
     (|qvel| <= 1e-2); the joint torque observable must read -tau within 1e-2;
   * hands_test.py:195-228  five golden Adroit fingertip positions reached by the IK
     solver (linear_tol 1e-3, early stop, first successful attempt) and confirmed by
-    forward kinematics within atol 1e-3.
+    forward kinematics within atol 1e-3;
+and two contact known answers from physics rather than the restatement: the inclined
+plane (Coulomb stick / slide) and the resting cube's equilibrium penetration (MuJoCo's
+published soft-contact model).
 """
 
 import os
@@ -17,7 +20,7 @@ import pytest
 
 from dexterity_amd import _lib, blob
 from dexterity_amd.mjcf.compiler import CompiledModel
-from tests.conftest import ROOT
+from tests.conftest import RESTING_CASES, ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -132,6 +135,26 @@ def test_adroit_fingertip_golden_ik(gpu, oracle_mod, adroit_hand):
     tips = d.site_xpos.reshape(-1, 3)[solver.sites]
     np.testing.assert_allclose(tips, FINGERTIP_GOLDEN, atol=1e-3)
     solver.close()
+
+
+@pytest.mark.parametrize("condim,mu,solref", RESTING_CASES)
+def test_resting_contact_depth_kat(gpu, condim, mu, solref):
+    """The resting-contact known answer on the fp32 kernel (tests/test_oracle.py has it
+    on the oracle): a cube left on a level plane settles at the penetration MuJoCo's
+    published soft-contact model gives (tests/conftest.py resting_depth: K, d(r), R with
+    frictionless or pyramidal rows), within 1e-3 of it (fp32 position near 0.02 m:
+    ulp 1.9e-9 against depths of 1.4e-5 .. 1.2e-3 m), at rest (|qvel| < 1e-5) after 2 s."""
+    from tests.conftest import resting_box_scene, resting_depth
+
+    cm = resting_box_scene(condim, mu, solref)
+    ph = gpu.BatchedPhysics(gpu.Model(cm), 4)
+    ph.step(1000)
+    q = ph.qpos.astype(np.float64)
+    v = ph.qvel.astype(np.float64)
+    ph.close()
+    r = resting_depth(condim, mu, solref)
+    assert np.abs(v).max() < 1e-5, np.abs(v).max()
+    assert np.all(np.abs((0.02 - q[:, 2]) - r) <= 1e-3 * r), (0.02 - q[:, 2], r)
 
 
 @pytest.mark.parametrize("tilt", [5.0, 10.0, 15.0, 25.0, 30.0])

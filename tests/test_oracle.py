@@ -7,7 +7,8 @@ The oracle's dynamics cannot be compared with real MuJoCo here (absent, SURVEY.m
   * gravity torques against J^T(m g) built from numpy jacobians;
   * Coriolis power identity v.C(q,v)v = 1/2 v.dM/dt v;
   * gravity compensation (utils/mujoco_utils.py:91-99) cancels gravity exactly;
-  * free fall, contact resting equilibrium (sum of normal forces = m g), energy
+  * free fall, contact resting equilibrium (sum of normal forces = m g; a cube's
+    penetration = the one MuJoCo's published soft-contact model gives), energy
     conservation of a frictionless undamped system, 100 steps without divergence
     (hands_test.py:52-57).
 """
@@ -20,7 +21,7 @@ import pytest
 from dexterity_amd import blob
 from dexterity_amd.mjcf import setconst
 from dexterity_amd.physics import gravity_compensation
-from tests.conftest import ROOT, random_hand_state
+from tests.conftest import RESTING_CASES, ROOT, random_hand_state
 
 
 def _data(oracle_mod, compiled):
@@ -358,6 +359,27 @@ def test_oracle_inclined_plane_friction_kat(oracle_mod, tilt):
         expect = g * (np.sin(th) - mu * np.cos(th))
         assert abs(a - expect) <= 0.05 * expect, (tilt, a, expect)
     assert abs(d.qpos[2] - 0.02) < 1e-3  # still resting on a face
+
+
+@pytest.mark.parametrize("condim,mu,solref", RESTING_CASES)
+def test_oracle_resting_contact_depth_kat(oracle_mod, condim, mu, solref):
+    """Contact dynamics against MuJoCo's published soft-contact model rather than the
+    restatement: a cube left on a level plane settles (|qvel| < 1e-9 after 2 s) at the
+    penetration tests/conftest.py resting_depth derives from K, d(r) and R alone, within
+    1e-6 of it; four contacts (one per bottom corner).  tests/test_gpu_kat.py runs the
+    same cases on the GPU kernel."""
+    from tests.conftest import resting_box_scene, resting_depth
+
+    cm = resting_box_scene(condim, mu, solref)
+    assert abs(cm.body_invweight0[1][0] - 1.0 / 0.064) < 1e-9  # A = 1 / m
+    d = oracle_mod.OracleData(oracle_mod.OracleModel(blob.pack(cm.arrays)))
+    d.qpos[:] = cm.qpos0
+    for _ in range(1000):
+        d.step()
+    r = resting_depth(condim, mu, solref)
+    assert d.ncon == 4
+    assert np.abs(d.qvel).max() < 1e-9
+    assert abs((0.02 - d.qpos[2]) - r) <= 1e-6 * r, (0.02 - d.qpos[2], r)
 
 
 def test_batch_step_watch_is_the_fall_test(oracle_mod, reorient_compiled):
