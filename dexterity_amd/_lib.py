@@ -20,7 +20,7 @@ SENSOR_TORQUE, DIVERGED = 15, 16
 INT_FIELDS = (NCON, GROUND_CONTACT, NITER, NCAND, STEP_COST, DIVERGED)
 HEALTH_WORDS, NCON_HIST = 16, 65
 HEALTH = ("contact_overflow", "candidate_overflow", "jacobian_dof_overflow", "row_overflow", "diverged",
-          "ncon_max", "contact_deferred")
+          "ncon_max", "contact_deferred", "mid_tier_gave_up", "deferred_behind_launch")
 
 EXPORTS = (
     "dx_model_load", "dx_model_free", "dx_model_sizes", "dx_model_lds_bytes", "dx_field_width",

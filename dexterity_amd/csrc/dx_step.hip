@@ -4181,7 +4181,10 @@ dx_step_hi_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub) 
   for (unsigned i = blockIdx.x; i < n1; i += gridDim.x) {
     unsigned e = 0;
     int got = 0;
-    if (LANE == 0) got = defer_claim(B.defer, i, &e);
+    if (LANE == 0) {
+      got = defer_claim(B.defer, i, &e);
+      if (got == 1) atomicAdd(B.health + 8, 1u);  // a step-kernel deferral the mid tier did not take
+    }
     if (__shfl(got, 0, 64) != 1) continue;
     e = __shfl(e, 0, 64);
     const int env = defer_env(e), s0 = defer_step(e);
@@ -4290,8 +4293,10 @@ dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub,
     unsigned e = 0;
     int got = 0;
     if (LANE == 0) {
+      unsigned last = ~0u;
       for (unsigned n = 0;; n++) {
-        const bool done = (int)(__hip_atomic_load(B.qdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0;
+        const unsigned qd = __hip_atomic_load(B.qdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool done = (int)(qd - target) >= 0;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned cnt = __hip_atomic_load(B.defer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (i < cnt) {
@@ -4303,11 +4308,16 @@ dx_step_mid_kernel(const DevModel* __restrict__ mp, DevBatch B, Lds L, int nsub,
         }
         __builtin_amdgcn_s_sleep(4);
         // Giving up is always safe -- the overflow tier takes every entry left -- so the
-        // wait is short and sets no error: it ends a mid tier that runs before its
-        // launch's step kernel (a profiler serialising the dispatches) or one whose
-        // launch aborted
-        if (++n > (1u << 17) || ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+        // wait sets no error: it ends a mid tier that runs before its launch's step kernel
+        // (a profiler serialising the dispatches) or one whose launch aborted.  The clock
+        // restarts whenever the launch finishes a task, so a long launch (CG, PGS: 5-18 ms)
+        // keeps its mid tier; ~14 ms without one finished task ends the wait.  Counted in
+        // health word 7 (speed only: the entries then run behind the launch).
+        if (qd != last) { last = qd; n = 0; }
+        if (++n > (1u << 17) || ((n & 1023u) == 0 && __hip_atomic_load(B.qerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+          atomicAdd(B.health + 7, 1u);
           break;
+        }
       }
     }
     i = __shfl(i, 0, 64);

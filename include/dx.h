@@ -162,6 +162,10 @@ int dx_sensor_enable(dx_batch* b, int enable);
  *     were therefore run by a larger pool -- the mid tier (64 contacts, beside a queued
  *     step launch on a side stream) or the overflow tier (256, behind the launch), the
  *     same physics: not a truncation
+ *   7 mid-tier launches that stopped waiting for deferrals before their step launch ended
+ *     (~14 ms without a finished task: a serialised dispatch order or an aborted launch)
+ *   8 step-kernel deferrals run by the overflow tier behind the launch instead of by the
+ *     mid tier beside it (words 7 and 8: speed only, the same physics)
  * then, when the histogram is on (dx_ncon_histogram), out[16 .. 16 + 65): env-substeps
  * by contacts found (bins 0..63, then >= 64).  Synchronises the batch's stream. */
 #define DX_HEALTH_WORDS 16

@@ -43,16 +43,19 @@ def env_config(name, domain, task, nenv, steps=50, warmup=10, solver=None):
     env.physics.sync()
     L.dx_timing_enable(env.physics.ptr, 1)
     _kernel_ms(L, env.physics.ptr)
+    env.physics.health_clear()
     t = time.perf_counter()
     for i in range(steps):
         env.step_random(warmup + i)
     env.physics.sync()
     dt = time.perf_counter() - t
     kms, kn = _kernel_ms(L, env.physics.ptr)
+    h = env.physics.health()  # the deferral tiers over the timed region (include/dx.h dx_health)
     env.close()
     return {"config": name, "envs": nenv, "solver": solver or "Newton", "env_steps_per_s": round(nenv * steps / dt, 1),
             "ms_per_step": round(dt / steps * 1e3, 4), "step_kernel_ms_avg": round(kms, 4),
-            "step_kernel_launches_per_step": kn / steps}
+            "step_kernel_launches_per_step": kn / steps,
+            "deferred": {k: h[k] for k in ("contact_deferred", "mid_tier_gave_up", "deferred_behind_launch")}}
 
 
 def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
