@@ -2667,7 +2667,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
     for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
   SYNC();
   if (inv) {
-    if (nefc <= 2 * DX_PGS_AR) {
+    if (nefc <= 2 * DX_PGS_AR + DX_WAVE) {
       // MuJoCo's own form (mj_solPGS on efc_AR): AR = J M^-1 J' + R, lane k holding
       // column k (a[r] = AR[r][k] = AR[k][r]) and the residual res_k = (AR f)_k + b_k
       // (b = J qacc_smooth - aref).  A row update is then a readlane of res_r, a few
@@ -2678,8 +2678,13 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       // blocks (lane k: rows k and 64 + k), each holding its own diagonal block of AR
       // (a[], b[]); the coupling between the blocks enters when a block's sweep starts,
       // through its residuals recomputed from the current forces matrix-free (J (qacc_smooth
-      // + M^-1 J'f) - aref + R f) -- exactly the Gauss-Seidel sweep in row order.
+      // + M^-1 J'f) - aref + R f) -- exactly the Gauss-Seidel sweep in row order.  Rows
+      // past 128 (the tail, at most 64: contact rows of the envs with 26 or more contacts,
+      // which set the launch) go one at a time after block 1, matrix-free on qacc (lane =
+      // dof) as the path below, with their AR diagonal formed once per solve (lane t: tail
+      // row t).
       const bool two = nefc > DX_PGS_AR;
+      const int ntail = max(0, nefc - 2 * DX_PGS_AR);
       float a[DX_PGS_AR], b[DX_PGS_AR];
       constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
       static_for([&](auto K) { a[K.value] = 0.f; }, rows);
@@ -2714,7 +2719,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       }
       if (two) {
         static_for([&](auto K) { b[K.value] = 0.f; }, rows);
-        for (int r = DX_PGS_AR; r < nefc; r++) {
+        for (int r = DX_PGS_AR; r < min(nefc, 2 * DX_PGS_AR); r++) {
           pgs_row(c, r, Jd);
           minv(Jd, u);
           jac_vec(c, u, jar);
@@ -2722,6 +2727,14 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
           if (k1 == r) { v += rk1; dg1 = v; }
           static_for([&](auto K) { b[K.value] = K.value + DX_PGS_AR == r ? v : b[K.value]; }, rows);
         }
+      }
+      float ardt = 1.f;  // lane t: AR[128 + t][128 + t]
+      for (int t = 0; t < ntail; t++) {
+        const int r = 2 * DX_PGS_AR + t;
+        pgs_row(c, r, Jd);
+        minv(Jd, u);
+        const float sr = wave_sum(LANE < nv ? Jd[LANE] * u[LANE] : 0.f) + 1.0f / D[r];
+        ardt = LANE == t ? sr : ardt;
       }
       const float idg = 1.0f / dg, idg1 = 1.0f / dg1;
       // each row's projection as a box [lo, hi]: friction loss [-floss, floss], limits and
@@ -2739,10 +2752,16 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       box(k1, lok1, hik1);
       float res = bk, res1 = 0.f;
       // both blocks' residuals from the current forces, matrix-free
-      auto resid = [&]() {
+      // (jar = -f / R is each row's force as a residual, what jac_t_force reads; the tail
+      // rows' forces live in f[] and their jar is restored here after each jac_vec)
+      auto forces_out = [&]() {
         if (LANE < nefc) { f[LANE] = fk; jar[LANE] = -fk / D[LANE]; }
         if (k1 < nefc) { f[k1] = fk1; jar[k1] = -fk1 / D[k1]; }
+        if (LANE < ntail) { const int r = 2 * DX_PGS_AR + LANE; jar[r] = -f[r] / D[r]; }
         SYNC();
+      };
+      auto resid = [&]() {
+        forces_out();
         jac_t_force(c, g);
         minv(g, u);
         for (int i = LANE; i < nv; i += DX_WAVE) u[i] += a0[i];
@@ -2794,19 +2813,42 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
           stage_mark(c, ST_NEWTON_LS);
         }
 #undef DX_PGS_ROW
+        if (ntail) {
+          // the tail after block 1: qacc = qacc_smooth + M^-1 J'f from the current forces,
+          // then row by row res_r = J_r qacc - aref_r + R_r f_r, qacc += dl M^-1 J_r'
+          forces_out();
+          jac_t_force(c, g);
+          minv(g, u);
+          float qa = LANE < nv ? u[LANE] + a0[LANE] : 0.f;
+          SYNC();
+          stage_mark(c, ST_NEWTON_GRAD);
+          for (int t = 0; t < ntail; t++) {
+            const int r = 2 * DX_PGS_AR + t;
+            const float jr = pgs_jrow(c, r);
+            if (LANE < nv) Jd[LANE] = jr;
+            const float fo = f[r], rr = wave_sum(jr * qa) - aref[r] + fo / D[r];
+            const float ar = rl(ardt, t);
+            float lo, hi;
+            box(r, lo, hi);
+            const float fn = __builtin_amdgcn_fmed3f(fo - rr / ar, lo, hi);
+            const float dl = fn - fo;
+            if (dl != 0.f) {
+              SYNC();
+              mat_vec(T, Jd, u, nv);
+              SYNC();
+              if (LANE < nv) qa = fmaf(dl, u[LANE], qa);
+              if (LANE == 0) f[r] = fn;
+              impr -= 0.5f * ar * dl * dl + dl * rr;
+            }
+            SYNC();
+          }
+          stage_mark(c, ST_NEWTON_LS);
+        }
         it++;
         if (scale * impr < tol) break;
       }
       // the forces, as residuals whose primal force is f_r; qacc = qacc_smooth + M^-1 J'f
-      if (LANE < nefc) {
-        f[LANE] = fk;
-        jar[LANE] = -fk / D[LANE];
-      }
-      if (k1 < nefc) {
-        f[k1] = fk1;
-        jar[k1] = -fk1 / D[k1];
-      }
-      SYNC();
+      forces_out();
       jac_t_force(c, g);
       minv(g, u);
       for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i] + u[i];

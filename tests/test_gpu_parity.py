@@ -1331,6 +1331,73 @@ def test_pgs_solver_parity(gpu, oracle_mod, reorient_setup):
         phys.close()
 
 
+def test_pgs_tail_rows_parity(gpu, oracle_mod):
+    """PGS past 128 constraint rows: the AR path's tail rows (dx_step.hip solve_pgs, rows
+    128+ one at a time on qacc after the two register blocks).  The reorient envs of the
+    bench's state mix with 27 or more contacts (24 friction-loss rows + 4 pyramid edges per
+    contact: more than 128 rows, the envs that set the PGS launch) take one forward pass
+    with <option solver="PGS">: run to convergence, kernel vs the oracle's PGS
+    within PGS_CONV_MAX (test_pgs_solver_parity); at MuJoCo's defaults (100 sweeps, not
+    converged on these states), kernel vs oracle within PGS_TAIL_MAX.  Both on the GPU's
+    own contact list (dxo_set_contacts)."""
+    from dexterity_amd import manipulation
+
+    n = 4096
+    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=n)
+    env.reset()
+    states = []
+    for step in range(80):
+        env.step_random(step)
+        ph = env.physics
+        sel = np.nonzero(ph.get(_lib.NCON)[:, 0] >= 27)[0][:3]
+        if len(sel):
+            q, v, w, u = ph.qpos, ph.qvel, ph.get(_lib.QACC_WARMSTART), ph.get(_lib.CTRL)
+            states += [tuple(np.asarray(x[e], dtype=np.float64) for x in (q, v, w, u)) for e in sel]
+        if len(states) >= 6:
+            break
+    xfrc = env.task.gravity_compensation
+    cm = env.task.compiled
+    env.close()
+    om = oracle_mod.OracleModel(blob.pack(cm.arrays))
+    nefc = [_oracle_forward(oracle_mod, om, cm, xfrc, st).nefc for st in states]
+    print("tail states: nefc", nefc)
+    assert sum(k > 128 for k in nefc) >= 2, nefc
+    # on the GPU's own contact list (dxo_set_contacts): the deep contacts of these grasps
+    # move under fp32 MPR (the full-batch test's "geometry" states); the solver is the test
+    def run(model_cm):
+        phys = _load_states(gpu, gpu.Model(model_cm), xfrc, states)
+        phys.debug(True)
+        phys.forward()
+        phys.sync()
+        con, qacc = phys.debug_get("contact"), phys.qacc
+        phys.close()
+        return con, qacc
+
+    def err(om_x, con, qacc, e, st):
+        gc = con[e, : (con[e, :, 15] != 0).sum()]
+        d = _oracle_forward(oracle_mod, om, cm, xfrc, st)
+        scale = max(1.0, np.abs(d.qacc_smooth).max())
+        return np.abs(qacc[e] - _qacc_on_gpu_contacts(oracle_mod, om_x, xfrc, st, gc)).max() / scale
+
+    pg = cm.with_solver("PGS", iterations=3000, tolerance=1e-13)
+    om_pg = oracle_mod.OracleModel(blob.pack(pg.arrays))
+    con, qacc = run(pg)
+    e_pg = np.array([err(om_pg, con, qacc, e, st) for e, st in enumerate(states)])
+    e_nt = np.array([err(om, con, qacc, e, st) for e, st in enumerate(states)])
+    print(f"PGS tail, converged: |qacc| err / scale vs oracle PGS {np.round(e_pg, 7).tolist()}, "
+          f"vs Newton {np.round(e_nt, 7).tolist()}")
+    pgd = cm.with_solver("PGS")
+    om_d = oracle_mod.OracleModel(blob.pack(pgd.arrays))
+    con, qacc = run(pgd)
+    ea = np.array([err(om_d, con, qacc, e, st) for e, st in enumerate(states)])
+    print(f"PGS tail, defaults: |qacc| err / scale {np.round(ea, 7).tolist()}")
+    ok = np.array([k > 128 for k in nefc])
+    # (3000 sweeps do not reach the Newton optimum on every one of these states -- the
+    # oracle's own PGS stays as far from it -- so Newton is reported, not asserted)
+    assert e_pg[ok].max() <= PGS_CONV_MAX
+    assert ea[ok].max() <= PGS_TAIL_MAX
+
+
 # PGS bounds.  Measured (r4) over the 12 states: converged (3000 sweeps, 1e-13) qacc
 # within 2.9e-4 x scale of both the oracle's PGS and the Newton optimum (fp32's floor
 # here, CG's bound); defaults, one forward: median 4.4e-5, max 1.9e-4; 1 / 3 substeps:
@@ -1338,6 +1405,9 @@ def test_pgs_solver_parity(gpu, oracle_mod, reorient_setup):
 PGS_CONV_MAX = 5e-4
 PGS_QACC_MED, PGS_QACC_MAX = 2e-4, 1e-3
 PGS_QPOS_MAX, PGS_QVEL_MAX = 1e-6, 1e-5
+# tail states (r5, 7 states, nefc 128-144, on the GPU's contacts): converged max 2.4e-5,
+# defaults max 2.9e-5 of the scale
+PGS_TAIL_MAX = 1e-4
 
 
 # CG at MuJoCo's defaults stops after 100 iterations or at 1e-8 on a linearly converging

@@ -16,10 +16,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dexterity_amd import _lib, manipulation  # noqa: E402
 
 
-def main(nenv=4096, steps=60, domain="reorient"):
-    env = manipulation.load(domain, "state_dense", seed=1, num_envs=nenv, device=0)
+def main(nenv=4096, steps=60, domain="reorient", solver=None):
+    if solver is None:
+        env = manipulation.load(domain, "state_dense", seed=1, num_envs=nenv, device=0)
+    else:  # <option solver=...> at MuJoCo's defaults (tools/bench_configs.py configs 3' / 3'')
+        t = manipulation.SUITE[(domain, "state_dense")]()
+        t.compiled = t.compiled.with_solver(solver)
+        env = manipulation.GoalEnvironment(t, num_envs=nenv, seed=1)
     env.reset()
     costs = []
+    ncons = []
     L = _lib.load()
     kms = []
     for i in range(steps):
@@ -29,6 +35,7 @@ def main(nenv=4096, steps=60, domain="reorient"):
         env.step_random(i)
         if i >= 10:
             costs.append(env.physics.get(_lib.STEP_COST).ravel().astype(np.float64) * 1024)
+            ncons.append(env.physics.get(_lib.NCON).ravel().astype(np.int64))
             kt, kn = ctypes.c_double(), ctypes.c_int32()
             _lib.check(L.dx_timing_read(env.physics.ptr, ctypes.byref(kt), ctypes.byref(kn)))
             kms.append(kt.value / max(kn.value, 1))
@@ -54,11 +61,16 @@ def main(nenv=4096, steps=60, domain="reorient"):
         ranks.extend(prev_rank[np.argsort(-c[t])[:20]].tolist())
     print("previous-step rank of each step's 20 heaviest envs: median", np.median(ranks),
           "p90", np.percentile(ranks, 90))
+    nc = np.array(ncons)
+    top = np.argsort(-c.ravel())[:12]
+    print("heaviest env-steps (Mcycles, contacts at the step's end):",
+          [(round(c.ravel()[k] / 1e6, 2), int(nc.ravel()[k])) for k in top])
+    print(f"per-step max / kernel cycles {np.mean(c.max(axis=1)) / (km * 1e-3 * clk):.3f}")
     hist, edges = np.histogram(c.ravel() / 1e6, bins=20)
     print("hist (Mcycles):", list(zip(np.round(edges[:-1], 2).tolist(), hist.tolist())))
     env.close()
 
 
 if __name__ == "__main__":
-    # cost_probe.py [nenv] [steps] [domain]
-    main(*[int(a) for a in sys.argv[1:3]], *sys.argv[3:4])
+    # cost_probe.py [nenv] [steps] [domain] [solver]
+    main(*[int(a) for a in sys.argv[1:3]], *sys.argv[3:5])
