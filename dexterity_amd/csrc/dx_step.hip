@@ -2788,6 +2788,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
       constexpr auto groups = std::make_integer_sequence<int, DX_PGS_AR / 8>{};
       constexpr auto eight = std::make_integer_sequence<int, 8>{};
       float impr = 0.f;
+      float qa = 0.f;  // qacc (lane = dof) after the tail rows
       int it = 0;
       for (; it < c.iterations;) {
         stage_count(c, CNT_NEWTON_IT);
@@ -2795,7 +2796,16 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
         // (profiling: the residual passes count as newton_grad, the row updates as
         // newton_linesearch, the formation above as newton_hessian)
         if (two) {
-          resid();  // block 0 after the last sweep's block 1
+          if (it > 0 && ntail) {
+            // block 0 after the last sweep's tail: qa, carried through the tail rows, is
+            // already qacc_smooth + M^-1 J'f of the current forces
+            if (LANE < nv) u[LANE] = qa;
+            SYNC();
+            jac_vec(c, u, jar);
+            res = LANE < nefc ? jar[LANE] - aref[LANE] + fk * rk : 0.f;
+          } else {
+            resid();  // block 0 after the last sweep's block 1
+          }
           stage_mark(c, ST_NEWTON_GRAD);
         }
         static_for([&](auto G) {
@@ -2819,7 +2829,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
           forces_out();
           jac_t_force(c, g);
           minv(g, u);
-          float qa = LANE < nv ? u[LANE] + a0[LANE] : 0.f;
+          qa = LANE < nv ? u[LANE] + a0[LANE] : 0.f;
           SYNC();
           stage_mark(c, ST_NEWTON_GRAD);
           for (int t = 0; t < ntail; t++) {

@@ -13,7 +13,13 @@ from dexterity_amd import _lib, manipulation  # noqa: E402
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
 domain = sys.argv[3] if len(sys.argv) > 3 else "reorient"  # e.g. reach_shadow (BASELINE config 2)
-env = manipulation.load(domain, "state_dense", seed=3, num_envs=B)
+solver = sys.argv[4] if len(sys.argv) > 4 else None  # CG / PGS: <option solver=...> at MuJoCo's defaults
+if solver is None:
+    env = manipulation.load(domain, "state_dense", seed=3, num_envs=B)
+else:
+    task = manipulation.SUITE[(domain, "state_dense")]()
+    task.compiled = task.compiled.with_solver(solver)
+    env = manipulation.GoalEnvironment(task, num_envs=B, seed=3)
 L = _lib.load()
 env.reset()
 for i in range(10):
