@@ -2305,15 +2305,18 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // new point is returned in *cost_new: the rows' costs plus the Gauss term, continued along
 // the line as gauss + alpha qb + alpha^2 qa / 2 (M qacc_smooth = qfrc_smooth), so the
 // solver needs no separate cost pass.
-template <bool NEWTON = false, class Ctx>
+// HAVE_MDIR: the caller already holds M dir in v4 (CG's recurrence), no product here.
+template <bool NEWTON = false, bool HAVE_MDIR = false, class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed,
                                              float* slope0 = nullptr, const float* grad = nullptr,
                                              float gauss = 0.f, float* cost_new = nullptr, float* gauss_new = nullptr) {
   const DevModel& m = c.mdl();
   int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
-  mat_vec(c.f(c.L.M), dir, Mdir, nv);
-  stage_mark(c, ST_MATVEC);
+  if (!HAVE_MDIR) {
+    mat_vec(c.f(c.L.M), dir, Mdir, nv);
+    stage_mark(c, ST_MATVEC);
+  }
   float* jv = c.f(c.L.efc_jv);
   jac_vec(c, dir, jv);  // includes SYNC
   stage_mark(c, ST_JACVEC);
@@ -2458,14 +2461,18 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
     gmg += grad[i] * Mg[i];
   }
   float gmg_old = wave_sum(gmg);
+  // M dir by recurrence instead of a product per iteration: dir = -M^-1 grad + beta dir_old
+  // gives M dir = -grad + beta M dir_old (-grad on a restart)
+  float* Mdir = c.f(c.L.v4);
+  for (int i = LANE; i < nv; i += DX_WAVE) Mdir[i] = -grad[i];
+  SYNC();
   for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
     int changed = 0;
     float g0 = 0.f;
-    const float alpha = line_search(c, qacc, Ma, dir, &changed, &g0);
+    const float alpha = line_search<false, true>(c, qacc, Ma, dir, &changed, &g0);
     stage_mark(c, ST_NEWTON_LS);
     if (alpha == 0.f) break;
-    const float* Mdir = c.f(c.L.v4);
     const float* jvd = c.f(c.L.efc_jv);
     for (int i = LANE; i < nv; i += DX_WAVE) {
       qacc[i] += alpha * dir[i];
@@ -2508,8 +2515,11 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
       dir[i] = di;
     }
     // not a descent direction (fp32 line searches are exact to 1e-6): restart along -Mgrad
-    if (!(wave_sum(slope) < 0.f))
-      for (int i = LANE; i < nv; i += DX_WAVE) dir[i] = -Mg[i];
+    const bool restart = !(wave_sum(slope) < 0.f);
+    for (int i = LANE; i < nv; i += DX_WAVE) {
+      if (restart) dir[i] = -Mg[i];
+      Mdir[i] = restart ? -grad[i] : fmaf(beta, Mdir[i], -grad[i]);
+    }
     SYNC();
   }
   if (LANE == 0) c.I[I_NITER] = it;
