@@ -1853,6 +1853,30 @@ __device__ __forceinline__ void mat_vec(const float* M, const float* x, float* y
   if (LANE < n) y[LANE] = s;
 }
 
+// n <= 30: lane i holds row i of the packed symmetric M in registers (0 past n), loaded
+// once per solve; M x is then 30 readlanes of x and 30 FMAs per lane -- no LDS gather and
+// no packed-index arithmetic per product (the Newton solve takes ~4.4 per substep).
+__device__ __forceinline__ void mrow_load(const float* M, int n, float (&mr)[30]) {
+  const int i = min(LANE, n - 1);
+#pragma unroll
+  for (int k = 0; k < 30; k++) {
+    const int kc = min(k, n - 1);
+    const float t = M[ti(max(i, kc)) + min(i, kc)];
+    mr[k] = LANE < n && k < n ? t : 0.f;
+  }
+}
+__device__ __forceinline__ void mat_vec_rows(const float (&mr)[30], const float* x, float* y, int n) {
+  const float xi = x[min(LANE, n - 1)];
+  float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 30; k += 2) {
+    s0 = fmaf(mr[k], rl(xi, k), s0);
+    s1 = fmaf(mr[k + 1], rl(xi, k + 1), s1);
+  }
+  if (LANE < n) y[LANE] = s0 + s1;
+}
+__device__ float dx_mrow_none[30];  // (the reference line_search / eval_cost take when MREG is off)
+
 template <class Ctx>
 __device__ __forceinline__ void jac_rows(const Ctx& c, const float* x, float* out);
 // J x for every row -> out[r]; uses cq as contact-frame scratch.  The contact
@@ -1953,10 +1977,12 @@ __device__ __forceinline__ float total_cost(const Ctx& c, const float* qacc, con
 }
 
 // jar = J qacc - aref, Ma = M qacc; returns cost
-template <class Ctx>
-__device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma, float* gauss = nullptr) {
+template <bool MREG = false, class Ctx>
+__device__ __forceinline__ float eval_cost(const Ctx& c, const float* qacc, float* Ma, float* gauss = nullptr,
+                                           const float (&mr)[30] = dx_mrow_none) {
   int nv = c.nv;
-  mat_vec(c.f(c.L.M), qacc, Ma, nv);
+  if (MREG) mat_vec_rows(mr, qacc, Ma, nv);
+  else mat_vec(c.f(c.L.M), qacc, Ma, nv);
   stage_mark(c, ST_MATVEC);
   float* jar = c.f(c.L.efc_jar);
   jac_vec(c, qacc, jar);
@@ -2306,15 +2332,18 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // the line as gauss + alpha qb + alpha^2 qa / 2 (M qacc_smooth = qfrc_smooth), so the
 // solver needs no separate cost pass.
 // HAVE_MDIR: the caller already holds M dir in v4 (CG's recurrence), no product here.
-template <bool NEWTON = false, bool HAVE_MDIR = false, class Ctx>
+// MREG: M's rows in registers (mrow_load), the product without LDS.
+template <bool NEWTON = false, bool HAVE_MDIR = false, bool MREG = false, class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed,
                                              float* slope0 = nullptr, const float* grad = nullptr,
-                                             float gauss = 0.f, float* cost_new = nullptr, float* gauss_new = nullptr) {
+                                             float gauss = 0.f, float* cost_new = nullptr, float* gauss_new = nullptr,
+                                             const float (&mr)[30] = dx_mrow_none) {
   const DevModel& m = c.mdl();
   int nv = c.nv;
   float* Mdir = c.f(c.L.v4);
   if (!HAVE_MDIR) {
-    mat_vec(c.f(c.L.M), dir, Mdir, nv);
+    if (MREG) mat_vec_rows(mr, dir, Mdir, nv);
+    else mat_vec(c.f(c.L.M), dir, Mdir, nv);
     stage_mark(c, ST_MATVEC);
   }
   float* jv = c.f(c.L.efc_jv);
@@ -2997,7 +3026,11 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
   float gw = 0.f;
-  float cw = eval_cost(c, qacc, Ma, &gw);
+  // the incremental sweep path (nv <= 30, Newton): M's rows in registers for its products
+  const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
+  float mr[30];
+  if (inc && c.solver == 2) mrow_load(c.f(c.L.M), nv, mr);
+  float cw = inc && c.solver == 2 ? eval_cost<true>(c, qacc, Ma, &gw, mr) : eval_cost(c, qacc, Ma, &gw);
   // c.solver is a compile-time constant in a scene specialization (DX_DIMS), so a Newton
   // kernel carries no CG / PGS code
   if (c.solver == 0) {  // the dual solver starts from the warm start's forces
@@ -3026,7 +3059,6 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     solve_cg(c, scale, tol);
     return;
   }
-  const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
   float wo[DX_NCH][5] = {};
   for (; it < c.iterations; it++) {
     stage_count(c, CNT_NEWTON_IT);
@@ -3056,7 +3088,7 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float nc = 0.f, gnew = 0.f;
-    float alpha = inc ? line_search<true>(c, qacc, Ma, dir, &changed, nullptr, grad, gauss, &nc, &gnew)
+    float alpha = inc ? line_search<true, false, true>(c, qacc, Ma, dir, &changed, nullptr, grad, gauss, &nc, &gnew, mr)
                       : line_search(c, qacc, Ma, dir, &changed);
     stage_mark(c, ST_NEWTON_LS);
     // qacc += alpha dir; M qacc and J qacc - aref follow by linearity from the line
