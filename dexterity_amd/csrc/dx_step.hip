@@ -2468,10 +2468,14 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
   // region, which CG does not use), then one product per iteration; larger nv solve each
   // time (the LDS Cholesky)
   const bool inv = DX_SWEEP && nv <= 30;
-  if (inv) mfma_sweep_inverse30(M, nv, T);
+  float trow[30];  // lane i: row i of M^-1 in registers (mrow_load), one product per iteration
+  if (inv) {
+    mfma_sweep_inverse30(M, nv, T);
+    mrow_load(T, nv, trow);
+  }
   auto minv = [&]() {
     if (inv) {
-      mat_vec(T, grad, Mg, nv);
+      mat_vec_rows(trow, grad, Mg, nv);
       SYNC();
     } else {
       for (int i = LANE; i < nv; i += DX_WAVE) Mg[i] = grad[i];
