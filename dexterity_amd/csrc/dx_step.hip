@@ -3030,11 +3030,12 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
   float gw = 0.f;
-  // the incremental sweep path (nv <= 30, Newton): M's rows in registers for its products
   const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
+  // Newton with nv <= 30: M's rows in registers for the solve's products
+  const bool mreg = nv <= 30 && c.solver == 2;
   float mr[30];
-  if (inc && c.solver == 2) mrow_load(c.f(c.L.M), nv, mr);
-  float cw = inc && c.solver == 2 ? eval_cost<true>(c, qacc, Ma, &gw, mr) : eval_cost(c, qacc, Ma, &gw);
+  if (mreg) mrow_load(c.f(c.L.M), nv, mr);
+  float cw = mreg ? eval_cost<true>(c, qacc, Ma, &gw, mr) : eval_cost(c, qacc, Ma, &gw);
   // c.solver is a compile-time constant in a scene specialization (DX_DIMS), so a Newton
   // kernel carries no CG / PGS code
   if (c.solver == 0) {  // the dual solver starts from the warm start's forces
@@ -3092,8 +3093,10 @@ __device__ __forceinline__ void solve(const Ctx& c) {
     stage_mark(c, ST_NEWTON_CHOL);
     int changed = 0;
     float nc = 0.f, gnew = 0.f;
-    float alpha = inc ? line_search<true, false, true>(c, qacc, Ma, dir, &changed, nullptr, grad, gauss, &nc, &gnew, mr)
-                      : line_search(c, qacc, Ma, dir, &changed);
+    float alpha = inc    ? line_search<true, false, true>(c, qacc, Ma, dir, &changed, nullptr, grad, gauss, &nc, &gnew, mr)
+                  : mreg ? line_search<false, false, true>(c, qacc, Ma, dir, &changed, nullptr, nullptr, 0.f, nullptr,
+                                                           nullptr, mr)
+                         : line_search(c, qacc, Ma, dir, &changed);
     stage_mark(c, ST_NEWTON_LS);
     // qacc += alpha dir; M qacc and J qacc - aref follow by linearity from the line
     // search's M dir (v4) and J dir (efc_jv): no products recomputed (the Newton-mode
