@@ -3030,7 +3030,16 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = ws[i];
   SYNC();
   float gw = 0.f;
-  const bool inc = DX_SWEEP && nv <= 30 && c.nlimt == 0;  // incremental Hessian + sweep solve
+  // incremental Hessian + sweep solve: nv <= 30 and no tendon-limit row in this solve (a
+  // model with limited tendons -- the reach scenes -- takes it whenever none is active)
+  bool limt = false;
+  if (c.nlimt > 0) {
+    const int* meta = (const int*)c.f(c.L.efc_meta);
+    bool any = false;
+    for (int r = LANE; r < nefc; r += DX_WAVE) any |= (meta[r] & 15) == DXR_LIMT;
+    limt = __any(any);
+  }
+  const bool inc = DX_SWEEP && nv <= 30 && !limt;
   // Newton with nv <= 30: M's rows in registers for the solve's products
   const bool mreg = nv <= 30 && c.solver == 2;
   float mr[30];
