@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--envs-per-gpu", type=int, default=4096)
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="bounded CPU-baseline sample (all threads)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--host-api-steps", type=int, default=50, help="extra line: the host-action call shape (0: off)")
     return p.parse_args()
 
 
@@ -165,6 +166,46 @@ def cpu_baseline_reach_1env(seconds: float, hand: str = "adroit"):
     }
 
 
+def host_api_line(env, steps: int, warmup: int):
+    """The reference's own call shape at the headline size: `GoalEnvironment.step` with a
+    host action np.float32[B, nu] and the host TimeStep back every control step
+    (environment.py:25-34, task.py:63-73) -- dx_env_step_host through page-locked buffers,
+    then the dm_env-style float64 observation dict.  The random actions are drawn before
+    the timed region (the agent is not the environment's cost)."""
+    import numpy as np
+
+    from dexterity_amd import _lib
+
+    L = _lib.load()
+    B, nu = env.num_envs, env.model.nu
+    lo, hi = env.task.compiled.actuator_ctrlrange.T
+    acts = np.random.RandomState(7).uniform(lo, hi, size=(warmup + steps, B, nu)).astype(np.float32)
+    for i in range(warmup):
+        env.step(acts[i])
+    pin_a, pin_o = env._pin_act, env._pin_out
+    t_call = t_ts = 0.0
+    t0 = time.perf_counter()
+    for i in range(steps):
+        a = time.perf_counter()
+        np.copyto(pin_a, acts[warmup + i])
+        _lib.check(L.dx_env_step_host(env.ptr, pin_a.ctypes.data, pin_o.ctypes.data))
+        b = time.perf_counter()
+        ts = env._timestep_packed(pin_o)
+        t_call += b - a
+        t_ts += time.perf_counter() - b
+    dt = time.perf_counter() - t0
+    assert np.all(np.isfinite(ts.reward))
+    return {
+        "api": "GoalEnvironment.step(np.float32[%d, %d]) -> host TimeStep" % (B, nu),
+        "env_steps_per_s": round(B * steps / dt, 1),
+        "ms_per_step": round(dt / steps * 1e3, 4),
+        "ms_per_step_upload_step_download": round(t_call / steps * 1e3, 4),
+        "ms_per_step_timestep_dict": round(t_ts / steps * 1e3, 4),
+        "bytes_per_step": {"upload": B * nu * 4, "download": B * (env.obs_dim + 3) * 4},
+        "steps": steps,
+    }
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -255,6 +296,7 @@ def main():
                 p = json.load(f)
             if p.get("envs") == B:
                 traffic = p.get("hbm_bytes_per_launch")
+        host_api = host_api_line(env, args.host_api_steps, 5) if world == 1 and args.host_api_steps > 0 else None
         cpu, extra = None, []
         if world == 1 and not args.no_cpu_baseline:
             gpu_states = [ph.get(f) for f in (_lib.QPOS, _lib.QVEL, _lib.QACC_WARMSTART)]
@@ -316,6 +358,9 @@ def main():
                 },
             },
             "health": health,
+            # the reference's call shape (host action in, host TimeStep out), beside the
+            # device-resident headline
+            "host_api": host_api,
             "cpu_baseline": cpu,
             "cpu_baseline_extra": extra,
         }

@@ -37,7 +37,8 @@ EXPORTS = (
     "dx_allgather_obs", "dx_comm_allreduce_max", "dx_comm_barrier", "dx_sensor_enable",
     "dx_env_set_time_limit", "dx_set_outputs", "dx_env_create_shard",
     "dx_health", "dx_health_clear", "dx_ncon_histogram", "dx_env_set_goal_time_limit",
-    "dx_env_step_random", "dx_env_save", "dx_env_load", "dx_env_state_field",
+    "dx_env_step_random", "dx_env_save", "dx_env_load", "dx_env_state_field", "dx_env_step_host",
+    "dx_build_key",
 )
 COMM_ID_BYTES = 128
 STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constraints", "velocity",
@@ -48,7 +49,7 @@ COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "
             31: "np_trips", 32: "broad_keep", 33: "mid_pairs", 34: "mid_keep", 35: "queue_wait"}
 NSTAGE = 40
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES, OUT_GOAL_QPOS = range(8)
-TASK_REORIENT, TASK_REACH = 0, 1
+TASK_REORIENT, TASK_REACH, TASK_HANDOVER = 0, 1, 2
 REACH_NPARAMS_HEAD = 26
 
 _lib = None
@@ -83,6 +84,16 @@ def load(path: str = LIB_PATH):
             f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
         )
     L = ctypes.CDLL(path)
+    L.dx_build_key.restype = ctypes.c_char_p
+    if path == os.path.join(_HERE, "libdx.so") and os.path.isdir(os.path.join(_HERE, "csrc")):
+        # the in-tree library must have been built from the sources beside it (a GPU box
+        # runs the library that travelled with the tree, without rebuilding)
+        from dexterity_amd import build as _build
+
+        want, have = _build.source_key(), L.dx_build_key().decode()
+        if want != have:
+            raise DxError(f"{path} was built from other sources (key {have}, sources {want}): rebuild it "
+                          "(python -c 'import __graft_entry__ as g; g.build()')")
     vp, i32, sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_size_t
     L.dx_model_load.restype = vp
     L.dx_model_load.argtypes = [ctypes.c_char_p, sz]
@@ -139,6 +150,7 @@ def load(path: str = LIB_PATH):
     L.dx_env_state_field.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
                                      ctypes.POINTER(sz)]
     L.dx_env_pack_outputs.argtypes = [vp, vp]
+    L.dx_env_step_host.argtypes = [vp, vp, vp]
     L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.dx_stage_timing.argtypes = [vp, ctypes.c_int]

@@ -64,7 +64,12 @@ def _units() -> list:
     """(object name, source, extra flags): every source once, plus dx_step.hip once per
     scene specialization (-DDX_SPEC_ONLY), so the kernels compile in parallel."""
     units = [(os.path.splitext(s)[0], s, ()) for s in SOURCES]
-    units += [(f"dx_step_{n}", "dx_step.hip", (f"-DDX_SPEC_ONLY={n}",)) for n in _spec_names()]
+    # a PGS specialization runs one wave per SIMD: AR's diagonal blocks and the rows' P
+    # take ~420 VGPRs (dx_step.hip solve_pgs_ar), which two waves per SIMD would spill
+    pgs_waves = os.environ.get("DX_PGS_WAVES", "1")
+    units += [(f"dx_step_{n}", "dx_step.hip",
+               (f"-DDX_SPEC_ONLY={n}",) + ((f"-DDX_STEP_WAVES={pgs_waves}",) if n.endswith("_pgs") else ()))
+              for n in _spec_names()]
     # the overflow tier: the step kernel's physics with the DX_NCON_HI contact pool
     units.append(("dx_step_hi", "dx_step.hip", ("-DDX_TIER_HI", "-DDX_NCON_MAX=DX_NCON_HI")))
     # the mid tier: the same physics with the DX_NCON_MID pool, beside queued launches
@@ -83,19 +88,30 @@ def _compile(out: str, verbose: bool) -> None:
         _compile_locked(out, verbose)
 
 
-def _compile_locked(out: str, verbose: bool) -> None:
-    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+def source_key(csrc: str = None) -> str:
+    """Hash of everything a libdx.so is built from (sources, headers, the scene
+    specializations, the C ABI header, the flags).  The library carries it
+    (dx_build_key), and _lib.load refuses an in-tree library built from other sources."""
+    csrc = csrc or CSRC
     h = hashlib.sha1()
     for f in sorted(SOURCES + HEADERS + ("dx_specs.inc",)):
-        path = os.path.join(CSRC, f)
+        path = os.path.join(csrc, f)
         if os.path.exists(path):
             h.update(f.encode() + open(path, "rb").read())
     h.update(open(os.path.join(ROOT, "include", "dx.h"), "rb").read())
     h.update(" ".join(FLAGS).encode())
-    key = h.hexdigest()[:16]
+    return h.hexdigest()[:16]
+
+
+def _compile_locked(out: str, verbose: bool) -> None:
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    key = source_key()
     jobs, objs = [], []
     for name, src, extra in _units():
-        obj = os.path.join(OBJ, f"{name}.{key}.o")
+        if src == "dx_api.hip":
+            extra = extra + (f'-DDX_BUILD_KEY="{key}"',)
+        xk = hashlib.sha1(" ".join(extra).encode()).hexdigest()[:6]  # (per-unit flags: DX_PGS_WAVES)
+        obj = os.path.join(OBJ, f"{name}.{key}{xk}.o")
         objs.append(obj)
         if not os.path.exists(obj):
             jobs.append(([hipcc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", f"{obj}.{os.getpid()}.tmp"], obj))

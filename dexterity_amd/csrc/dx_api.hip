@@ -1592,10 +1592,14 @@ extern "C" dx_env* dx_env_create(const dx_model* m, int32_t nenv, int32_t device
 extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t device, int32_t task,
                                        uint64_t seed, int64_t env0, const float* params, int32_t nparams) {
   if (env0 < 0 || env0 + (int64_t)nenv > 0x7fffffffll) { fail(DX_EINVAL, "env0 out of range"); return nullptr; }
-  if (task != DX_TASK_REORIENT && task != DX_TASK_REACH) { fail(DX_EINVAL, "unknown task kind"); return nullptr; }
+  if (task != DX_TASK_REORIENT && task != DX_TASK_REACH && task != DX_TASK_HANDOVER) {
+    fail(DX_EINVAL, "unknown task kind");
+    return nullptr;
+  }
   if (!m) { fail(DX_EINVAL, "null model"); return nullptr; }
   const int nq = m->dm.nq, nu = m->dm.nu;
   if (!params || (task == DX_TASK_REORIENT && nparams < DX_REORIENT_NPARAMS) ||
+      (task == DX_TASK_HANDOVER && nparams < DX_HANDOVER_NPARAMS) ||
       (task == DX_TASK_REACH && nparams < DX_REACH_NPARAMS_HEAD + 3 * nq + nu * nq)) {
     fail(DX_EINVAL, "too few task params");
     return nullptr;
@@ -1607,7 +1611,7 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
   const DevModel& d = b->dm;
   TaskParams& P = e->P;
   memset(&P, 0, sizeof(P));
-  P.kind = task == DX_TASK_REACH ? DX_KIND_REACH : DX_KIND_REORIENT;
+  P.kind = task == DX_TASK_REACH ? DX_KIND_REACH : task == DX_TASK_HANDOVER ? DX_KIND_HANDOVER : DX_KIND_REORIENT;
   P.nenv = nenv; P.nq = d.nq; P.nv = d.nv; P.nu = d.nu; P.nsite = d.nsite;
   P.seed = seed;
   P.env0 = (int)env0;
@@ -1615,11 +1619,11 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
   P.hand_nq = (int)params[1]; P.hand_nv = (int)params[2];
   int watch_geom = -1, watch_body = -1;
   bool bad = false;
-  if (task == DX_TASK_REORIENT) {
+  if (task != DX_TASK_REACH) {  // reorient, and the handover on the same params
     P.prop_qadr = (int)params[3]; P.prop_dadr = (int)params[4];
     int tip0 = (int)params[5];
     P.ntips = (int)params[6];
-    for (int t = 0; t < P.ntips && t < 8; t++) P.tip_sites[t] = tip0 + t;
+    for (int t = 0; t < P.ntips && t < DX_MAX_TIPS; t++) P.tip_sites[t] = tip0 + t;
     P.successes_needed = (int)params[7]; P.steps_before_change = (int)params[8];
     P.fall_termination = (int)params[9];
     P.threshold = params[10]; P.eps = params[11]; P.w_orient = params[12]; P.w_success = params[13];
@@ -1635,13 +1639,20 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
       }
     }
     watch_geom = (int)params[22]; watch_body = (int)params[23];
-    P.goal_dim = 4;
-    P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + (P.prop_qadr >= 0 ? 17 : 0) + 4;
+    P.goal_dim = 4;  // the target quaternion, or (handover) the target point and receiving hand
+    // (the handover has no hint prop: no target_prop/orientation block)
+    const int prop_obs = P.prop_qadr < 0 ? 0 : task == DX_TASK_HANDOVER ? 13 : 17;
+    P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + prop_obs + 4;
     bad = P.prop_qadr >= 0 && (P.prop_qadr + 7 > d.nq || P.prop_dadr + 6 > d.nv);
+    if (task == DX_TASK_HANDOVER) {
+      for (int h = 0; h < 2; h++)
+        for (int k = 0; k < 3; k++) P.hand_target[h][k] = params[38 + 3 * h + k];
+      bad = bad || P.prop_qadr < 0;
+    }
   } else {
     P.prop_qadr = -1; P.prop_dadr = -1;
     P.ntips = (int)params[3];
-    for (int t = 0; t < P.ntips && t < 8; t++) P.tip_sites[t] = (int)params[4 + t];
+    for (int t = 0; t < P.ntips && t < DX_MAX_TIPS; t++) P.tip_sites[t] = (int)params[4 + t];
     P.successes_needed = (int)params[9]; P.steps_before_change = (int)params[10];
     P.threshold = params[11]; P.max_time = params[12]; P.dense = (int)params[13];
     P.range_frac = params[14]; P.goal_scale = params[15]; P.max_reject = (int)params[16];
@@ -1655,8 +1666,8 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
     P.obs_dim = 2 * P.hand_nq + P.hand_nv + 6 * P.ntips + P.goal_dim;
     bad = bad || P.hand_nq != d.nq || P.ncoupled > 4 || P.max_reject < 1;
   }
-  for (int t = 0; t < P.ntips && t < 8; t++) bad = bad || P.tip_sites[t] < 0 || P.tip_sites[t] >= d.nsite;
-  if (bad || P.ntips > 8 || P.hand_nq > d.nq || P.hand_nv > d.nv || e->nsub < 1) {
+  for (int t = 0; t < P.ntips && t < DX_MAX_TIPS; t++) bad = bad || P.tip_sites[t] < 0 || P.tip_sites[t] >= d.nsite;
+  if (bad || P.ntips > DX_MAX_TIPS || P.hand_nq > d.nq || P.hand_nv > d.nv || e->nsub < 1) {
     fail(DX_EINVAL, "task parameters inconsistent with the model");
     dx_batch_destroy(b);
     delete e;
@@ -1678,7 +1689,7 @@ extern "C" dx_env* dx_env_create_shard(const dx_model* m, int32_t nenv, int32_t 
   rc |= al((void**)&S.time_d, E * 8); rc |= al((void**)&S.solve_start_d, E * 8);
   rc |= al((void**)&S.nsub_d, E * 4); rc |= al((void**)&S.solve_n, E * 4);
   if (task == DX_TASK_REACH) rc |= al((void**)&S.goal_qpos, E * nq * 4);
-  if (task == DX_TASK_REORIENT) {
+  if (task != DX_TASK_REACH) {
     rc |= al((void**)&S.mt_env, E * DX_MT_WORDS * 4);
     rc |= al((void**)&S.mt_goal, E * DX_MT_WORDS * 4);
     if (!rc) {
@@ -1756,7 +1767,7 @@ extern "C" __global__ void dx_sample_actions_kernel(int nenv, int nu, const floa
 static int env_run(dx_env* e, const float* action, bool random = false, uint64_t seed = 0, int step = 0) {
   dx_batch* b = e->batch;
   HIPCHK(hipSetDevice(b->device));
-  const bool fuse = !getenv("DX_NO_FUSE") && ((e->P.kind == DX_KIND_REORIENT && b->db.defer) ||
+  const bool fuse = !getenv("DX_NO_FUSE") && ((e->P.kind != DX_KIND_REACH && b->db.defer) ||
                                               (e->P.kind == DX_KIND_REACH && b->spec >= 0 && dx_spec_reach(b->spec)));
   if (fuse) {
     DevBatch& B = b->db;
@@ -2036,6 +2047,38 @@ extern "C" int dx_env_pack_outputs(dx_env* e, float* dst_dev) {
   hipLaunchKernelGGL(dx_pack_outputs_kernel, dim3((n + 255) / 256), dim3(256), 0, b->stream, e->P.nenv,
                      e->P.obs_dim, e->S.obs, e->S.reward, e->S.discount, e->S.step_type, dst_dev);
   HIPCHK(hipGetLastError());
+  return 0;
+}
+
+#ifndef DX_BUILD_KEY
+#define DX_BUILD_KEY "unkeyed"
+#endif
+// The hash of the sources this library was built from (dexterity_amd/build.py source_key)
+extern "C" const char* dx_build_key(void) { return DX_BUILD_KEY; }
+
+// The reference's own call shape: GoalEnvironment.step(action) with a host action and a
+// host TimeStep back (environment.py:25-34, task.py:63-73).  One stream: the action's
+// upload into the library's action buffer, the control step, the pack of [obs | reward |
+// discount | step_type] and its download, then one synchronisation.  With page-locked
+// host buffers both copies are DMA transfers queued behind / ahead of the kernels.
+extern "C" int dx_env_step_host(dx_env* e, const float* action_host, float* out_host) {
+  if (!e || !action_host || !out_host) return fail(DX_EINVAL, "null argument");
+  dx_batch* b = e->batch;
+  HIPCHK(hipSetDevice(b->device));
+  void* act = nullptr;
+  if (int rc = dx_env_action_buffer(e, &act)) return rc;
+  const size_t nout = (size_t)e->P.nenv * (e->P.obs_dim + 3);
+  if (e->allocs.size() < 2) {  // the packed outputs' device buffer
+    void* p = nullptr;
+    if (int rc = balloc(b, &p, nout * 4)) return rc;
+    e->allocs.push_back(p);
+  }
+  float* pack = (float*)e->allocs[1];
+  HIPCHK(hipMemcpyAsync(act, action_host, (size_t)e->P.nenv * e->P.nu * 4, hipMemcpyHostToDevice, b->stream));
+  if (int rc = env_run(e, (const float*)act)) return rc;
+  if (int rc = dx_env_pack_outputs(e, pack)) return rc;
+  HIPCHK(hipMemcpyAsync(out_host, pack, nout * 4, hipMemcpyDeviceToHost, b->stream));
+  HIPCHK(hipStreamSynchronize(b->stream));
   return 0;
 }
 

@@ -208,6 +208,7 @@ struct SpecRT {
 // reference.)
 template <class SP>
 struct CtxT {
+  static constexpr bool is_spec = true;  // a scene specialization (dims and layout constant)
   const DevModel& m;
   static constexpr Lds L = SP::L;
 #define DX_X(n) static constexpr int n = SP::n;
@@ -227,6 +228,7 @@ struct CtxT {
 };
 template <>
 struct CtxT<SpecRT> {
+  static constexpr bool is_spec = false;
   const DevModel& m;
   const Lds& L;
 #define DX_X(n) int n;
@@ -1118,6 +1120,134 @@ __device__ __forceinline__ void chol_solve(const float* A, int n, DiagAdd dd, fl
 }
 __device__ __forceinline__ void chol_solve(const float* A, int n, float* x, float* T) {
   chol_solve(A, n, DiagAdd{0.f, 0.f}, x, T);
+}
+
+// The Cholesky factor of an n <= 30 SPD matrix, in place: A (packed lower triangle,
+// LDS) -> G (packed lower triangle with its diagonal), G G' = A.  The factorisation of
+// mfma_chol_solve32 (two columns per step, one rank-2 MFMA on the trailing matrix),
+// storing each column pair as it is produced; A is read whole before the first store.
+__device__ __forceinline__ void mfma_chol_factor30(float* A, int n) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  const int jc = min(j, n - 1);
+  float av[16];
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int ic = min(8 * (v >> 2) + 4 * hi + (v & 3), n - 1);
+    av[v] = A[ti(max(ic, jc)) + min(ic, jc)];
+  }
+  dx_f16v C;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    C[v] = i < n && j < n ? av[v] : (i == j ? 1.f : 0.f);
+  }
+  SYNC();
+#pragma unroll
+  for (int k = 0; k < 30; k += 2) {
+    if (k >= n) continue;  // identity padding (a uniform branch)
+    const int vk = 4 * (k >> 3) + (k & 3);
+    const bool up = (k & 7) >= 4;
+    const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // C[k][j], C[k+1][j]
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
+    const float l21 = rl(rk1, k) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    const float lk = rk * i11;                 // G[j][k]   (j >= k; the diagonal at j = k)
+    const float lk1 = (rk1 - lk * l21) * i22;  // G[j][k+1] (j >= k + 1)
+    if (hi == 0 && j >= k && j < n) A[ti(j) + k] = lk;
+    if (hi == 0 && j > k && j < n) A[ti(j) + k + 1] = lk1;
+    const float p = j > k + 1 ? (hi ? lk1 : lk) : 0.f;
+    C = __builtin_amdgcn_mfma_f32_32x32x2f32(-p, p, C, 0, 0, 0);
+  }
+  SYNC();
+}
+
+// The Gram matrix P P' of the wave's 64 rows on the matrix cores: lane k holds row k of
+// P (30 entries, zero past nv); out[r] in lane k is P_r . P_k, plus diag (this lane's
+// value) on the diagonal -- lane k holds column k.  Rows 0-31 and 32-63 are the two row
+// tiles: one v_permlane32_swap of (P[2s], P[2s+1]) gives both tiles' A operands of k step
+// s (lanes 0-31 supply P[i][2s], lanes 32-63 P[i][2s+1] of the tile's row i), and B = A'
+// is the same operand, so the four 32 x 32 tiles take 15 v_mfma_f32_32x32x2_f32 each
+// (`full`: rows past 32 exist; else tile (0, 0) alone).  The accumulator holds C[i][j] in
+// lane j + 32 b for the rows i with bit 2 = b; one more swap per register pair gives
+// every lane its whole column.
+__device__ __forceinline__ void pgs_gram64(const float (&P)[30], float diag, bool full, float (&out)[64]) {
+  const int l = LANE;
+  const int j = l & 31, hi = l >> 5;
+  const float d0 = half_dup(diag, false), d1 = half_dup(diag, true);  // diag of rows j and 32 + j
+  dx_f16v C00, C10, C01, C11;
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int i = 8 * (v >> 2) + 4 * hi + (v & 3);
+    C00[v] = i == j ? d0 : 0.f;
+    C11[v] = i == j ? d1 : 0.f;
+    C10[v] = 0.f;
+    C01[v] = 0.f;
+  }
+  if (full) {
+#pragma unroll
+    for (int s = 0; s < 15; s++) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(P[2 * s]), __float_as_uint(P[2 * s + 1]), false, false);
+      const float a0 = __uint_as_float(sw[0]), a1 = __uint_as_float(sw[1]);
+      C00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a0, C00, 0, 0, 0);
+      C10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, a0, C10, 0, 0, 0);
+      C01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a1, C01, 0, 0, 0);
+      C11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, a1, C11, 0, 0, 0);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 15; s++) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(P[2 * s]), __float_as_uint(P[2 * s + 1]), false, false);
+      const float a0 = __uint_as_float(sw[0]);
+      C00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a0, C00, 0, 0, 0);
+    }
+    C11 = C10;  // (zero)
+  }
+  // lane j (< 32) keeps its rows of tiles (., 0) and takes lane j + 32's; lane j + 32
+  // keeps its rows of tiles (., 1) and takes lane j's: after the swap sw[0] holds the
+  // rows with bit 2 clear of this lane's column, sw[1] those with bit 2 set
+#pragma unroll
+  for (int v = 0; v < 16; v++) {
+    const int r = 8 * (v >> 2) + (v & 3);
+    const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(C00[v]), __float_as_uint(C01[v]), false, false);
+    out[r] = __uint_as_float(s0[0]);
+    out[r + 4] = __uint_as_float(s0[1]);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(C10[v]), __float_as_uint(C11[v]), false, false);
+    out[32 + r] = __uint_as_float(s1[0]);
+    out[32 + r + 4] = __uint_as_float(s1[1]);
+  }
+}
+
+// Reduce-scatter of 32-vectors over the wave: each lane holds t[0..31]; returns, in lane
+// L, component c = L >> 1 of the sum over all 64 lanes (lanes 2c and 2c + 1 hold it).  A
+// permlane32 swap halves the vectors across the half-waves (16 adds), a permlane16 swap
+// across the rows (8), then row_mirror, row_half_mirror and two quad_perms within the
+// rows (4 + 2 + 1 + 1): 32 adds and 70 instructions in all, against 32 wave sums.
+__device__ __forceinline__ float wave_reduce_scatter32(const float (&t)[32]) {
+  float u[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) {  // u[i]: component i + 16 b5
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(t[i]), __float_as_uint(t[16 + i]), false, false);
+    u[i] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  float v[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) {  // v[i]: component i + 8 b4 + 16 b5
+    const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(u[i]), __float_as_uint(u[8 + i]), false, false);
+    v[i] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
+  }
+  const int L = LANE;
+  const bool b3 = (L >> 3) & 1, b2 = (L >> 2) & 1, b1 = (L >> 1) & 1;
+  float x[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++)  // + 4 b3; the partner 15 - L (row_mirror) has b3 flipped
+    x[i] = (b3 ? v[4 + i] : v[i]) + dpp_f<0x140, 0xF>(b3 ? v[i] : v[4 + i]);
+  float y[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++)  // + 2 b2; the partner 7 - L within the half-row (row_half_mirror)
+    y[i] = (b2 ? x[2 + i] : x[i]) + dpp_f<0x141, 0xF>(b2 ? x[i] : x[2 + i]);
+  const float z = (b1 ? y[1] : y[0]) + dpp_f<0x4E, 0xF>(b1 ? y[0] : y[1]);  // + b1; partner L ^ 2
+  return z + dpp_f<0xB1, 0xF>(z);                                          // partner L ^ 1
 }
 
 // x <- (M + diag(dd))^-1 x for a matrix with the kinematic tree's sparsity (M, and

@@ -243,19 +243,21 @@ struct Lds {
 };
 
 // Task parameters and per-env task state, see dx_task.hip.
-enum { DX_KIND_REORIENT = 0, DX_KIND_REACH = 1 };
+enum { DX_KIND_REORIENT = 0, DX_KIND_REACH = 1, DX_KIND_HANDOVER = 2 };
+#define DX_MAX_TIPS 16  // fingertip sites a task observes (two hands: 10)
 struct TaskParams {
   int kind;                 // DX_KIND_*
   int nenv, nq, nv, nu, nsite;
   int hand_nq, hand_nv;     // hand joints are qpos[0:hand_nq], qvel[0:hand_nv]
   int prop_qadr, prop_dadr; // free joint of the prop (reorient), -1 otherwise
   int ntips;                // fingertip sites
-  int tip_sites[8];
+  int tip_sites[DX_MAX_TIPS];
   int obs_dim, goal_dim;
   int successes_needed, steps_before_change, fall_termination;
   float threshold, eps, w_orient, w_success, w_action, max_time, timestep_ctrl;
   float time_limit;         // composer Environment time_limit (s); +inf: none
   float bbox_lo[3], bbox_hi[3];
+  float hand_target[2][3];  // handover: the point above each palm the cube is handed to
   double bbox_lo_d[3], bbox_hi_d[3];  // the same box in fp64 (the reference's values)
   // reach (fingertip_position.py / dexterous_hand.py samplers)
   int dense, max_reject, ncoupled;

@@ -2554,6 +2554,14 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
       Mdir[i] = restart ? -grad[i] : fmaf(beta, Mdir[i], -grad[i]);
     }
     SYNC();
+    // The recurrences hold only as far as M Mg = grad does, i.e. to the rounding of the
+    // fp32 M^-1: M qacc and M dir exactly on a restart and every 8 iterations, so the
+    // gradient (and CG's stopping point) does not drift from the cost's
+    if (restart || (it & 7) == 7) {
+      mat_vec(M, qacc, Ma, nv);
+      mat_vec(M, dir, Mdir, nv);
+      SYNC();
+    }
   }
   if (LANE == 0) c.I[I_NITER] = it;
   SYNC();
@@ -2600,55 +2608,269 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
   SYNC();
 }
 
-#ifndef DX_PGS_AR
-#define DX_PGS_AR 64  // PGS on AR in registers (one column per lane) up to this many rows
+#ifndef DX_PGS_NB
+#define DX_PGS_NB 2  // PGS register blocks of 64 rows (AR's diagonal blocks, one column per lane)
 #endif
-// y = M^-1 J_k' for constraint row k of this lane (k < 0: zero), nv <= 30, from the row's
-// compact form (jac_rows / pgs_jrow) and Minv, the sweep's inverse as a packed lower
-// triangle in LDS: y[d] = sum over the row's nonzeros (e, v) of Minv[d][e] v.
-template <class Ctx>
-__device__ __forceinline__ void pgs_minv_row(const Ctx& c, int k, const float* Minv, float (&y)[30]) {
+#define DX_PGS_AR 64
+// Visit the nonzeros (e, v) of constraint row k (k < 0: none) from the row's compact form
+// (jac_rows / pgs_jrow): one dof (friction loss, joint limit), a tendon's dofs, or a
+// contact row's support dofs.  k may differ by lane (then e and v do too) or be uniform.
+template <class Ctx, class F>
+__device__ __forceinline__ void pgs_row_nz(const Ctx& c, int k, F&& add) {
   const DevModel& m = c.mdl();
   const int nv = c.nv;
-#pragma unroll
-  for (int d = 0; d < 30; d++) y[d] = 0.f;
   const int mt = k >= 0 ? ((const int*)c.f(c.L.efc_meta))[k] : 0;
   const int type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
   const bool on = k >= 0;
-  // the row's nonzeros: one dof (friction loss, joint limit), a tendon's dofs, or a
-  // contact row's support dofs
   const bool con = on && (type == DXR_CON || type == DXR_CONFL);
   const float* rc = c.f(c.L.con) + DX_CON_STRIDE * (con ? id : 0);
   uint64_t sup = con ? ((uint64_t)(uint32_t)__float_as_int(rc[18]) | ((uint64_t)(uint32_t)__float_as_int(rc[19]) << 32)) : 0ull;
   const int kk = 1 + (aux >> 1);
   const float mu = type == DXR_CON ? rc[15 + kk] * ((aux & 1) ? -1.f : 1.f) : 0.f;
   const float* cv = c.f(c.L.cj_val) + (con ? id : 0) * 3 * DX_DOFMAX;
-  auto add = [&](int e, float v) {  // y += Minv[:, e] v
-#pragma unroll
-    for (int d = 0; d < 30; d++) {
-      const int dc = min(d, nv - 1);
-      y[d] = fmaf(Minv[ti(max(dc, e)) + min(dc, e)], d < nv ? v : 0.f, y[d]);
-    }
-  };
-  if (on && (type == DXR_FRIC || type == DXR_LIMJ)) add(id, type == DXR_LIMJ && aux ? -1.f : 1.f);
-  if (c.nlimt > 0 && on && type == DXR_LIMT)
+  const bool one = on && (type == DXR_FRIC || type == DXR_LIMJ);
+  if (__any(one)) add(one ? id : 0, one ? (type == DXR_LIMJ && aux ? -1.f : 1.f) : 0.f);
+  if (c.nlimt > 0 && __any(on && type == DXR_LIMT))
     for (int e = 0; e < nv; e++) {
-      const float tj = m.tendon_J[id * nv + e];
-      add(e, aux ? -tj : tj);
+      const float tj = m.tendon_J[(on && type == DXR_LIMT ? id : 0) * nv + e];
+      add(e, on && type == DXR_LIMT ? (aux ? -tj : tj) : 0.f);
     }
 #pragma unroll 1
-  for (int q = 0; q < DX_DOFMAX; q++) {  // (not unrolled: y is what stays live)
+  for (int q = 0; q < DX_DOFMAX; q++) {  // (not unrolled: the caller's accumulators stay live)
+    if (!__any(sup != 0ull)) break;
     const int e = sup ? (int)__builtin_ctzll(sup) : 0;
     const float v = sup ? cv[q] + mu * cv[kk * DX_DOFMAX + q] : 0.f;
     sup &= sup - 1;
     if (__any(v != 0.f)) add(e, v);
   }
 }
+// P_k = G' J_k' for constraint row k of this lane (k < 0: zero), nv <= 30, where G (a
+// packed lower triangle with its diagonal in LDS, mfma_chol_factor30) is the Cholesky
+// factor of M^-1: y[d] = sum over the row's nonzeros (e, v) of G[e][d] v (d <= e), so
+// that P_k . P_r = J_k M^-1 J_r' = A[k][r].
+template <class Ctx>
+__device__ __forceinline__ void pgs_p_row(const Ctx& c, int k, const float* G, float (&y)[30]) {
+  const int nv = c.nv;
+#pragma unroll
+  for (int d = 0; d < 30; d++) y[d] = 0.f;
+  pgs_row_nz(c, k, [&](int e, float v) {
+#pragma unroll
+    for (int d = 0; d < 30; d++) y[d] = fmaf(G[ti(e) + min(d, e)], d <= e && d < nv ? v : 0.f, y[d]);
+  });
+}
+// Lane d: (G' J_r')[d] for a uniform row r (the tail rows past the register blocks)
+template <class Ctx>
+__device__ __forceinline__ float pgs_p_lane(const Ctx& c, int r, const float* G) {
+  const int d = LANE, nv = c.nv;
+  float p = 0.f;
+  pgs_row_nz(c, r, [&](int e, float v) { p = fmaf(G[ti(e) + min(d, e)], d <= e && d < nv ? v : 0.f, p); });
+  return p;
+}
 // f(std::integral_constant<int, I>) for I in the sequence, unrolled: a register array
 // indexed by I stays in registers
 template <class F, int... I>
 __device__ __forceinline__ void static_for(F&& f, std::integer_sequence<int, I...>) {
   (f(std::integral_constant<int, I>{}), ...);
+}
+// PGS on MuJoCo's own form (mj_solPGS on efc_AR) for nv <= 30, solve_pgs's path up to
+// DX_PGS_NB x 64 rows (+ a tail of 64).  AR = J M^-1 J' + R is held in registers in
+// diagonal blocks of 64 rows, lane k holding column k of its block (A[B][r] = AR[64B +
+// r][64B + k], AR is symmetric); the coupling between blocks is carried in "whitened"
+// force space.  With G the Cholesky factor of M^-1 (mfma_chol_factor30 over the sweep's
+// inverse) and P_k = G' J_k' (lane k of block B holds its row's P, 30 registers), AR =
+// P P' + R, and the residual of row k is res_k = (AR f)_k + b_k = P_k . w + R_k f_k + b_k
+// with w = sum over all rows of f_r P_r and b = J qacc_smooth - aref.
+//  * Forming: P by the rows' compact forms (pgs_p_row), each diagonal block P_B P_B' on
+//    the matrix cores (pgs_gram64: 15-60 v_mfma_f32_32x32x2_f32) -- the batched J M^-1 J'
+//    contraction;
+//  * a block's sweep starts from its residuals recomputed from w (w reduce-scattered
+//    over the lanes from every lane's f P, wave_reduce_scatter32, then 30 readlanes and
+//    FMAs) -- the Gauss-Seidel sweep in row order, with no matrix-free pass through J,
+//    M^-1 and J';
+//  * a row update runs in the row's own lane: every lane projects its own candidate
+//    (fmed3 of f - res / AR_kk onto the row's box [-floss, floss] or [0, inf); padding rows
+//    past nefc have the box [0, 0]), the row's change is one readlane, and every lane's
+//    residual takes one FMA with its AR entry: 7 instructions, no reduction and no
+//    per-row broadcast of the row's constants on the chain from one row to the next;
+//  * the sweep's dual-cost decrease sum_r -(AR_rr df_r^2 / 2 + df_r res_r) from each lane's
+//    force change and its residual at its own update (snapshot), one wave sum per sweep;
+//  * rows past the blocks (the tail) run one at a time in w space: lane d holds w[d] and
+//    (G' J_r')[d] (pgs_p_lane), res_r = wave sum + R_r f_r + b_r, w += df P_r;
+//  * at the end qacc = qacc_smooth + M^-1 J'f = qacc_smooth + G w.
+// Rows visited, projections and stopping test are the oracle's (dx_oracle.c solve_pgs).
+template <int NB, class Ctx>
+__device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float tol, float* T) {
+  const int nv = c.nv, nefc = c.I[I_NEFC];
+  float* qacc = c.f(c.L.qacc);
+  const float* a0 = c.f(c.L.qacc_smooth);
+  float* f = c.f(c.L.efc_jv);
+  float* jar = c.f(c.L.efc_jar);
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* D = c.f(c.L.efc_D);
+  const float* fl = c.f(c.L.efc_fl);
+  const float* aref = c.f(c.L.efc_aref);
+  const int nb = min(NB, (nefc + DX_PGS_AR - 1) / DX_PGS_AR);  // blocks in use
+  const int ntail = max(0, nefc - NB * DX_PGS_AR);
+  jac_vec(c, a0, jar);       // J qacc_smooth (the warm start's residuals were consumed): b = jar - aref
+  mfma_chol_factor30(T, nv);  // G over M^-1
+  const float* G = T;
+  auto box = [&](int k, float& lo, float& hi) {
+    const int kc = min(k, nefc - 1);
+    const bool fr = (meta[kc] & 15) == DXR_FRIC;
+    hi = k >= nefc ? 0.f : fr ? fl[kc] : __builtin_inff();
+    lo = fr && k < nefc ? -hi : 0.f;
+  };
+  constexpr auto blocks = std::make_integer_sequence<int, NB>{};
+  constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
+  float P[NB][30], A[NB][DX_PGS_AR];
+  float fb[NB], res[NB], idg[NB], lo[NB], hi[NB], rs[NB], bb[NB], rk[NB], hdg[NB];
+  static_for([&](auto Bc) {
+    constexpr int B = Bc.value;
+    const int k = DX_PGS_AR * B + LANE;
+    const bool in = k < nefc;
+    const int kc = min(k, nefc - 1);
+    rk[B] = in ? 1.0f / D[kc] : 0.f;
+    fb[B] = in ? f[kc] : 0.f;
+    bb[B] = in ? jar[kc] - aref[kc] : 0.f;
+    box(k, lo[B], hi[B]);
+    res[B] = 0.f;
+    rs[B] = 0.f;
+    if (B < nb) {
+      pgs_p_row(c, in ? k : -1, G, P[B]);
+      pgs_gram64(P[B], rk[B], nefc > DX_PGS_AR * B + 32, A[B]);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 30; d++) P[B][d] = 0.f;
+      static_for([&](auto K) { A[B][K.value] = 0.f; }, rows);
+    }
+    float dg = 1.f;  // AR_kk, this lane's diagonal entry (1 on a padding row)
+    static_for([&](auto K) { dg = LANE == K.value ? A[B][K.value] : dg; }, rows);
+    dg = in ? dg : 1.f;
+    idg[B] = 1.0f / dg;
+    hdg[B] = 0.5f * dg;
+  }, blocks);
+  float ardt = 1.f;  // lane t: AR of tail row NB x 64 + t on the diagonal
+  for (int t = 0; t < ntail; t++) {
+    const int r = NB * DX_PGS_AR + t;
+    const float p = pgs_p_lane(c, r, G);
+    const float s = wave_sum(p * p) + 1.0f / D[r];
+    ardt = LANE == t ? s : ardt;
+  }
+  stage_mark(c, ST_NEWTON_HESS);
+  // w (lane d: w[d]) from every row's current force; wt, the tail rows' part, is kept
+  // current by their updates
+  float wt = 0.f, wl = 0.f;
+  auto wsum = [&]() {
+    float t[32];
+#pragma unroll
+    for (int d = 0; d < 32; d++) t[d] = 0.f;
+    static_for([&](auto Bc) {
+#pragma unroll
+      for (int d = 0; d < 30; d++) t[d] = fmaf(fb[Bc.value], P[Bc.value][d], t[d]);
+    }, blocks);
+    const float r = wave_reduce_scatter32(t);  // component LANE >> 1
+    const float wd = __int_as_float(__builtin_amdgcn_ds_bpermute(8 * (LANE & 31), __float_as_int(r)));
+    wl = (LANE < nv ? wd : 0.f) + wt;
+  };
+  auto dotw = [&](const float (&p)[30]) {
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int d = 0; d < 30; d += 2) {
+      s0 = fmaf(p[d], rl(wl, d), s0);
+      s1 = fmaf(p[d + 1], rl(wl, d + 1), s1);
+    }
+    return s0 + s1;
+  };
+  // one row update, in the row's lane q (q static: a register name of A[B])
+#define DX_PGS_ROWL(q, Acol, rsv, fv, idgv, lov, hiv, snap)                 \
+  {                                                                          \
+    const float fn = __builtin_amdgcn_fmed3f(fmaf(-rsv, idgv, fv), lov, hiv); \
+    const float dl = rl(fn - fv, q);                                         \
+    const bool me = LANE == (q);                                             \
+    snap = me ? rsv : snap;                                                  \
+    fv = me ? fn : fv;                                                       \
+    rsv = fmaf(dl, Acol[q], rsv);                                            \
+  }
+  constexpr auto groups = std::make_integer_sequence<int, DX_PGS_AR / 8>{};
+  constexpr auto eight = std::make_integer_sequence<int, 8>{};
+  int it = 0;
+  for (; it < c.iterations;) {
+    stage_count(c, CNT_NEWTON_IT);
+    float il = 0.f;  // this lane's rows' dual-cost decrease
+    float impr = 0.f;
+    static_for([&](auto Bc) {
+      constexpr int B = Bc.value;
+      if (B < nb) {
+        // (profiling: the residuals count as newton_grad, the row updates as
+        // newton_linesearch, the formation above as newton_hessian)
+        if (nb > 1 || ntail > 0 || it == 0) {  // (one block alone keeps its residuals current)
+          wsum();
+          res[B] = dotw(P[B]) + bb[B] + rk[B] * fb[B];
+          stage_mark(c, ST_NEWTON_GRAD);
+        }
+        const float f0 = fb[B];
+        static_for([&](auto Gc) {
+          if (DX_PGS_AR * B + 8 * Gc.value < nefc)
+            static_for([&](auto Q) { DX_PGS_ROWL(8 * Gc.value + Q.value, A[B], res[B], fb[B], idg[B], lo[B], hi[B], rs[B]) },
+                       eight);
+        }, groups);
+        const float df = fb[B] - f0;
+        il -= df * fmaf(hdg[B], df, rs[B]);
+        stage_mark(c, ST_NEWTON_LS);
+      }
+    }, blocks);
+    if (ntail) {
+      wsum();
+      stage_mark(c, ST_NEWTON_GRAD);
+      for (int t = 0; t < ntail; t++) {
+        const int r = NB * DX_PGS_AR + t;
+        const float p = pgs_p_lane(c, r, G);
+        const float fo = f[r];
+        const float rr = wave_sum(p * wl) + (jar[r] - aref[r]) + fo / D[r];
+        const float ar = rl(ardt, t);
+        float l, h;
+        box(r, l, h);
+        const float fn = __builtin_amdgcn_fmed3f(fo - rr / ar, l, h);
+        const float dl = fn - fo;
+        if (dl != 0.f) {
+          wl = fmaf(dl, p, wl);
+          wt = fmaf(dl, p, wt);
+          if (LANE == 0) f[r] = fn;
+          impr -= 0.5f * ar * dl * dl + dl * rr;
+        }
+        SYNC();
+      }
+      stage_mark(c, ST_NEWTON_LS);
+    }
+    impr += wave_sum(il);
+    it++;
+    if (scale * impr < tol) break;
+  }
+#undef DX_PGS_ROWL
+  // qacc = qacc_smooth + G w (lane d: sum over e <= d of G[d][e] w[e])
+  wsum();
+  {
+    const int d = min(LANE, nv - 1);
+    float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 30; e += 2) {
+      s0 = fmaf(e <= d ? G[ti(d) + min(e, d)] : 0.f, rl(wl, min(e, 29)), s0);
+      s1 = fmaf(e + 1 <= d ? G[ti(d) + min(e + 1, d)] : 0.f, rl(wl, min(e + 1, 29)), s1);
+    }
+    SYNC();
+    if (LANE < nv) qacc[LANE] = a0[LANE] + (s0 + s1);
+  }
+  // the forces, as residuals whose primal force is f_r
+  static_for([&](auto Bc) {
+    const int k = DX_PGS_AR * Bc.value + LANE;
+    if (k < nefc) {
+      f[k] = fb[Bc.value];
+      jar[k] = -fb[Bc.value] / D[k];
+    }
+  }, blocks);
+  for (int r = NB * DX_PGS_AR + LANE; r < nefc; r += DX_WAVE) jar[r] = -f[r] / D[r];
+  if (LANE == 0) c.I[I_NITER] = it;
+  SYNC();
 }
 // [3P] MuJoCo's PGS (mj_solPGS), <option solver="PGS">: projected Gauss-Seidel on the
 // dual, min_f 0.5 f'(A + R) f + f'b with A = J M^-1 J' and b = J qacc_smooth - aref;
@@ -2710,203 +2932,10 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
     for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
   SYNC();
   if (inv) {
-    if (nefc <= 2 * DX_PGS_AR + DX_WAVE) {
-      // MuJoCo's own form (mj_solPGS on efc_AR): AR = J M^-1 J' + R, lane k holding
-      // column k (a[r] = AR[r][k] = AR[k][r]) and the residual res_k = (AR f)_k + b_k
-      // (b = J qacc_smooth - aref).  A row update is then a readlane of res_r, a few
-      // uniform scalars and, for a changed force, one FMA of every lane's residual with
-      // its AR entry -- no J row, no M^-1 J_r' and no reduction on the chain from one
-      // row to the next.  The loop over rows is unrolled (AR's column index is a
-      // register name), with a uniform exit past nefc.  Past 64 rows the rows form two
-      // blocks (lane k: rows k and 64 + k), each holding its own diagonal block of AR
-      // (a[], b[]); the coupling between the blocks enters when a block's sweep starts,
-      // through its residuals recomputed from the current forces matrix-free (J (qacc_smooth
-      // + M^-1 J'f) - aref + R f) -- exactly the Gauss-Seidel sweep in row order.  Rows
-      // past 128 (the tail, at most 64: contact rows of the envs with 26 or more contacts,
-      // which set the launch) go one at a time after block 1, matrix-free on qacc (lane =
-      // dof) as the path below, with their AR diagonal formed once per solve (lane t: tail
-      // row t).
-      const bool two = nefc > DX_PGS_AR;
-      const int ntail = max(0, nefc - 2 * DX_PGS_AR);
-      float a[DX_PGS_AR], b[DX_PGS_AR];
-      constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
-      static_for([&](auto K) { a[K.value] = 0.f; }, rows);
-      const int k1 = DX_PGS_AR + LANE;  // this lane's row of the second block
-      jac_vec(c, a0, jar);  // J qacc_smooth (jar's warm-start residuals were consumed above)
-      const float bk = LANE < nefc ? jar[LANE] - aref[LANE] : 0.f;
-      float fk = LANE < nefc ? f[LANE] : 0.f, fk1 = k1 < nefc ? f[k1] : 0.f;
-      const float rk = LANE < nefc ? 1.0f / D[LANE] : 0.f, rk1 = k1 < nefc ? 1.0f / D[k1] : 0.f;
-      float dg = 1.f, dg1 = 1.f;
-      // AR's first diagonal block: lane k forms y_k = M^-1 J_k' for its row k (from the
-      // row's compact form and the sweep's M^-1 in LDS), then each column r is AR[k][r] =
-      // y_k . J_r (J_r lane-distributed by pgs_jrow, 30 readlanes), + R_r on the diagonal.
-      // The second block (two) goes column by column through LDS (J_r, M^-1 J_r' by the
-      // sweep's inverse, J (M^-1 J_r')): its registers are then the only ones live beside
-      // the first block's.
-      {
-        float y[30];
-        pgs_minv_row(c, LANE < nefc ? LANE : -1, T, y);
-        const int r1 = min(nefc, DX_PGS_AR);
-        for (int r = 0; r < r1; r++) {
-          const float jr = pgs_jrow(c, r);
-          float v0 = 0.f, v1 = 0.f;
-#pragma unroll
-          for (int d = 0; d < 30; d += 2) {
-            v0 = fmaf(y[d], rl(jr, d), v0);
-            v1 = fmaf(y[d + 1], rl(jr, d + 1), v1);
-          }
-          float v = LANE < nefc ? v0 + v1 : 0.f;
-          if (LANE == r) { v += rk; dg = v; }
-          static_for([&](auto K) { a[K.value] = K.value == r ? v : a[K.value]; }, rows);
-        }
-      }
-      if (two) {
-        static_for([&](auto K) { b[K.value] = 0.f; }, rows);
-        for (int r = DX_PGS_AR; r < min(nefc, 2 * DX_PGS_AR); r++) {
-          pgs_row(c, r, Jd);
-          minv(Jd, u);
-          jac_vec(c, u, jar);
-          float v = k1 < nefc ? jar[k1] : 0.f;
-          if (k1 == r) { v += rk1; dg1 = v; }
-          static_for([&](auto K) { b[K.value] = K.value + DX_PGS_AR == r ? v : b[K.value]; }, rows);
-        }
-      }
-      float ardt = 1.f;  // lane t: AR[128 + t][128 + t]
-      for (int t = 0; t < ntail; t++) {
-        const int r = 2 * DX_PGS_AR + t;
-        pgs_row(c, r, Jd);
-        minv(Jd, u);
-        const float sr = wave_sum(LANE < nv ? Jd[LANE] * u[LANE] : 0.f) + 1.0f / D[r];
-        ardt = LANE == t ? sr : ardt;
-      }
-      const float idg = 1.0f / dg, idg1 = 1.0f / dg1;
-      // each row's projection as a box [lo, hi]: friction loss [-floss, floss], limits and
-      // pyramid edges [0, inf)
-      // (a padding row past nefc has the box [0, 0], force 0 and residual 0: its update
-      // changes nothing, so the rows go in groups of 8 with one test per group)
-      auto box = [&](int k, float& lo, float& hi) {
-        const int kc = min(k, nefc - 1);
-        const bool fr = (meta[kc] & 15) == DXR_FRIC;
-        hi = k >= nefc ? 0.f : fr ? fl[kc] : __builtin_inff();
-        lo = fr && k < nefc ? -hi : 0.f;
-      };
-      float lok, hik, lok1, hik1;
-      box(LANE, lok, hik);
-      box(k1, lok1, hik1);
-      float res = bk, res1 = 0.f;
-      // both blocks' residuals from the current forces, matrix-free
-      // (jar = -f / R is each row's force as a residual, what jac_t_force reads; the tail
-      // rows' forces live in f[] and their jar is restored here after each jac_vec)
-      auto forces_out = [&]() {
-        if (LANE < nefc) { f[LANE] = fk; jar[LANE] = -fk / D[LANE]; }
-        if (k1 < nefc) { f[k1] = fk1; jar[k1] = -fk1 / D[k1]; }
-        if (LANE < ntail) { const int r = 2 * DX_PGS_AR + LANE; jar[r] = -f[r] / D[r]; }
-        SYNC();
-      };
-      auto resid = [&]() {
-        forces_out();
-        jac_t_force(c, g);
-        minv(g, u);
-        for (int i = LANE; i < nv; i += DX_WAVE) u[i] += a0[i];
-        SYNC();
-        jac_vec(c, u, jar);
-        res = LANE < nefc ? jar[LANE] - aref[LANE] + fk * rk : 0.f;
-        res1 = k1 < nefc ? jar[k1] - aref[k1] + fk1 * rk1 : 0.f;
-      };
-      if (!two) static_for([&](auto K) { res = K.value < nefc ? fmaf(a[K.value], rl(fk, K.value), res) : res; }, rows);
-      stage_mark(c, ST_NEWTON_HESS);
-      // one row update (q static: a register name of a[] / b[])
-// (branch-free: an unchanged force gives dl = 0, and fma(0, x, res) = res, so the
-// residuals, the force and the improvement are those of the branch that skips it)
-#define DX_PGS_ROW(q, col, rs, fv, dgv, idgv, lov, hiv)                                                       \
-  {                                                                                                        \
-    const float rr = rl(rs, q), fo = rl(fv, q), ir = rl(idgv, q);                                          \
-    const float ar = rl(dgv, q), lo = rl(lov, q), hi = rl(hiv, q);                                         \
-    const float fn = __builtin_amdgcn_fmed3f(fo - rr * ir, lo, hi); /* min(hi, max(lo, .)), lo <= hi */   \
-    const float dl = fn - fo;                                                                              \
-    rs = fmaf(dl, col[q], rs);                                                                             \
-    fv = LANE == (q) ? fn : fv;                                                                            \
-    impr -= 0.5f * ar * dl * dl + dl * rr;                                                                 \
-  }
-      constexpr auto groups = std::make_integer_sequence<int, DX_PGS_AR / 8>{};
-      constexpr auto eight = std::make_integer_sequence<int, 8>{};
-      float impr = 0.f;
-      float qa = 0.f;  // qacc (lane = dof) after the tail rows
-      int it = 0;
-      for (; it < c.iterations;) {
-        stage_count(c, CNT_NEWTON_IT);
-        impr = 0.f;
-        // (profiling: the residual passes count as newton_grad, the row updates as
-        // newton_linesearch, the formation above as newton_hessian)
-        if (two) {
-          if (it > 0 && ntail) {
-            // block 0 after the last sweep's tail: qa, carried through the tail rows, is
-            // already qacc_smooth + M^-1 J'f of the current forces
-            if (LANE < nv) u[LANE] = qa;
-            SYNC();
-            jac_vec(c, u, jar);
-            res = LANE < nefc ? jar[LANE] - aref[LANE] + fk * rk : 0.f;
-          } else {
-            resid();  // block 0 after the last sweep's block 1
-          }
-          stage_mark(c, ST_NEWTON_GRAD);
-        }
-        static_for([&](auto G) {
-          if (8 * G.value < nefc)
-            static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, a, res, fk, dg, idg, lok, hik) }, eight);
-        }, groups);
-        stage_mark(c, ST_NEWTON_LS);
-        if (two) {
-          resid();  // block 1 after this sweep's block 0
-          stage_mark(c, ST_NEWTON_GRAD);
-          static_for([&](auto G) {
-            if (DX_PGS_AR + 8 * G.value < nefc)
-              static_for([&](auto Q) { DX_PGS_ROW(8 * G.value + Q.value, b, res1, fk1, dg1, idg1, lok1, hik1) }, eight);
-          }, groups);
-          stage_mark(c, ST_NEWTON_LS);
-        }
-#undef DX_PGS_ROW
-        if (ntail) {
-          // the tail after block 1: qacc = qacc_smooth + M^-1 J'f from the current forces,
-          // then row by row res_r = J_r qacc - aref_r + R_r f_r, qacc += dl M^-1 J_r'
-          forces_out();
-          jac_t_force(c, g);
-          minv(g, u);
-          qa = LANE < nv ? u[LANE] + a0[LANE] : 0.f;
-          SYNC();
-          stage_mark(c, ST_NEWTON_GRAD);
-          for (int t = 0; t < ntail; t++) {
-            const int r = 2 * DX_PGS_AR + t;
-            const float jr = pgs_jrow(c, r);
-            if (LANE < nv) Jd[LANE] = jr;
-            const float fo = f[r], rr = wave_sum(jr * qa) - aref[r] + fo / D[r];
-            const float ar = rl(ardt, t);
-            float lo, hi;
-            box(r, lo, hi);
-            const float fn = __builtin_amdgcn_fmed3f(fo - rr / ar, lo, hi);
-            const float dl = fn - fo;
-            if (dl != 0.f) {
-              SYNC();
-              mat_vec(T, Jd, u, nv);
-              SYNC();
-              if (LANE < nv) qa = fmaf(dl, u[LANE], qa);
-              if (LANE == 0) f[r] = fn;
-              impr -= 0.5f * ar * dl * dl + dl * rr;
-            }
-            SYNC();
-          }
-          stage_mark(c, ST_NEWTON_LS);
-        }
-        it++;
-        if (scale * impr < tol) break;
-      }
-      // the forces, as residuals whose primal force is f_r; qacc = qacc_smooth + M^-1 J'f
-      forces_out();
-      jac_t_force(c, g);
-      minv(g, u);
-      for (int i = LANE; i < nv; i += DX_WAVE) qacc[i] = a0[i] + u[i];
-      if (LANE == 0) c.I[I_NITER] = it;
-      SYNC();
+    // (the generic kernel and the contact tiers, within two waves' VGPRs: one block)
+    constexpr int NB = Ctx::is_spec ? DX_PGS_NB : 1;
+    if (nefc <= NB * DX_PGS_AR + DX_WAVE) {
+      solve_pgs_ar<NB>(c, scale, tol, T);
       return;
     }
     // nv <= 30: the sweep's M^-1 row of dof d in lane d's registers, qacc[d] in lane d,
@@ -3977,6 +4006,9 @@ __device__ __forceinline__ void fused_post(const Ctx& c, const DevBatch& B, int 
 template <class Ctx>
 __device__ __forceinline__ float fused_reach_prep(Ctx& c, const DevBatch& B, int env, float time) {
   const TaskState& S = *(const TaskState*)(const DXG TaskState*)B.ts;
+  // (a reach scene's specialization; the guard keeps another task on a layout-equal
+  // scene from reading reach state it does not keep)
+  if (((const DXG TaskParams*)B.tp)->kind != DX_KIND_REACH) return time;
   int need = 0;
   if (LANE == 0) need = S.need[env];
   if (!__builtin_amdgcn_readfirstlane(need)) return time;

@@ -95,7 +95,7 @@ __device__ __forceinline__ int task_pre(const TaskParams& P, const TaskState& S,
     }
     B.time[env] = 0;
     if (B.nstep) B.nstep[env] = 0;
-    if (P.kind == DX_KIND_REORIENT) {
+    if (P.kind != DX_KIND_REACH) {
       // reorient.py:182-188 in the reference's draw order: the goal first
       // (GoalTask.initialize_episode, task.py:137-152 -> PropOrientation.next_goal,
       // prop_orientation.py:34-38, whose sampler gets the RandomState positionally
@@ -104,7 +104,12 @@ __device__ __forceinline__ int task_pre(const TaskParams& P, const TaskState& S,
       // uniform quaternion (3 draws).  A spawn never touches the hand (the box is above
       // it, tests/test_host_logic.py), so PropPlacer's first attempt is always kept.
       float g[4];
-      dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);
+      if (P.kind == DX_KIND_HANDOVER) {  // the cube spawns over the first hand, handed to the second
+        for (int k = 0; k < 3; k++) g[k] = P.hand_target[1][k];
+        g[3] = 1.f;
+      } else {
+        dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);
+      }
       for (int k = 0; k < 4; k++) W::st(S.goal, (size_t)P.goal_dim * env + k, g[k]);
       if (P.prop_qadr >= 0) {
         uint32_t w[12];  // position (3 doubles) then the quaternion (3 doubles), one fetch
@@ -137,9 +142,15 @@ __device__ __forceinline__ int task_pre(const TaskParams& P, const TaskState& S,
   W::st(S.skip, env, 0);
   // GoalTask.before_step (task.py:154-165)
   if (S.counter[env] > P.steps_before_change) {
-    if (P.kind == DX_KIND_REORIENT) {
+    if (P.kind != DX_KIND_REACH) {
       float g[4];
-      dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);  // numpy's global stream
+      if (P.kind == DX_KIND_HANDOVER) {  // the goal switches to the other hand: the cube goes back
+        const int h = S.goal[(size_t)P.goal_dim * env + 3] > 0.5f ? 0 : 1;
+        for (int k = 0; k < 3; k++) g[k] = P.hand_target[h][k];
+        g[3] = (float)h;
+      } else {
+        dx_mt_uniform_quat(S.mt_goal, P.nenv, env, g);  // numpy's global stream
+      }
       for (int k = 0; k < 4; k++) W::st(S.goal, (size_t)P.goal_dim * env + k, g[k]);
       W::st(S.counter, env, 0);
       W::st(S.exceeded, env, 0);
@@ -169,7 +180,7 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
     for (int k = 0; k < 4; k++) cur[k] = q[P.prop_qadr + 3 + k];
   // goal distance: orientation (prop_orientation.py:40-50) or per-fingertip
   // Cartesian distances (fingertip_position.py:127-137)
-  float dist = 0, dtip[8];
+  float dist = 0, dtip[DX_MAX_TIPS];
   bool all_close = true;
   float rsum = 0;
   if (reach) {
@@ -182,6 +193,11 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
       // reach.py:196-210: dense -tanh^2(d, 0.1), sparse -1, 0 within the threshold
       rsum += close ? 0.f : (P.dense ? -tanh_squared(dtip[t], 0.1f) : -1.f);
     }
+  } else if (P.kind == DX_KIND_HANDOVER) {
+    // the cube's distance to the receiving hand's target point
+    const float d0 = q[P.prop_qadr] - g[0], d1 = q[P.prop_qadr + 1] - g[1], d2 = q[P.prop_qadr + 2] - g[2];
+    dist = sqrtf(d0 * d0 + d1 * d1 + d2 * d2);
+    all_close = dist <= P.threshold;
   } else {
     dist = quat_distance(g, cur);
     all_close = dist <= P.threshold;
@@ -233,7 +249,8 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
       if (reach) {
         r = rsum / (float)P.ntips;
       } else {
-        // reorient.py:238-284: 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2
+        // reorient.py:238-284: 1/(d+eps) + 800*[d<=thr] - 0.1*|ctrl|^2 (handover: the same
+        // shape on the cube's distance to the target point, with the task's weights)
         float cn = 0;
         for (int i = 0; i < P.nu; i++) {
           float c = B.ctrl[(size_t)env * P.nu + i];
@@ -250,7 +267,8 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
   // observation (STATE_ONLY), flat layout:
   // [sin/cos(qpos_hand) 2*hand_nq | qvel_hand | tip pos 3*ntips | tip linvel 3*ntips |
   //  reorient: prop pos 3 | prop quat 4 | prop linvel 3 | prop angvel 3 | target quat 4 |
-  //  goal (4 quaternion, or 3*ntips fingertip positions for reach)]
+  //  goal (4 quaternion, or 3*ntips fingertip positions for reach; handover: the prop block
+  //  without the target quaternion, goal = target point + receiving hand)]
   float* o = S.obs + (size_t)env * P.obs_dim;
   const float n = sqrtf(cur[0] * cur[0] + cur[1] * cur[1] + cur[2] * cur[2] + cur[3] * cur[3]);
   for (int k = lane; k < P.obs_dim; k += 64) {
@@ -284,6 +302,8 @@ __device__ __forceinline__ void task_post(const TaskParams& P, const TaskState& 
           const float R1 = r == 0 ? 2 * (x * y - w0 * z) : (r == 1 ? 1 - 2 * (x * x + z * z) : 2 * (y * z + w0 * x));
           const float R2 = r == 0 ? 2 * (x * z + w0 * y) : (r == 1 ? 2 * (y * z - w0 * x) : 1 - 2 * (x * x + y * y));
           val = R0 * wl[0] + R1 * wl[1] + R2 * wl[2];
+        } else if (P.kind == DX_KIND_HANDOVER) {
+          val = g[e - 13];  // goal_state (no hint prop)
         } else if (e < 17) {
           val = g[e - 13];  // target_prop/orientation (hint cube = goal)
         } else {

@@ -13,6 +13,8 @@ Suite (names as in the reference):
   reach.state_sparse     manipulation/tasks/reach.py:262-269
   reach_shadow.state_dense  BASELINE.json config 2: reach with the Shadow hand,
                          contact-free smooth dynamics (not a reference suite entry)
+  bimanual.state_dense   BASELINE.json config 5: two Shadow hands hand the cube over
+                         (Handover; not a reference suite entry)
 """
 
 from __future__ import annotations
@@ -138,6 +140,116 @@ class ReOrient:
 
     def observation_layout(self):
         return observation_layout(self.hand_nq, self.hand_nv, self.ntips, True, self.hand_name)
+
+
+@dataclasses.dataclass(frozen=True)
+class HandoverConfig:
+    """BASELINE.json config 5 as a task (synthetic: the reference has no bimanual task; its
+    two-hand pattern is Juggle's hands and effectors, juggle.py:147-177 with
+    arenas/arena.py:58-105).  Two Shadow hands palm-up side by side (mjcf/scenes.py
+    bimanual_handover), the reorient cube spawned over the first (left) hand and handed to
+    the target point above the other palm; GoalTask bookkeeping, reward in the shape of
+    reorient.py:238-284 on the cube-to-target distance, fall termination of
+    reorient.py:229-235.  Timesteps as reorient's."""
+
+    physics_timestep: float = 0.005
+    control_timestep: float = 0.025
+    distance_eps: float = 0.05  # 1 / (d + eps), d in metres
+    success_threshold: float = 0.02  # the cube within 2 cm of the receiving palm's target
+    distance_weight: float = 1.0
+    success_bonus_weight: float = 800.0  # reorient.py:55
+    action_smoothing_weight: float = -0.1  # reorient.py:56
+    successes_needed: int = 3  # handovers (there and back, and there again)
+    max_steps_single_solve: int = 300  # reorient.py:67
+    steps_before_moving_target: int = 5  # task.py's goal change: the cube goes back
+    fall_termination: bool = True
+    # the reorient spawn box (reorient.py:72-78) over the left hand (+0.12 m in x)
+    prop_bbox_lower: tuple = (0.095, -0.155, 0.16)
+    prop_bbox_upper: tuple = (0.145, -0.105, 0.16)
+    # where the cube comes to rest on each palm from the spawn box's centre (the fp64
+    # oracle: 0.1308 m high, 0.13 m in front of the forearms), left then right
+    hand_targets: tuple = ((0.12, -0.13, 0.131), (-0.12, -0.13, 0.131))
+
+    @property
+    def n_sub_steps(self) -> int:
+        return int(round(self.control_timestep / self.physics_timestep))
+
+    @property
+    def max_time_per_goal(self) -> float:
+        return self.max_steps_single_solve * self.control_timestep
+
+
+class Handover(ReOrient):
+    """The two-hand cube handover behind the Task / Effector / Environment surface
+    (HandoverConfig).  Both hands' joints, velocities and fingertips are the hand block of
+    the observation (left then right, as the scene orders them), then the cube's pose and
+    velocities and the goal [target xyz, receiving hand]."""
+
+    domain = "bimanual"
+    kind = _lib.TASK_HANDOVER
+
+    def __init__(self, config: HandoverConfig = HandoverConfig(), asset: str = "bimanual_handover.npz"):
+        self.config = config
+        self.compiled = CompiledModel.load(os.path.join(ASSETS, asset))
+        cm = self.compiled
+        if abs(cm.timestep - config.physics_timestep) > 1e-12:
+            raise ValueError("asset timestep does not match the task's physics timestep")
+        names = cm.names
+        self.hand_names = ("shadow_hand_left", "shadow_hand_right")
+        self.hand_name = "bimanual"
+        self.hand_joint_ids = [i for i, n in enumerate(names["joint"]) if n.startswith("shadow_hand_")]
+        self.hand_nq = len(self.hand_joint_ids)
+        self.hand_nv = self.hand_nq
+        prop_j = names["joint"].index("prop/")
+        self.prop_qadr = int(cm.jnt_qposadr[prop_j])
+        self.prop_dadr = int(cm.jnt_dofadr[prop_j])
+        if self.prop_qadr != self.hand_nq:  # the hands' joints first, then the cube's
+            raise ValueError("bimanual scene: hand joints must precede the prop's")
+        self.prop_body = names["body"].index("prop/")
+        self.ground_geom = names["geom"].index("ground")
+        tips = [f"{h}/{t}_site" for h in self.hand_names for t in ("fftip", "mftip", "rftip", "lftip", "thtip")]
+        self.tip_site0 = names["site"].index(tips[0])
+        assert [names["site"].index(s) for s in tips] == list(range(self.tip_site0, self.tip_site0 + 10))
+        self.ntips = 10
+        self.actuator_ids = list(range(cm.nu))
+        self.hand_effector = effectors_lib.HandEffector(self.actuator_ids, self.hand_name)
+        self.gravity_compensation = physics_lib.gravity_compensation(cm, "shadow_hand_")
+
+    def params(self) -> np.ndarray:
+        c = self.config
+        p = np.zeros(44, dtype=np.float32)
+        p[0] = c.n_sub_steps
+        p[1], p[2] = self.hand_nq, self.hand_nv
+        p[3], p[4] = self.prop_qadr, self.prop_dadr
+        p[5], p[6] = self.tip_site0, self.ntips
+        p[7], p[8], p[9] = c.successes_needed, c.steps_before_moving_target, int(c.fall_termination)
+        p[10], p[11] = c.success_threshold, c.distance_eps
+        p[12], p[13], p[14] = c.distance_weight, c.success_bonus_weight, c.action_smoothing_weight
+        p[15] = c.max_time_per_goal
+        p[16:19] = c.prop_bbox_lower
+        p[19:22] = c.prop_bbox_upper
+        p[22], p[23] = self.ground_geom, self.prop_body
+        box = np.array(c.prop_bbox_lower + c.prop_bbox_upper, dtype=np.float64)
+        p[26:38] = box.view(np.float32)
+        p[38:44] = np.asarray(c.hand_targets, dtype=np.float32).ravel()
+        return p
+
+    def observation_layout(self):
+        """Per-hand keys: the scene orders the left hand's joints, dofs and fingertips
+        before the right's, so each hand's block is a contiguous slice."""
+        out = collections.OrderedDict()
+        nh, k = self.hand_nq // 2, 0
+        blocks = (("joint_positions_sin_cos", 2 * nh), ("joint_velocities", nh), ("fingertip_positions", 15),
+                  ("fingertip_linear_velocities", 15))
+        for name, n in blocks:
+            for h in self.hand_names:
+                out[f"{h}/{name}"] = slice(k, k + n)
+                k += n
+        for name, n in (("prop/position", 3), ("prop/orientation", 4), ("prop/linear_velocity", 3),
+                        ("prop/angular_velocity", 3), ("goal_state", 4)):
+            out[name] = slice(k, k + n)
+            k += n
+        return out
 
 
 @dataclasses.dataclass(frozen=True)
@@ -274,12 +386,18 @@ class GoalEnvironment:
         self._action_spec = task.hand_effector.action_spec(self.physics)
         self._host_action = np.zeros((self.num_envs, self.model.nu), dtype=np.float32)
         self._dev_action = self._out(-1)
+        self._pins = []  # page-locked host buffers of step() (freed by close)
+        self._pin_act = self._pin_out = None
         if np.isfinite(self.time_limit):
             _lib.check(L.dx_env_set_time_limit(self.ptr, self.time_limit))
         # max_time_per_goal in fp64 (the params carry it as a float)
         _lib.check(L.dx_env_set_goal_time_limit(self.ptr, float(task.config.max_time_per_goal)))
 
     def close(self):
+        for p in getattr(self, "_pins", ()):
+            _hip_runtime().hipHostFree(ctypes.c_void_p(p))
+        self._pins = []
+        self._pin_act = self._pin_out = None
         if getattr(self, "physics", None) is not None:
             self.physics.ptr = None
         if getattr(self, "ptr", None) and _lib._lib is not None:
@@ -318,15 +436,30 @@ class GoalEnvironment:
         if device_action:
             _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(int(action))))
             return None
-        a = np.ascontiguousarray(action, dtype=np.float32).reshape(self.num_envs, -1)
+        a = np.asarray(action, dtype=np.float32).reshape(self.num_envs, -1)
         if a.shape[1] != self.model.nu:
             raise ValueError(f"action must be [{self.num_envs}, {self.model.nu}], got {a.shape}")
-        # host actions go into the library's device action buffer (the pre-kernel
-        # reads it and writes ctrl: mujoco_actuation.py:33)
-        self.physics.sync()
-        _copy_h2d(self._dev_action, a)
-        _lib.check(L.dx_env_step(self.ptr, ctypes.c_void_p(self._dev_action)))
-        return self.timestep()
+        # the reference's call shape (environment.py:25-34): host actions in, the host
+        # TimeStep out, through page-locked buffers -- dx_env_step_host uploads them into
+        # the library's action buffer (the step kernel writes ctrl from it:
+        # mujoco_actuation.py:33), steps, packs [obs | reward | discount | step_type] and
+        # downloads it, all on the env's stream with one synchronisation
+        if self._pin_act is None:
+            self._pin_act = _pinned((self.num_envs, self.model.nu), np.float32, self._pins)
+            self._pin_out = _pinned((self.num_envs, self.obs_dim + 3), np.float32, self._pins)
+        np.copyto(self._pin_act, a)
+        _lib.check(L.dx_env_step_host(self.ptr, self._pin_act.ctypes.data, self._pin_out.ctypes.data))
+        return self._timestep_packed(self._pin_out)
+
+    def _timestep_packed(self, packed: np.ndarray) -> TimeStep:
+        """A TimeStep (copies) from the packed [obs | reward | discount | step_type] rows."""
+        d = self.obs_dim
+        observation = collections.OrderedDict(
+            (k, packed[:, s].astype(np.float64) if self.strip_singleton_obs_buffer_dim
+             else packed[:, None, s].astype(np.float64)) for k, s in self._layout.items()
+        )
+        return TimeStep(packed[:, d + 2].astype(np.int32), packed[:, d].astype(np.float64),
+                        packed[:, d + 1].astype(np.float64), observation)
 
     def step_random(self, step: int) -> None:
         """One control step under the random agent: the actions `sample_actions(step)`
@@ -444,7 +577,21 @@ def _hip_runtime():
         _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         _hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
         _hip.hipFree.argtypes = [ctypes.c_void_p]
+        _hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+        _hip.hipHostFree.argtypes = [ctypes.c_void_p]
     return _hip
+
+
+def _pinned(shape, dtype, owner: list) -> np.ndarray:
+    """A page-locked host array (hipHostMalloc); its address is appended to `owner`."""
+    nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+    p = ctypes.c_void_p()
+    rc = _hip_runtime().hipHostMalloc(ctypes.byref(p), nbytes, 0)
+    if rc != 0 or not p.value:
+        raise _lib.DxError(f"hipHostMalloc failed ({rc})")
+    owner.append(p.value)
+    buf = (ctypes.c_byte * nbytes).from_address(p.value)
+    return np.frombuffer(buf, dtype=dtype).reshape(shape)
 
 
 def _copy_d2h(out: np.ndarray, devptr: int) -> None:
@@ -466,6 +613,7 @@ SUITE = {
     ("reach", "state_dense"): lambda: Reach(ReachConfig(dense_reward=True), hand="adroit"),
     ("reach", "state_sparse"): lambda: Reach(ReachConfig(dense_reward=False), hand="adroit"),
     ("reach_shadow", "state_dense"): lambda: Reach(ReachConfig(dense_reward=True), hand="shadow"),
+    ("bimanual", "state_dense"): Handover,
 }
 ALL_TASKS = tuple(sorted(SUITE))
 ALL_NAMES = [".".join(t) for t in ALL_TASKS]

@@ -192,7 +192,7 @@ int dx_debug_get(dx_batch* b, const char* name, float* dst, size_t nfloats);
  * observation vector, for every env, with dm_env auto-reset (an env that returned
  * LAST is re-initialised by its next step and returns FIRST). */
 typedef struct dx_env dx_env;
-enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
+enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1, DX_TASK_HANDOVER = 2 };
 /* Reorient params (float[26], or float[38] with the fp64 bbox), reorient.py:40-78 / task.py:120-135:
  *  0 n_sub_steps  1 hand_nq  2 hand_nv  3 prop_qposadr  4 prop_dofadr
  *  5 first fingertip site  6 n fingertips  7 successes_needed
@@ -220,6 +220,17 @@ enum dx_task_kind { DX_TASK_REORIENT = 0, DX_TASK_REACH = 1 };
  *  numpy's cached polar gaussians, then the uniform joint angles); without them, from a
  *  counter-based stream. */
 #define DX_REACH_NPARAMS_HEAD 26
+/* Handover params (float[44]): a two-hand scene (BASELINE config 5; the reference has no
+ * bimanual task -- its pattern is Juggle's two hands and effectors, juggle.py:147-177,
+ * arenas/arena.py:58-105), the cube handed from palm to palm behind the GoalTask surface.
+ * 0-37 as reorient's, with hand_nq / hand_nv / fingertips counting both hands and the
+ * bbox the giving (first) hand's spawn box; then 38-40 / 41-43 the target points above
+ * the first / second hand's palm.  The goal is [target xyz, receiving hand]: at reset
+ * the second hand's target; after steps_before_changing_goal successes it switches to
+ * the other hand (the cube handed back).  Reward reorient.py:238-284's shape on the
+ * cube-to-target distance d: w_orientation / (d + eps) + w_success [d <= threshold] +
+ * w_action |ctrl|^2; the cube touching the ground ends the episode (discount 1). */
+#define DX_HANDOVER_NPARAMS 44
 enum dx_env_out { DX_OUT_OBS = 0, DX_OUT_REWARD = 1, DX_OUT_DISCOUNT = 2, DX_OUT_STEP_TYPE = 3,
                   DX_OUT_GOAL = 4, DX_OUT_SUCCESSES = 5, DX_OUT_GOAL_FAILURES = 6,
                   DX_OUT_GOAL_QPOS = 7 /* reach: [nenv][nq] f32, FingertipCartesianPosition.qpos
@@ -286,6 +297,12 @@ int dx_env_state_field(dx_env* e, int32_t i, const char** name, size_t* offset, 
 /* Packs [obs | reward | discount | step_type] per env into dst ([nenv][obs_dim+3]
  * f32, device memory) on the env's stream: the shard an RCCL all-gather collates. */
 int dx_env_pack_outputs(dx_env* e, float* dst_dev);
+/* The reference's call shape, GoalEnvironment.step(action) -> TimeStep
+ * (environment.py:25-34, task.py:63-73): action_host [nenv][nu] f32 and out_host
+ * [nenv][obs_dim+3] f32 ([obs | reward | discount | step_type as float]) are host memory
+ * (page-locked for asynchronous DMA); upload, control step, pack and download run on the
+ * env's stream, and the call returns once out_host holds the TimeStep. */
+int dx_env_step_host(dx_env* e, const float* action_host, float* out_host);
 
 /* Multi-GPU observation collation over RCCL -------- */
 /* The reference runs one environment per process and has no collective; here each
@@ -369,6 +386,9 @@ int dx_stage_read(dx_batch* b, uint64_t* out, int32_t n);
 int dx_debug_poison_lds(int32_t device);
 
 const char* dx_last_error(void);
+/* The hash of the sources the library was built from (dexterity_amd/build.py source_key):
+ * the Python layer refuses an in-tree library whose sources have changed since. */
+const char* dx_build_key(void);
 int dx_abi_version(void);
 
 #ifdef __cplusplus

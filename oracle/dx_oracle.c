@@ -257,7 +257,7 @@ void dxo_data_free(dxo_data* d) {
                   d->xfrc_applied, d->xpos, d->xquat, d->xmat, d->xipos, d->ximat, d->xanchor,
                   d->xaxis, d->geom_xpos, d->geom_xmat, d->site_xpos, d->site_xmat,
                   d->subtree_com, d->cinert, d->cdof, d->cvel, d->cdof_dot, d->crb, d->cacc,
-                  d->cfrc, d->ten_length, d->ten_J, d->actuator_length, d->actuator_moment,
+                  d->cfrc, d->cfrc_ext, d->cfrc_int, d->cacc_post, d->sensor_torque, d->ten_length, d->ten_J, d->actuator_length, d->actuator_moment,
                   d->actuator_force, d->M, d->L, d->H, d->qfrc_bias, d->qfrc_passive,
                   d->qfrc_actuator, d->qfrc_applied, d->qfrc_smooth, d->qfrc_constraint,
                   d->contact, d->efc_type, d->efc_id, d->efc_state, d->efc_J, d->efc_pos,

@@ -147,3 +147,40 @@ def reach_observation(d, hand: str, hand_nq: int, hand_nv: int, tip_sites, goal)
     out = {f"{hand}/{k}": v for k, v in _hand_observation(d, hand_nq, hand_nv, tip_sites).items()}
     out["goal_state"] = np.asarray(goal, dtype=np.float64)
     return out
+
+
+# --------------------------------------------------------------------------- #
+# the two-hand handover (BASELINE config 5 as a task; dexterity_amd.manipulation.Handover)
+# --------------------------------------------------------------------------- #
+def handover_reward(distance: float, ctrl, cfg) -> float:
+    """reorient.py:238-284's shape on the cube-to-target distance (metres), with the
+    Handover task's weights."""
+    return weighted_average([
+        (1.0 / (distance + cfg.distance_eps), cfg.distance_weight),
+        (1.0 if 0.0 <= distance <= cfg.success_threshold else 0.0, cfg.success_bonus_weight),
+        (np.linalg.norm(ctrl) ** 2, cfg.action_smoothing_weight),
+    ])
+
+
+def handover_observation(d, compiled, hands, hand_nq: int, tip_sites, prop_body: int,
+                         goal) -> "dict[str, np.ndarray]":
+    """The handover's observation: each hand's STATE_ONLY observables (its half of the
+    joints, dofs and fingertips), the cube's inertial-frame pose and velocities, and the
+    goal [target xyz, receiving hand]."""
+    nh = hand_nq // 2
+    both = _hand_observation(d, hand_nq, hand_nq, tip_sites)
+    out = {}
+    for name, per in (("joint_positions_sin_cos", 2 * nh), ("joint_velocities", nh), ("fingertip_positions", 15),
+                      ("fingertip_linear_velocities", 15)):
+        for i, h in enumerate(hands):
+            out[f"{h}/{name}"] = both[name][i * per:(i + 1) * per]
+    xq = d.xquat.reshape(-1, 4)[prop_body]
+    iq = np.asarray(compiled.body_iquat, dtype=np.float64).reshape(-1, 4)[prop_body]
+    quat = quat_mul(xq, iq)
+    vel = d.object_velocity("body", prop_body)
+    out["prop/position"] = d.xipos.reshape(-1, 3)[prop_body].copy()
+    out["prop/orientation"] = quat / np.linalg.norm(quat)
+    out["prop/linear_velocity"] = vel[:3]
+    out["prop/angular_velocity"] = vel[3:]
+    out["goal_state"] = np.asarray(goal, dtype=np.float64)
+    return out

@@ -774,3 +774,91 @@ def test_effector_set_control_round_trip(built):
     expect[:, [1, 3, 5]] = 0.5
     np.testing.assert_array_equal(ph.get(_lib.CTRL), expect)
     env.close()
+
+
+def test_handover_observation_and_reward(built, oracle_mod):
+    """BASELINE config 5 as a task (manipulation.load("bimanual", "state_dense"): two
+    Shadow hands hand the cube over, dexterity_amd.manipulation.Handover): every float of
+    the 221-float observation against task_ref.handover_observation on the env's own
+    post-step state (within 1e-5 of each field's scale), and every MID step's reward
+    against task_ref.handover_reward on the same step's cube position, goal and ctrl
+    (rel 2e-4), over 256 envs after 8 random-action control steps."""
+    from dexterity_amd import _lib, manipulation
+    from oracle import task_ref
+
+    env = manipulation.load("bimanual", "state_dense", seed=4, num_envs=256)
+    t = env.task
+    ts = env.reset()
+    assert env.obs_dim == 221 and env.goal_dim == 4
+    np.testing.assert_allclose(env.goals()[:, :3], np.tile(t.config.hand_targets[1], (256, 1)), atol=1e-7)
+    assert np.all(env.goals()[:, 3] == 1.0) and np.all(ts.step_type == 0)
+    # the cube spawns in the left hand's box (uniform position, uniform quaternion)
+    q = env.physics.qpos
+    lo, hi = np.array(t.config.prop_bbox_lower), np.array(t.config.prop_bbox_upper)
+    assert np.all(q[:, t.prop_qadr:t.prop_qadr + 3] >= lo - 1e-6) and np.all(q[:, t.prop_qadr:t.prop_qadr + 3] <= hi + 1e-6)
+    for i in range(8):
+        env.step(env.sample_actions(i), device_action=True)
+    sites = list(range(t.tip_site0, t.tip_site0 + t.ntips))
+    worst = _check_observation(
+        env, oracle_mod,
+        lambda d, g: task_ref.handover_observation(d, t.compiled, t.hand_names, t.hand_nq, sites, t.prop_body, g))
+    assert set(worst) >= {"prop/angular_velocity", "shadow_hand_right/fingertip_linear_velocities"}
+    ts = env.timestep()
+    qpos, ctrl, goals = env.physics.qpos, env.physics.get(_lib.CTRL), env.goals()
+    mid = ts.step_type == 1
+    assert mid.sum() > 128
+    for e in np.flatnonzero(mid):
+        dist = float(np.linalg.norm(qpos[e, t.prop_qadr:t.prop_qadr + 3].astype(np.float64) - goals[e, :3]))
+        ref = task_ref.handover_reward(dist, ctrl[e].astype(np.float64), t.config)
+        assert abs(ts.reward[e] - ref) <= 2e-4 * max(1.0, abs(ref)), (e, ts.reward[e], ref)
+    env.close()
+
+
+def test_handover_goal_switches_hands(built):
+    """GoalTask.before_step (task.py:154-165) on the handover: with every step a success
+    (threshold above any distance), after steps_before_changing_goal successes the goal
+    moves to the other hand's target and back, registered once per goal -- step by step
+    against a host restatement; the host action path (dx_env_step_host) steps the env."""
+    from dexterity_amd import manipulation
+
+    cfg = manipulation.HandoverConfig(success_threshold=10.0, successes_needed=1000, fall_termination=False)
+    env = manipulation.GoalEnvironment(manipulation.Handover(cfg), num_envs=32, seed=5)
+    env.reset()
+    targets = np.array(cfg.hand_targets)
+    counter, successes, registered, hand = 0, 0, False, 1
+    for k in range(20):
+        ts = env.step(np.zeros((32, env.model.nu), dtype=np.float32))
+        if counter > cfg.steps_before_moving_target:
+            counter, registered, hand = 0, False, 1 - hand
+        counter += 1
+        if not registered:
+            successes, registered = successes + 1, True
+        g = env.goals()
+        assert np.all(env.successes() == successes), (k, successes)
+        np.testing.assert_allclose(g[:, :3], np.tile(targets[hand], (32, 1)), atol=1e-7)
+        assert np.all(g[:, 3] == hand) and np.all(ts.step_type == 1)
+        np.testing.assert_array_equal(ts.observation["goal_state"], g.astype(np.float64))
+    assert successes >= 3
+    env.close()
+
+
+def test_handover_fall_terminates(built):
+    """The handover's fall rule (reorient.py:229-235 on the two-hand scene): a cube-ground
+    contact ends the episode (LAST) with discount 1.0 and the next step returns FIRST; the
+    random agent drops the cube from the left palm within 60 control steps in most envs."""
+    from dexterity_amd import manipulation
+
+    env = manipulation.load("bimanual", "state_dense", seed=11, num_envs=256)
+    env.reset()
+    rec = _run(env, 60)
+    falls = 0
+    for k in range(1, len(rec)):
+        r, prev = rec[k], rec[k - 1]
+        mid = prev["st"] != 2
+        fell = mid & (r["watch"] == 1)
+        assert np.all(r["st"][fell] == 2)
+        assert np.all(r["disc"][fell & (r["succ"] < 3)] == 1.0)
+        assert np.all(r["st"][prev["st"] == 2] == 0)
+        falls += int(fell.sum())
+    assert falls >= 20
+    env.close()

@@ -4,8 +4,8 @@
 set -e
 mkdir -p gpurun_out
 for i in 1 2; do
-  timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 300 > gpurun_out/ab_base_$i.log 2>&1
-  env "$@" timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 300 > gpurun_out/ab_var_$i.log 2>&1
+  timeout -k 10 120 python -u bench.py --no-cpu-baseline --host-api-steps 0 --steps 300 > gpurun_out/ab_base_$i.log 2>&1
+  env "$@" timeout -k 10 120 python -u bench.py --no-cpu-baseline --host-api-steps 0 --steps 300 > gpurun_out/ab_var_$i.log 2>&1
 done
 env "$@" timeout -k 10 300 python3 tools/stage_profile.py 4096 10 > gpurun_out/ab_var_stages.log 2>&1
 for f in gpurun_out/ab_base_*.log gpurun_out/ab_var_*.log; do

@@ -7,6 +7,6 @@ for i in 1 2; do
   for lib in - "$@"; do
     tag=$(basename "$lib" .so); [ "$tag" = libdx ] && tag=$(basename "$(dirname "$lib")")
     if [ "$lib" = "-" ]; then tag=default; unset DX_LIB; else export DX_LIB=$lib; fi
-    timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 300 > gpurun_out/ab_${tag}_$i.log 2>&1
+    timeout -k 10 120 python -u bench.py --no-cpu-baseline --host-api-steps 0 --steps 300 > gpurun_out/ab_${tag}_$i.log 2>&1
   done
 done

@@ -59,9 +59,10 @@ def env_config(name, domain, task, nenv, steps=50, warmup=10, solver=None):
 
 
 def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
-    import torch
-
+    """Config 5 as raw physics (no task): random ctrl held for 5 substeps, uploaded once
+    into a hipMalloc'd device buffer (libdx's HIP runtime, no PyTorch)."""
     from dexterity_amd import _lib, physics
+    from dexterity_amd.manipulation import _copy_h2d, _hip_runtime
     from dexterity_amd.mjcf.compiler import CompiledModel
 
     L = _lib.load()
@@ -73,12 +74,14 @@ def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
     q0[:, 48:51] += np.random.RandomState(0).uniform(-0.02, 0.02, size=(nenv, 3)) * [1, 1, 0]
     phys.set(_lib.QPOS, q0)
     lo, hi = cm.actuator_ctrlrange.T
-    acts = torch.tensor(np.random.RandomState(1).uniform(lo, hi, size=(warmup + steps, nenv, cm.nu)),
-                        dtype=torch.float32, device="cuda:0")
-    torch.cuda.synchronize()
+    acts = np.random.RandomState(1).uniform(lo, hi, size=(warmup + steps, nenv, cm.nu)).astype(np.float32)
+    dev = ctypes.c_void_p()
+    assert _hip_runtime().hipMalloc(ctypes.byref(dev), acts.nbytes) == 0
+    _copy_h2d(dev.value, acts)
+    row = nenv * cm.nu * 4
 
     def one(i):
-        phys.set_device(_lib.CTRL, acts[i].data_ptr(), 0, nenv)
+        phys.set_device(_lib.CTRL, dev.value + i * row, 0, nenv)
         phys.step(nsub)
 
     for i in range(warmup):
@@ -95,16 +98,15 @@ def bimanual(nenv=4096, steps=30, warmup=5, nsub=5):
     ncon = phys.get(_lib.NCON)[:, 0]
     ok = bool(np.isfinite(phys.qpos).all())
     phys.close()
-    return {"config": "5 bimanual handover physics (nv 54)", "envs": nenv,
+    _hip_runtime().hipFree(dev)
+    return {"config": "5p bimanual handover physics only (nv 54)", "envs": nenv,
             "env_steps_per_s": round(nenv * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 4),
             "step_kernel_ms_avg": round(kms, 4), "substeps": nsub, "mean_ncon": float(ncon.mean()),
             "finite": ok}
 
 
 def main():
-    """Every config, or (arguments) only those whose key is given: 1 1' 2 2' 3 3' 3'' 5."""
-    import torch  # noqa: F401  (one HIP runtime for torch and libdx)
-
+    """Every config, or (arguments) only those whose key is given: 1 1' 2 2' 3 3' 3'' 5 5p."""
     from bench import cpu_baseline_reach_1env
 
     runs = {
@@ -119,7 +121,8 @@ def main():
                                  "state_dense", 4096, solver="CG"),
         "3''": lambda: env_config("3'' reorient.state_dense, PGS solver at MuJoCo's defaults", "reorient",
                                   "state_dense", 4096, solver="PGS"),
-        "5": bimanual,
+        "5": lambda: env_config("5 bimanual.state_dense (two-hand handover task)", "bimanual", "state_dense", 4096),
+        "5p": bimanual,
     }
     for k in (sys.argv[1:] or list(runs)):
         print(json.dumps(runs[k]()), flush=True)

@@ -16,7 +16,7 @@ cd /tmp && export TMPDIR=/tmp
 for v in new prev; do
   lib=""; [ $v = prev ] && lib="DX_LIB=$R/variants/prev/libdx.so"
   env $lib timeout -k 10 240 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY --kernel-trace -d $O/$v -o pmc --output-format csv -- \
-    python3 $R/bench.py --steps 6 --warmup 2 --no-cpu-baseline > $O/$v.log 2>&1 || exit 1
+    python3 $R/bench.py --steps 6 --warmup 2 --no-cpu-baseline --host-api-steps 0 > $O/$v.log 2>&1 || exit 1
 done
 cd $R && python3 - <<'PY'
 import csv, glob, statistics

@@ -4,5 +4,5 @@
 set -e
 mkdir -p gpurun_out
 for pad in ${@:-0 1000 4000}; do
-  DX_LDS_PAD=$pad timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 300 > gpurun_out/occ_$pad.log 2>&1
+  DX_LDS_PAD=$pad timeout -k 10 120 python -u bench.py --no-cpu-baseline --host-api-steps 0 --steps 300 > gpurun_out/occ_$pad.log 2>&1
 done

@@ -11,7 +11,7 @@ run() {  # run <name> <counter> [ENV=VALUE]
   name=$1; ctr=$2; shift 2
   for kv in "$@"; do export "$kv"; done
   timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace -d "$O/$name/$ctr" -o pmc --output-format csv -- \
-    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/$name.$ctr.log" 2>&1
+    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --host-api-steps 0 > "$O/$name.$ctr.log" 2>&1
   for kv in "$@"; do unset "${kv%%=*}"; done
 }
 run xcd FETCH_SIZE

@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 run() {  # run <name> <counter> [ENV=VALUE ...]
   name=$1; ctr=$2; shift 2
   env "$@" timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace -d "$O/$name/$ctr" -o pmc --output-format csv -- \
-    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/$name.$ctr.log" 2>&1
+    python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --host-api-steps 0 > "$O/$name.$ctr.log" 2>&1
   rc=$?; echo "$name $ctr rc=$rc"; return $rc
 }
 for cfg in "default" "noqueue DX_NO_QUEUE=1" "nofuse DX_NO_FUSE=1"; do

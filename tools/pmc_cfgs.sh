@@ -12,7 +12,7 @@ while [ $# -gt 0 ]; do
   name=$1; vars=$2; shift 2; names+=("$name")
   for ctr in FETCH_SIZE WRITE_SIZE; do
     env $vars timeout -k 10 240 rocprofv3 --pmc "$ctr" --kernel-trace -d "$O/$name/$ctr" -o pmc --output-format csv -- \
-      python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/$name.$ctr.log" 2>&1
+      python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --host-api-steps 0 > "$O/$name.$ctr.log" 2>&1
     rc=$?; echo "$name $ctr rc=$rc"; [ $rc = 0 ] || exit $rc
   done
 done

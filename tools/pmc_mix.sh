@@ -16,7 +16,7 @@ for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY" "SQ_AC
            "SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA" "SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH" "SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --kernel-trace -d "$O/p$i" -o pmc --output-format csv -- \
-    python3 "$R/bench.py" --steps 6 --warmup 2 --no-cpu-baseline > "$O/p$i.log" 2>&1
+    python3 "$R/bench.py" --steps 6 --warmup 2 --no-cpu-baseline --host-api-steps 0 > "$O/p$i.log" 2>&1
   rc=$?
   echo "pass $i ($grp) rc=$rc"
   case $rc in 124|137|134|139) exit $rc;; esac

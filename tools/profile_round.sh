@@ -8,11 +8,11 @@ O=$R/gpurun_out/prof
 rm -rf "$O"; mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- \
-  python3 "$R/bench.py" --steps 40 --warmup 5 --no-cpu-baseline > "$O/bench_under_rocprof.log" 2>&1
+  python3 "$R/bench.py" --steps 40 --warmup 5 --no-cpu-baseline --host-api-steps 0 > "$O/bench_under_rocprof.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$O/fetch" -o pmc --output-format csv -- \
-  python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/fetch.log" 2>&1
+  python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --host-api-steps 0 > "$O/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$O/write" -o pmc --output-format csv -- \
-  python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$O/write.log" 2>&1
+  python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --host-api-steps 0 > "$O/write.log" 2>&1
 cd "$R"
 timeout -k 10 300 python3 tools/stage_profile.py 4096 10 > "$O/stages.log" 2>&1
 cp gpurun_out/stages.json "$O/stages.json"
