@@ -84,8 +84,8 @@ def load(path: str = LIB_PATH):
             f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
         )
     L = ctypes.CDLL(path)
-    L.dx_build_key.restype = ctypes.c_char_p
     if path == os.path.join(_HERE, "libdx.so") and os.path.isdir(os.path.join(_HERE, "csrc")):
+        L.dx_build_key.restype = ctypes.c_char_p
         # the in-tree library must have been built from the sources beside it (a GPU box
         # runs the library that travelled with the tree, without rebuilding)
         from dexterity_amd import build as _build
@@ -150,7 +150,8 @@ def load(path: str = LIB_PATH):
     L.dx_env_state_field.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(sz),
                                      ctypes.POINTER(sz)]
     L.dx_env_pack_outputs.argtypes = [vp, vp]
-    L.dx_env_step_host.argtypes = [vp, vp, vp]
+    if hasattr(L, "dx_env_step_host"):  # (round 6; an older variant library for A/B lacks it)
+        L.dx_env_step_host.argtypes = [vp, vp, vp]
     L.dx_timing_enable.argtypes = [vp, ctypes.c_int]
     L.dx_timing_read.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(i32)]
     L.dx_stage_timing.argtypes = [vp, ctypes.c_int]

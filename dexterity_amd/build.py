@@ -66,10 +66,13 @@ def _units() -> list:
     units = [(os.path.splitext(s)[0], s, ()) for s in SOURCES]
     # a PGS specialization runs one wave per SIMD: AR's diagonal blocks and the rows' P
     # take ~420 VGPRs (dx_step.hip solve_pgs_ar), which two waves per SIMD would spill
-    pgs_waves = os.environ.get("DX_PGS_WAVES", "1")
-    units += [(f"dx_step_{n}", "dx_step.hip",
-               (f"-DDX_SPEC_ONLY={n}",) + ((f"-DDX_STEP_WAVES={pgs_waves}",) if n.endswith("_pgs") else ()))
-              for n in _spec_names()]
+    waves = {"_pgs": os.environ.get("DX_PGS_WAVES", "1"), "_cg": os.environ.get("DX_CG_WAVES")}
+
+    def spec_flags(n):
+        w = next((v for k, v in waves.items() if n.endswith(k) and v), None)
+        return (f"-DDX_SPEC_ONLY={n}",) + ((f"-DDX_STEP_WAVES={w}",) if w else ())
+
+    units += [(f"dx_step_{n}", "dx_step.hip", spec_flags(n)) for n in _spec_names()]
     # the overflow tier: the step kernel's physics with the DX_NCON_HI contact pool
     units.append(("dx_step_hi", "dx_step.hip", ("-DDX_TIER_HI", "-DDX_NCON_MAX=DX_NCON_HI")))
     # the mid tier: the same physics with the DX_NCON_MID pool, beside queued launches

@@ -281,18 +281,18 @@ __device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i,
 }
 // Group reduction: the lowest vertex index among the lanes holding the maximum (a
 // cell's list is sorted by vertex index, a whole hull is scanned in index order, so
-// this is the vertex the oracle's serial scan returns); its coordinates come from the
-// lane that scanned it, found by ballot and read through ds_bpermute.
+// this is the vertex the oracle's serial scan returns); its coordinates reach the group
+// by a DPP max over the group in which every other lane offers -3e38 (one lane holds
+// the winning slot: the indices of a group's slots are distinct) -- no ballot and no
+// ds_bpermute round trip.
 template <int NPG>
 __device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
   float vmax = row_max_f<NPG>(h.d);
   int bi = row_min_i<NPG>(h.d == vmax ? h.i : 0x7fffffff);
-  const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
-  const unsigned grp = (unsigned)(own >> GBASE) & ((1u << NPG) - 1u);
-  int src = GBASE | (grp ? __builtin_ctz(grp) : 0);
-  lp[0] = __shfl(h.x, src, 64);
-  lp[1] = __shfl(h.y, src, 64);
-  lp[2] = __shfl(h.z, src, 64);
+  const bool win = h.d == vmax && h.i == bi;
+  lp[0] = row_max_f<NPG>(win ? h.x : -3.0e38f);
+  lp[1] = row_max_f<NPG>(win ? h.y : -3.0e38f);
+  lp[2] = row_max_f<NPG>(win ? h.z : -3.0e38f);
 }
 // Cube-map cell of local direction ld (host twin: dx_api.hip cell_corners).  Returns
 // -1 for a zero direction (then the whole hull is scanned, as the oracle does).
@@ -455,16 +455,23 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
         hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < nov && idx >= 0);
       }
     }
-    // half reduction: the lowest vertex index among the maxima, coordinates from its lane
+    // half reduction: the lowest vertex index among the maxima, its coordinates by a DPP
+    // max in which only the winning lane offers its own (hull_reduce)
     float vmax = fmaxf(h.d, dpp_f<0xB1, 0xF>(h.d));
     if (H == 4) vmax = fmaxf(vmax, dpp_f<0x4E, 0xF>(vmax));
     int bi = h.d == vmax ? h.i : 0x7fffffff;
     bi = min(bi, dpp_i<0xB1, 0xF>(bi));
     if (H == 4) bi = min(bi, dpp_i<0x4E, 0xF>(bi));
-    const unsigned long long own = __ballot(h.d == vmax && h.i == bi);
-    const unsigned qb = (unsigned)(own >> (LANE & ~(H - 1))) & ((1u << H) - 1u);
-    const int src = (LANE & ~(H - 1)) | (qb ? __builtin_ctz(qb) : 0);
-    const float hx = __shfl(h.x, src, 64), hy = __shfl(h.y, src, 64), hz = __shfl(h.z, src, 64);
+    const bool win = h.d == vmax && h.i == bi;
+    float hx = win ? h.x : -3.0e38f, hy = win ? h.y : -3.0e38f, hz = win ? h.z : -3.0e38f;
+    hx = fmaxf(hx, dpp_f<0xB1, 0xF>(hx));
+    hy = fmaxf(hy, dpp_f<0xB1, 0xF>(hy));
+    hz = fmaxf(hz, dpp_f<0xB1, 0xF>(hz));
+    if (H == 4) {
+      hx = fmaxf(hx, dpp_f<0x4E, 0xF>(hx));
+      hy = fmaxf(hy, dpp_f<0x4E, 0xF>(hy));
+      hz = fmaxf(hz, dpp_f<0x4E, 0xF>(hz));
+    }
     if (mesh) { lp[0] = hx; lp[1] = hy; lp[2] = hz; }
   }
   if (type != DXG_MESH) support_prim(S, ld, lp);
@@ -2609,7 +2616,7 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
 }
 
 #ifndef DX_PGS_NB
-#define DX_PGS_NB 2  // PGS register blocks of 64 rows (AR's diagonal blocks, one column per lane)
+#define DX_PGS_NB 3  // PGS register blocks of 64 rows (AR's diagonal blocks, one column per lane)
 #endif
 #define DX_PGS_AR 64
 // Visit the nonzeros (e, v) of constraint row k (k < 0: none) from the row's compact form
@@ -2722,17 +2729,26 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
   };
   constexpr auto blocks = std::make_integer_sequence<int, NB>{};
   constexpr auto rows = std::make_integer_sequence<int, DX_PGS_AR>{};
+  // Per lane and block: its row's P, its column of AR scaled by 1 / AR_kk (A'), and the
+  // row's state in the scaled form the row update's chain needs: res' = res / AR_kk, and
+  // the box relative to the force, lof = lo - f, hif = hi - f, so that the force change of
+  // a row is dl = med3(-res', lof, hif) (f - res / AR_kk projected on [lo, hi], minus f).
+  const int lane = LANE;
   float P[NB][30], A[NB][DX_PGS_AR];
-  float fb[NB], res[NB], idg[NB], lo[NB], hi[NB], rs[NB], bb[NB], rk[NB], hdg[NB];
+  float lof[NB], hif[NB], lob[NB], res[NB], rs[NB], bb[NB], rk[NB], dgv[NB], idg[NB];
   static_for([&](auto Bc) {
     constexpr int B = Bc.value;
-    const int k = DX_PGS_AR * B + LANE;
+    const int k = DX_PGS_AR * B + lane;
     const bool in = k < nefc;
     const int kc = min(k, nefc - 1);
     rk[B] = in ? 1.0f / D[kc] : 0.f;
-    fb[B] = in ? f[kc] : 0.f;
+    const float f0 = in ? f[kc] : 0.f;
     bb[B] = in ? jar[kc] - aref[kc] : 0.f;
-    box(k, lo[B], hi[B]);
+    float l, h;
+    box(k, l, h);
+    lob[B] = l;
+    lof[B] = l - f0;
+    hif[B] = h - f0;
     res[B] = 0.f;
     rs[B] = 0.f;
     if (B < nb) {
@@ -2744,10 +2760,11 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
       static_for([&](auto K) { A[B][K.value] = 0.f; }, rows);
     }
     float dg = 1.f;  // AR_kk, this lane's diagonal entry (1 on a padding row)
-    static_for([&](auto K) { dg = LANE == K.value ? A[B][K.value] : dg; }, rows);
+    static_for([&](auto K) { dg = lane == K.value ? A[B][K.value] : dg; }, rows);
     dg = in ? dg : 1.f;
+    dgv[B] = dg;
     idg[B] = 1.0f / dg;
-    hdg[B] = 0.5f * dg;
+    static_for([&](auto K) { A[B][K.value] *= idg[B]; }, rows);
   }, blocks);
   float ardt = 1.f;  // lane t: AR of tail row NB x 64 + t on the diagonal
   for (int t = 0; t < ntail; t++) {
@@ -2765,8 +2782,11 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
 #pragma unroll
     for (int d = 0; d < 32; d++) t[d] = 0.f;
     static_for([&](auto Bc) {
+      if (Bc.value < nb) {
+        const float fk = lob[Bc.value] - lof[Bc.value];  // this lane's row's force
 #pragma unroll
-      for (int d = 0; d < 30; d++) t[d] = fmaf(fb[Bc.value], P[Bc.value][d], t[d]);
+        for (int d = 0; d < 30; d++) t[d] = fmaf(fk, P[Bc.value][d], t[d]);
+      }
     }, blocks);
     const float r = wave_reduce_scatter32(t);  // component LANE >> 1
     const float wd = __int_as_float(__builtin_amdgcn_ds_bpermute(8 * (LANE & 31), __float_as_int(r)));
@@ -2781,15 +2801,18 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
     }
     return s0 + s1;
   };
-  // one row update, in the row's lane q (q static: a register name of A[B])
-#define DX_PGS_ROWL(q, Acol, rsv, fv, idgv, lov, hiv, snap)                 \
-  {                                                                          \
-    const float fn = __builtin_amdgcn_fmed3f(fmaf(-rsv, idgv, fv), lov, hiv); \
-    const float dl = rl(fn - fv, q);                                         \
-    const bool me = LANE == (q);                                             \
-    snap = me ? rsv : snap;                                                  \
-    fv = me ? fn : fv;                                                       \
-    rsv = fmaf(dl, Acol[q], rsv);                                            \
+  // one row update, in the row's lane q (q static: a register name of A[B]).  The chain
+  // from one row to the next is med3 -> readlane -> fma.  A lane's box (lof, hif) changes
+  // only at its own row, which a sweep visits once, so the row's change is kept (dsv) and
+  // the box moves after the block's sweep; its residual at the update is kept too (snap).
+#define DX_PGS_ROWL(q, Acol, rsv, lofv, hifv, dsv, snap)                \
+  {                                                                     \
+    const float dla = __builtin_amdgcn_fmed3f(-rsv, lofv, hifv);        \
+    const float dl = rl(dla, q);                                        \
+    const bool me = lg == (q);                                          \
+    dsv = me ? dla : dsv;                                               \
+    snap = me ? rsv : snap;                                             \
+    rsv = fmaf(dl, Acol[q], rsv);                                       \
   }
   constexpr auto groups = std::make_integer_sequence<int, DX_PGS_AR / 8>{};
   constexpr auto eight = std::make_integer_sequence<int, 8>{};
@@ -2805,17 +2828,24 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
         // newton_linesearch, the formation above as newton_hessian)
         if (nb > 1 || ntail > 0 || it == 0) {  // (one block alone keeps its residuals current)
           wsum();
-          res[B] = dotw(P[B]) + bb[B] + rk[B] * fb[B];
+          res[B] = (dotw(P[B]) + bb[B] + rk[B] * (lob[B] - lof[B])) * idg[B];
           stage_mark(c, ST_NEWTON_GRAD);
         }
-        const float f0 = fb[B];
+        float df = 0.f;  // this lane's row's force change in the sweep
         static_for([&](auto Gc) {
-          if (DX_PGS_AR * B + 8 * Gc.value < nefc)
-            static_for([&](auto Q) { DX_PGS_ROWL(8 * Gc.value + Q.value, A[B], res[B], fb[B], idg[B], lo[B], hi[B], rs[B]) },
+          if (DX_PGS_AR * B + 8 * Gc.value < nefc) {
+            // (the lane id laundered per group: the compiler would otherwise hoist all 64
+            // lane == q masks out of the sweep loop and spill them)
+            int lg = lane;
+            asm volatile("" : "+v"(lg));
+            static_for([&](auto Q) { DX_PGS_ROWL(8 * Gc.value + Q.value, A[B], res[B], lof[B], hif[B], df, rs[B]) },
                        eight);
+          }
         }, groups);
-        const float df = fb[B] - f0;
-        il -= df * fmaf(hdg[B], df, rs[B]);
+        lof[B] -= df;
+        hif[B] -= df;
+        // -(AR_kk df^2 / 2 + df res) with res = AR_kk res' at the row's update
+        il -= df * dgv[B] * fmaf(0.5f, df, rs[B]);
         stage_mark(c, ST_NEWTON_LS);
       }
     }, blocks);
@@ -2862,10 +2892,11 @@ __device__ __forceinline__ void solve_pgs_ar(const Ctx& c, float scale, float to
   }
   // the forces, as residuals whose primal force is f_r
   static_for([&](auto Bc) {
-    const int k = DX_PGS_AR * Bc.value + LANE;
+    const int k = DX_PGS_AR * Bc.value + lane;
+    const float fk = lob[Bc.value] - lof[Bc.value];
     if (k < nefc) {
-      f[k] = fb[Bc.value];
-      jar[k] = -fb[Bc.value] / D[k];
+      f[k] = fk;
+      jar[k] = -fk / D[k];
     }
   }, blocks);
   for (int r = NB * DX_PGS_AR + LANE; r < nefc; r += DX_WAVE) jar[r] = -f[r] / D[r];
