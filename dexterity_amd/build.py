@@ -65,8 +65,10 @@ def _units() -> list:
     scene specialization (-DDX_SPEC_ONLY), so the kernels compile in parallel."""
     units = [(os.path.splitext(s)[0], s, ()) for s in SOURCES]
     # a PGS specialization runs one wave per SIMD: AR's diagonal blocks and the rows' P
-    # take ~420 VGPRs (dx_step.hip solve_pgs_ar), which two waves per SIMD would spill
-    waves = {"_pgs": os.environ.get("DX_PGS_WAVES", "1"), "_cg": os.environ.get("DX_CG_WAVES")}
+    # take ~430 VGPRs (dx_step.hip solve_pgs_ar), which two waves per SIMD would spill
+    # (CG too: its launch is bound by its slowest envs' chains, which run faster alone on a
+    # SIMD -- config 3' 0.872 -> 0.900 M env-steps/s same-box, round 6)
+    waves = {"_pgs": os.environ.get("DX_PGS_WAVES", "1"), "_cg": os.environ.get("DX_CG_WAVES", "1")}
 
     def spec_flags(n):
         w = next((v for k, v in waves.items() if n.endswith(k) and v), None)

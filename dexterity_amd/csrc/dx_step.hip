@@ -2619,6 +2619,13 @@ __device__ __forceinline__ void pgs_row(const Ctx& c, int r, float* Jd) {
 #define DX_PGS_NB 3  // PGS register blocks of 64 rows (AR's diagonal blocks, one column per lane)
 #endif
 #define DX_PGS_AR 64
+#ifndef DX_PGS_NB_TIER
+#if defined(DX_TIER_HI)
+#define DX_PGS_NB_TIER 3
+#else
+#define DX_PGS_NB_TIER 2
+#endif
+#endif
 // Visit the nonzeros (e, v) of constraint row k (k < 0: none) from the row's compact form
 // (jac_rows / pgs_jrow): one dof (friction loss, joint limit), a tendon's dofs, or a
 // contact row's support dofs.  k may differ by lane (then e and v do too) or be uniform.
@@ -2963,8 +2970,9 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
     for (int r = LANE; r < nefc; r += DX_WAVE) f[r] = 0.f;
   SYNC();
   if (inv) {
-    // (the generic kernel and the contact tiers, within two waves' VGPRs: one block)
-    constexpr int NB = Ctx::is_spec ? DX_PGS_NB : 1;
+    // (the generic kernel and the mid tier, within two waves' VGPRs, hold two blocks; the
+    // overflow tier runs one wave per SIMD)
+    constexpr int NB = Ctx::is_spec ? DX_PGS_NB : DX_PGS_NB_TIER;
     if (nefc <= NB * DX_PGS_AR + DX_WAVE) {
       solve_pgs_ar<NB>(c, scale, tol, T);
       return;

@@ -588,14 +588,18 @@ def _contact_lists_agree(d, recs, cm=None, deep=None, divergent=False):
     an exact support-based answer, a terminal portal of MPR from another start (deep
     finger-finger overlaps of the two-hand scene, where MPR's answer is discontinuous).
 
-    `divergent` (the last resort of _account_full_batch): a deep mesh-mesh contact (|dist|
-    > 0.5 mm) whose point agrees within 2e-4 m and depth within 15 % also passes, whatever
-    its normal: fp32 MPR's refinement can stop on another sliver portal of a deep overlap
-    of two curved hulls than fp64 MPR's (same contact point, another normal and depth);
-    appended to `deep` with rule "divergent".  (10 % until round 5, when a reorient state
-    mix shifted by a rounding change held a finger-finger pair at 1.398 mm on the GPU
-    against the oracle's 1.265 mm -- the fp64 minimum penetration -- with the point
-    within 1.3e-8 m and the normal 0.42 apart: 10.5 %.)"""
+    `divergent` (the last resort of _account_full_batch): a deep hull-hull or box-hull
+    contact (|dist| > 0.5 mm) whose (normal, depth) is the reference algorithm's answer in
+    fp32 -- the
+    oracle's MPR restated with the arithmetic type as a parameter (oracle/mpr_ref.py),
+    evaluated in fp32 from the geoms' poses perturbed at the fp32 forward kinematics'
+    resolution, reproduces the GPU's contact to 1e-4 rad and 1e-4 of the depth
+    (fp32_reproduces) -- also passes: at a deep overlap of two curved hulls fp32 and fp64
+    MPR stop on different portals (another normal, a depth 4-11 % apart), and the fp32
+    one is what the kernel computes.  Appended to `deep` with rule "fp32 portal".  Round 6
+    replaced round 5's window (any normal, depth within 15 %) by this reproduction; the
+    states that needed it are committed fixtures (tests/golden/fullbatch_*_fp32_portal.npz,
+    tests/test_mpr_precision.py)."""
     oc = d.contacts()
     ties = 0
 
@@ -603,8 +607,11 @@ def _contact_lists_agree(d, recs, cm=None, deep=None, divergent=False):
         if cm is None or deep is None or abs(o[12]) <= 1e-4:
             return False
         g1, g2 = int(o[13]), int(o[14])
-        if int(cm.geom_type[g1]) != 7 or int(cm.geom_type[g2]) != 7:
+        t1, t2 = int(cm.geom_type[g1]), int(cm.geom_type[g2])
+        if t1 not in (6, 7) or t2 not in (6, 7):
             return False
+        if t1 != 7 or t2 != 7:  # a box against a hull: the fp32 portal rule alone
+            return fp32_portal(r, o, g1, g2)
         pen = _min_penetration(cm, d, g1, g2, (r[3:6], o[3:6]))
         if abs(r[12] - pen) <= 0.03 * abs(pen):
             deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(pen), "min"))
@@ -613,10 +620,16 @@ def _contact_lists_agree(d, recs, cm=None, deep=None, divergent=False):
         if abs(sep - r[12]) <= max(2e-5, 0.03 * abs(r[12])):
             deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(sep), "boundary"))
             return True
-        if (divergent and abs(o[12]) > 5e-4 and abs(r[12] - o[12]) <= 0.15 * abs(o[12])
-                and np.abs(r[0:3] - o[0:3]).max() < 2e-4):
-            deep.append((int(o[13]), int(o[14]), float(r[12]), float(o[12]), float(sep), "divergent"))
-            return True
+        return fp32_portal(r, o, g1, g2)
+
+    def fp32_portal(r, o, g1, g2):
+        if divergent and abs(o[12]) > 5e-4:
+            from oracle.mpr_ref import fp32_reproduces
+
+            ok, ang, dr, _ = fp32_reproduces(cm, d, g1, g2, r)
+            if ok:
+                deep.append((g1, g2, float(r[12]), float(o[12]), float(ang), "fp32 portal"))
+                return True
         return False
 
     used = np.zeros(len(oc), dtype=bool)
@@ -714,7 +727,7 @@ def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label
             dp = []
             why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, compiled, dp)
             deep += dp
-        if why is not None and sq <= 1e-6 and sv <= 5e-4:  # the last resort: a divergent deep portal
+        if why is not None and sq <= tq and sv <= tv:  # the last resort: a deep fp32 portal
             dp = []
             why, t = _contact_lists_agree(_oracle_forward(oracle_mod, om, None, x32, st), recs, compiled, dp, True)
             if why is None:
@@ -722,7 +735,7 @@ def _account_full_batch(oracle_mod, om, compiled, x32, h, states, gpu_out, label
                 kinds["divergent"] += 1
                 divergent.append(int(e))
                 continue
-        if why is None and sq <= 1e-6 and sv <= 5e-4:
+        if why is None and sq <= tq and sv <= tv:
             kinds["geometry"] += 1
             ties += t
         elif why is None and solver == "Newton" and excess <= 1e-7 and sv <= 5e-4 and sq <= h * 5e-4 * scale[e]:
@@ -762,19 +775,14 @@ FULL_SOLVER_QPOS, FULL_SOLVER_QVEL = 1e-4, 5e-3
 
 @pytest.mark.parametrize("solver", ["Newton", "CG", "PGS"])
 def test_full_batch_parity(gpu, oracle_mod, solver):
-    """BASELINE config 3 at full size, on the bench's own state mix: 4096 reorient envs
-    after 40 control steps of the random agent (auto-resets, falls, deep contact-rich
-    grasps, the overflow tier included).  Every env's fp32 state then takes one physics
-    step on the GPU and in the fp64 oracle (OpenMP over envs), with each of the three
-    solvers at MuJoCo's defaults: the headline's Newton, and CG / PGS (config 3' / 3'',
-    their own kernel specializations).  The state mix is the headline's for all three, so
-    the contact-geometry side of the accounting is one set of states and the solver
-    parametrization holds each solver kernel's step from every one of them.  (Stepped
-    along their own trajectories, CG's and PGS's mixes also held 2 and 1 box-mesh
-    contacts whose fp32 MPR normal differs from the fp64 oracle's by 0.1-0.27 rad at a
-    1-6 mm overlap -- tools/divergent_repro.py; geometry, the same MPR in every kernel.)  Tight: qpos within 1e-6 and qvel within 5e-4 of max(1,
-    |qacc_smooth|).  Every state outside it must be accounted for, one of three ways, and
-    none may remain:
+    """BASELINE config 3 at full size, on each configuration's own bench state mix: 4096
+    reorient envs after 40 control steps of the random agent (auto-resets, falls, deep
+    contact-rich grasps, the overflow tier included), with each of the three solvers at
+    MuJoCo's defaults -- the headline's Newton, and CG / PGS (config 3' / 3'', their own
+    kernel specializations), each stepping its own trajectory.  Every env's fp32 state then
+    takes one physics step on the GPU and in the fp64 oracle with the same solver (OpenMP
+    over envs).  Tight: qpos within 1e-6 and qvel within 5e-4 of max(1, |qacc_smooth|).
+    Every state outside it must be accounted for, one of these ways, and none may remain:
       * MPR discontinuity: the GPU equals (tight) one of the oracle's runs from the state
         perturbed at fp32 resolution (_nearest_perturbed);
       * contact geometry: the oracle's dynamics run on the GPU's own contact list
@@ -786,12 +794,23 @@ def test_full_batch_parity(gpu, oracle_mod, solver):
         the oracle's fp64 cost to within 1e-7 of the cost (the fp32 resolution of the cost
         the kernel's Newton stops at), qvel within the tight bound and qpos within that
         bound integrated over the step (h x 5e-4 of the scale); CG and PGS -- the oracle's
-        same solver on the GPU's contacts from the same warm start reproduces the GPU's
-        step within FULL_SOLVER_QPOS / FULL_SOLVER_QVEL."""
+        same solver from the same state and warm start (or on the GPU's contacts)
+        reproduces the GPU's step within FULL_SOLVER_QPOS / FULL_SOLVER_QVEL, their
+        "tight" (100 iterations / sweeps stop short of the optimum, where fp32 and fp64
+        walk the same iteration apart); CG, a primal method, also when its iterate is as
+        good in the oracle's fp64 cost as the oracle's own CG's (to 1e-6 of the cost);
+      * fp32 portal (the last resort): every contact list difference is a deep box-hull or
+        hull-hull contact that the reference MPR evaluated in fp32 reproduces
+        (_contact_lists_agree `divergent`, oracle/mpr_ref.py)."""
     from dexterity_amd import manipulation
 
     n = 4096
-    env = manipulation.load("reorient", "state_dense", seed=1, num_envs=n)
+    if solver == "Newton":
+        env = manipulation.load("reorient", "state_dense", seed=1, num_envs=n)
+    else:  # config 3' / 3'': <option solver=...> at MuJoCo's defaults (tools/bench_configs.py)
+        t = manipulation.SUITE[("reorient", "state_dense")]()
+        t.compiled = t.compiled.with_solver(solver)
+        env = manipulation.GoalEnvironment(t, num_envs=n, seed=1)
     env.reset()
     for step in range(40):
         env.step_random(step)
@@ -806,7 +825,7 @@ def test_full_batch_parity(gpu, oracle_mod, solver):
     ncon = ph.get(_lib.NCON)[:, 0]
     assert (ncon > 0).mean() > 0.5
     xfrc = env.task.gravity_compensation
-    model = env.model if solver == "Newton" else gpu.Model(env.task.compiled.with_solver(solver))
+    model = env.model
     env.close()
     # the GPU: the forward pass (contacts, qacc, and qacc_smooth for the error scale), then
     # one physics step from exactly these states
@@ -842,7 +861,7 @@ def test_full_batch_parity(gpu, oracle_mod, solver):
     cap = FULL_CEILINGS[solver]
     assert (~tight).mean() <= cap["outside"]
     assert kinds["perturbed"] <= cap["perturbed"] and kinds["geometry"] <= 20 and kinds["solver"] <= cap["solver"], kinds
-    assert kinds["divergent"] <= 2, kinds
+    assert kinds["divergent"] <= cap["fp32_portal"], kinds
     assert not unexplained
     # ("min": the GPU's depth within 3 % of the fp64 minimum penetration -- as good an
     # answer as MPR gives; the other rules are the ones held to a count)
@@ -853,9 +872,9 @@ def test_full_batch_parity(gpu, oracle_mod, solver):
 # the headline mix: CG 316 outside the tight bound -- 184 solver (its 100 iterations stop
 # short on a linearly converging path, fp32 and fp64 apart), 125 perturbed, 5 geometry, 2
 # divergent; PGS 204 -- 71 solver, 126 perturbed, 5 geometry, 2 divergent; 0 unexplained)
-FULL_CEILINGS = {"Newton": dict(outside=0.06, perturbed=220, solver=8),
-                 "CG": dict(outside=0.09, perturbed=180, solver=240),
-                 "PGS": dict(outside=0.07, perturbed=180, solver=120)}
+FULL_CEILINGS = {"Newton": dict(outside=0.06, perturbed=220, solver=8, fp32_portal=2),
+                 "CG": dict(outside=0.09, perturbed=300, solver=240, fp32_portal=6),
+                 "PGS": dict(outside=0.07, perturbed=220, solver=120, fp32_portal=6)}
 
 
 def test_ground_contact_watch_matches_oracle(gpu, oracle_mod, reorient_setup):
