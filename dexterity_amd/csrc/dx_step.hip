@@ -2340,7 +2340,7 @@ __device__ __forceinline__ int row_zone(int type, float Rf, float jar) {
 // solver needs no separate cost pass.
 // HAVE_MDIR: the caller already holds M dir in v4 (CG's recurrence), no product here.
 // MREG: M's rows in registers (mrow_load), the product without LDS.
-template <bool NEWTON = false, bool HAVE_MDIR = false, bool MREG = false, class Ctx>
+template <bool NEWTON = false, bool HAVE_MDIR = false, bool MREG = false, bool HAVE_JV = false, class Ctx>
 __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, const float* Ma, const float* dir, int* changed,
                                              float* slope0 = nullptr, const float* grad = nullptr,
                                              float gauss = 0.f, float* cost_new = nullptr, float* gauss_new = nullptr,
@@ -2354,8 +2354,10 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
     stage_mark(c, ST_MATVEC);
   }
   float* jv = c.f(c.L.efc_jv);
-  jac_vec(c, dir, jv);  // includes SYNC
-  stage_mark(c, ST_JACVEC);
+  if (!HAVE_JV) {  // (HAVE_JV: the caller has J dir in efc_jv)
+    jac_vec(c, dir, jv);  // includes SYNC
+    stage_mark(c, ST_JACVEC);
+  }
   const float* qs = c.f(c.L.qfrc_smooth);
   float qa = 0, qb = 0, qg = 0;
   for (int i = LANE; i < nv; i += DX_WAVE) {
@@ -2452,6 +2454,177 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
   return alpha;
 }
 
+// solve_cg for nv <= 30 and up to 128 rows, every vector in registers (round 6): lane d
+// holds qacc, M qacc, qfrc_smooth, grad, M^-1 grad, dir and M dir of dof d, lanes r and
+// 64 + r hold rows r / 64 + r -- J's row dense (30 registers), its type, D, floss, R and
+// residual.  M^-1 grad and M x are 30 readlanes and FMAs against the matrices' rows in
+// registers, J dir one FMA per dof in the row's lane, J'f a reduce-scatter of every lane's
+// f_r J_r (wave_reduce_scatter32); the exact line search runs on the row registers.  No LDS
+// vector, no contact-frame pass and no atomic per iteration: what is left on the chain is
+// the wave sums of the dot products.  The same algorithm and tests as solve_cg.
+template <class Ctx, class F>
+__device__ __forceinline__ void pgs_row_nz(const Ctx& c, int k, F&& add);
+template <class Ctx>
+__device__ __forceinline__ void solve_cg_reg(const Ctx& c, float scale, float tol) {
+  const int nv = c.nv, nefc = c.I[I_NEFC];
+  const int lane = LANE;
+  const bool dof = lane < nv;
+  const int dc = min(lane, nv - 1);
+  float* qacc = c.f(c.L.qacc);
+  float* Ma = c.f(c.L.v1);
+  float* jar = c.f(c.L.efc_jar);
+  const float* M = c.f(c.L.M);
+  const float* qs = c.f(c.L.qfrc_smooth);
+  float* T = c.f(c.L.H);
+  float x = dof ? qacc[dc] : 0.f, ma = dof ? Ma[dc] : 0.f, q0 = dof ? qs[dc] : 0.f;
+  float trow[30], mrow[30];  // lane i: row i of M^-1 and of M
+  mfma_sweep_inverse30(M, nv, T);
+  mrow_load(T, nv, trow);
+  mrow_load(M, nv, mrow);
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* Dp = c.f(c.L.efc_D);
+  const float* flp = c.f(c.L.efc_fl);
+  const float* Rfp = c.f(c.L.efc_Rf);
+  float Jd[2][30];
+  int ty[2];
+  float D[2], fl[2], Rf[2], ja[2], jj[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int r = lane + DX_WAVE * h, rc = min(r, nefc - 1);
+    const bool ok = r < nefc, fr = ok && r < c.nfric;
+    ty[h] = ok ? (meta[rc] & 15) : DXR_CON;
+    D[h] = ok ? Dp[rc] : 0.f;
+    fl[h] = fr ? flp[rc] : 0.f;
+    Rf[h] = fr ? Rfp[rc] : 0.f;
+    ja[h] = ok ? jar[rc] : 0.f;
+    jj[h] = 0.f;
+#pragma unroll
+    for (int d = 0; d < 30; d++) Jd[h][d] = 0.f;
+    if (DX_WAVE * h < nefc)
+      pgs_row_nz(c, ok ? r : -1, [&](int e, float v) {  // (v = 0 from lanes without a nonzero here)
+#pragma unroll
+        for (int d = 0; d < 30; d++) Jd[h][d] = d == e ? Jd[h][d] + v : Jd[h][d];
+      });
+  }
+  auto rows_of = [&](const float (&mr)[30], float v) {  // (mr v) of this lane's row
+    float y0 = 0.f, y1 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 30; e += 2) {
+      y0 = fmaf(mr[e], rl(v, e), y0);
+      y1 = fmaf(mr[e + 1], rl(v, e + 1), y1);
+    }
+    return y0 + y1;
+  };
+  auto jt_force = [&]() {  // (J'f)_d of the rows' forces at the residuals ja
+    float t[32];
+#pragma unroll
+    for (int d = 0; d < 32; d++) t[d] = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (DX_WAVE * h < nefc) {
+        float f, hw;
+        row_cost(ty[h], D[h], fl[h], Rf[h], ja[h], f, hw);
+#pragma unroll
+        for (int d = 0; d < 30; d++) t[d] = fmaf(f, Jd[h][d], t[d]);
+      }
+    }
+    const float w = wave_reduce_scatter32(t);  // component LANE >> 1
+    const float wd = __int_as_float(__builtin_amdgcn_ds_bpermute(8 * (lane & 31), __float_as_int(w)));
+    return dof ? wd : 0.f;
+  };
+  auto j_dir = [&](float v) {  // jj = J v, row by row in the row's lane
+    float xs[30];
+#pragma unroll
+    for (int d = 0; d < 30; d++) xs[d] = rl(v, d);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      float s0 = 0.f, s1 = 0.f;
+      if (DX_WAVE * h < nefc) {
+#pragma unroll
+        for (int d = 0; d < 30; d += 2) {
+          s0 = fmaf(Jd[h][d], xs[d], s0);
+          s1 = fmaf(Jd[h][d + 1], xs[d + 1], s1);
+        }
+      }
+      jj[h] = s0 + s1;
+    }
+  };
+  float grad = ma - q0 - jt_force();
+  float mg = rows_of(trow, grad);
+  float dir = -mg, mdir = -grad;
+  float gmg_old = wave_sum(grad * mg);
+  int it = 0;
+  for (; it < c.iterations; it++) {
+    stage_count(c, CNT_NEWTON_IT);
+    j_dir(dir);
+    stage_mark(c, ST_JACVEC);
+    // the exact line search (line_search<false, true>) on the row registers
+    const float qa = wave_sum(dir * mdir), qb = wave_sum(dir * (ma - q0));
+    float lo = 0.f, hi = -1.f, alpha = 0.f, g0 = 0.f;
+    int ls = 0;
+    for (; ls < 40; ls++) {
+      float g = 0.f, hh = 0.f;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        if (DX_WAVE * h < nefc) {
+          float f, hw;
+          row_cost(ty[h], D[h], fl[h], Rf[h], ja[h] + alpha * jj[h], f, hw);
+          g -= f * jj[h];
+          hh += hw * jj[h] * jj[h];
+        }
+      }
+      g = wave_sum(g) + qa * alpha + qb;
+      hh = wave_sum(hh) + qa;
+      if (ls == 0) g0 = g;
+      if (fabsf(g) <= 1e-6f * fabsf(g0)) break;
+      if (g < 0) lo = alpha; else hi = alpha;
+      float next = hh > 0 ? alpha - g / hh : alpha + 1;
+      if (hi >= 0 && (next <= lo || next >= hi)) next = 0.5f * (lo + hi);
+      if (hi < 0 && next <= lo) next = lo + 1;
+      if (fabsf(next - alpha) <= 1e-7f * fabsf(alpha)) break;
+      alpha = next;
+    }
+    stage_count(c, CNT_LS_IT, min(ls + 1, 40));
+    stage_mark(c, ST_NEWTON_LS);
+    if (alpha == 0.f) break;
+    x = fmaf(alpha, dir, x);
+    ma = fmaf(alpha, mdir, ma);
+    const float mg_old = mg;
+#pragma unroll
+    for (int h = 0; h < 2; h++) ja[h] = fmaf(alpha, jj[h], ja[h]);
+    // the decrease along the line, -alpha g0 / 2 (solve_cg)
+    const float impr = -0.5f * scale * alpha * g0;
+    grad = ma - q0 - jt_force();
+    const float gn = sqrtf(wave_sum(grad * grad)) * scale;
+    mg = rows_of(trow, grad);
+    stage_mark(c, ST_NEWTON_GRAD);
+    if (impr < tol || gn < tol) {
+      it++;
+      break;
+    }
+    const float num = wave_sum(grad * (mg - mg_old)), gmg = wave_sum(grad * mg);
+    const float beta = fmaxf(0.f, num / fmaxf(1e-15f, gmg_old));
+    gmg_old = gmg;
+    const float di = -mg + beta * dir;
+    const bool restart = !(wave_sum(grad * di) < 0.f);  // not a descent direction
+    dir = restart ? -mg : di;
+    mdir = restart ? -grad : fmaf(beta, mdir, -grad);
+    // (the recurrences hold only as far as M M^-1 = I: M qacc and M dir exactly on a
+    // restart and every 8 iterations, as solve_cg)
+    if (restart || (it & 7) == 7) {
+      ma = rows_of(mrow, x);
+      mdir = rows_of(mrow, dir);
+    }
+  }
+  if (dof) { qacc[lane] = x; Ma[lane] = ma; }
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int r = lane + DX_WAVE * h;
+    if (r < nefc) jar[r] = ja[h];
+  }
+  if (lane == 0) c.I[I_NITER] = it;
+  SYNC();
+}
 // [3P] MuJoCo's primal CG (mj_solCG), <option solver="CG">: the Newton solver's cost,
 // warm start and exact line search with Polak-Ribiere directions preconditioned by M
 // (Mgrad = M^-1 grad through the matrix-core Cholesky of M), and the same convergence
@@ -2490,8 +2663,74 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
       chol_solve(M, nv, Mg, T);
     }
   };
+  // J's rows dense in registers (lane r: rows r and 64 + r, up to 128 rows, nv <= 30):
+  // J dir is then one FMA per dof with dir broadcast from LDS, and J'f a reduce-scatter of
+  // every lane's f_r J_r over the wave (wave_reduce_scatter32) -- no contact-frame passes,
+  // no LDS atomics.  (Other sizes keep jac_vec / jac_t_force.)
+  const int nefc = c.I[I_NEFC];
+  const bool jreg = DX_SWEEP && nv <= 30 && nefc <= 2 * DX_WAVE;
+  const int lane = LANE;
+  float Jd[2][30];
+#pragma unroll
+  for (int d = 0; d < 30; d++) Jd[0][d] = Jd[1][d] = 0.f;
+  if (jreg) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int r = lane + DX_WAVE * h;
+      if (DX_WAVE * h < nefc)
+        pgs_row_nz(c, r < nefc ? r : -1, [&](int e, float v) {  // (v = 0 from lanes without a nonzero here)
+#pragma unroll
+          for (int d = 0; d < 30; d++) Jd[h][d] = d == e ? Jd[h][d] + v : Jd[h][d];
+        });
+    }
+  }
+  auto jdir = [&](const float* x, float* out) {  // out[r] = J_r x
+    float xs[30];
+#pragma unroll
+    for (int d = 0; d < 30; d++) xs[d] = x[min(d, nv - 1)];  // (uniform addresses: broadcast reads)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (DX_WAVE * h < nefc) {
+        float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+        for (int d = 0; d < 30; d += 2) {
+          s0 = fmaf(Jd[h][d], d < nv ? xs[d] : 0.f, s0);
+          s1 = fmaf(Jd[h][d + 1], d + 1 < nv ? xs[d + 1] : 0.f, s1);
+        }
+        const int r = lane + DX_WAVE * h;
+        if (r < nefc) out[r] = s0 + s1;
+      }
+    }
+    SYNC();
+  };
+  const int* meta = (const int*)c.f(c.L.efc_meta);
+  const float* Dp = c.f(c.L.efc_D);
+  const float* flp = c.f(c.L.efc_fl);
+  const float* Rfp = c.f(c.L.efc_Rf);
+  auto jtf = [&](float* out) {  // out = J'f, f the rows' forces at jar
+    float t[32];
+#pragma unroll
+    for (int d = 0; d < 32; d++) t[d] = 0.f;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (DX_WAVE * h < nefc) {
+        const int r = lane + DX_WAVE * h, rc = min(r, nefc - 1);
+        const bool fr = r < c.nfric;
+        float f, hw;
+        row_cost(meta[rc] & 15, Dp[rc], fr ? flp[rc] : 0.f, fr ? Rfp[rc] : 0.f, jar[rc], f, hw);
+        f = r < nefc ? f : 0.f;
+#pragma unroll
+        for (int d = 0; d < 30; d++) t[d] = fmaf(f, Jd[h][d], t[d]);
+      }
+    }
+    const float w = wave_reduce_scatter32(t);  // component LANE >> 1
+    const float wd = __int_as_float(__builtin_amdgcn_ds_bpermute(8 * (lane & 31), __float_as_int(w)));
+    if (lane < nv) out[lane] = wd;
+    SYNC();
+  };
   int it = 0;
-  jac_t_force(c, grad);  // grad <- J^T f
+  if (jreg) jtf(grad);
+  else jac_t_force(c, grad);  // grad <- J^T f
   for (int i = LANE; i < nv; i += DX_WAVE) grad[i] = Ma[i] - qs[i] - grad[i];
   SYNC();
   minv();
@@ -2510,7 +2749,14 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
     stage_count(c, CNT_NEWTON_IT);
     int changed = 0;
     float g0 = 0.f;
-    const float alpha = line_search<false, true>(c, qacc, Ma, dir, &changed, &g0);
+    float alpha;
+    if (jreg) {
+      jdir(dir, c.f(c.L.efc_jv));
+      stage_mark(c, ST_JACVEC);
+      alpha = line_search<false, true, false, true>(c, qacc, Ma, dir, &changed, &g0);
+    } else {
+      alpha = line_search<false, true>(c, qacc, Ma, dir, &changed, &g0);
+    }
     stage_mark(c, ST_NEWTON_LS);
     if (alpha == 0.f) break;
     const float* jvd = c.f(c.L.efc_jv);
@@ -2524,7 +2770,8 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
     // the decrease along the line, -alpha g0 / 2 (exact for a quadratic segment): the
     // difference of two fp32 costs drowns in rounding long before CG's slow tail ends
     const float impr = -0.5f * scale * alpha * g0;
-    jac_t_force(c, grad);
+    if (jreg) jtf(grad);
+    else jac_t_force(c, grad);
     float gn = 0;
     for (int i = LANE; i < nv; i += DX_WAVE) {
       grad[i] = Ma[i] - qs[i] - grad[i];
@@ -3138,7 +3385,8 @@ __device__ __forceinline__ void solve(const Ctx& c) {
   stage_count(c, CNT_SOLVE);
   stage_count(c, CNT_NEFC, nefc);
   if (c.solver == 1) {
-    solve_cg(c, scale, tol);
+    if (DX_SWEEP && nv <= 30 && nefc <= 2 * DX_WAVE) solve_cg_reg(c, scale, tol);
+    else solve_cg(c, scale, tol);
     return;
   }
   float wo[DX_NCH][5] = {};

@@ -48,8 +48,3 @@ def main(path, e, g1, g2, asset="shadow_reorient.npz"):
 if __name__ == "__main__":
     a = sys.argv[1:]
     main(a[0], int(a[1]), int(a[2]), int(a[3]), *(a[4:5]))
-
-
-if __name__ == "__main__":
-    a = sys.argv[1:]
-    main(a[0], int(a[1]), int(a[2]), int(a[3]), *(a[4:5]))
