@@ -47,7 +47,9 @@ STAGES = ("kinematics", "crb", "broadphase", "midphase", "narrowphase", "constra
 COUNTERS = {20: "plane_box", 21: "plane_convex", 22: "capsule", 23: "mpr", 24: "mpr_support", 25: "mpr_hit",
             26: "mpr_maxit", 27: "newton_iter", 28: "linesearch_iter", 29: "solves", 30: "nefc",
             31: "np_trips", 32: "broad_keep", 33: "mid_pairs", 34: "mid_keep", 35: "queue_wait"}
-NSTAGE = 40
+NSTAGE = 48
+# the narrowphase trip's parts (DX_NP_MARKS builds only)
+NP_STAGES = {36: "np_loop", 37: "np_fresh", 38: "np_supload", 39: "np_supred", 40: "np_portal"}
 OUT_OBS, OUT_REWARD, OUT_DISCOUNT, OUT_STEP_TYPE, OUT_GOAL, OUT_SUCCESSES, OUT_GOAL_FAILURES, OUT_GOAL_QPOS = range(8)
 TASK_REORIENT, TASK_REACH, TASK_HANDOVER = 0, 1, 2
 REACH_NPARAMS_HEAD = 26

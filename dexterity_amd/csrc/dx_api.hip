@@ -120,22 +120,23 @@ static void quat2mat_h(float* R, const float* q) {
 // ------------------------------------------------------------------------ //
 // direction-binned hulls (support-point acceleration, exact)
 // ------------------------------------------------------------------------ //
-// A hull with more than 16 vertices gets a cube map of n x n cells per face over the
-// local direction sphere (cell rule: dx_step.hip hull_cell).  Each cell lists the
-// vertices that can be a support point for some direction in the cell, sorted by
+// A hull with more than DX_HULL_K (8) vertices gets a cube map of n x n cells per face
+// over the local direction sphere (cell rule: dx_step.hip hull_cell).  Each cell lists
+// the vertices that can be a support point for some direction in the cell, sorted by
 // vertex index.  A vertex is dropped only if a single other vertex beats it by more
 // than 1e-5 R at all four corner directions of the (slightly enlarged) cell, hence at
 // every direction of the cell: every maximiser -- ties included -- of every direction
 // in the cell is kept, and the lowest-index maximiser over the cell's list is the
 // vertex the full scan returns (the oracle's rule).
-// Layout: one 16-slot block per cell (x, y, z, vertex index; index -1 pads), so the
-// device reads a cell with one memory round trip of two 16-B loads per lane.  A cell
-// with more than 16 candidates (the faces of a hull with many coplanar vertices: all
-// of them tie along the face normal) keeps candidates 0..14 in its block and a header
-// in slot 15 = (overflow offset in float4s from the hull's first cell, candidate
-// count, 0, index -2); candidates 15.. follow in the hull's overflow run, padded to a
-// multiple of 16.  n is the smallest of 1, 2, 3, 4, 6, 8 with at most 2 % of the
-// cells overflowing.
+// Layout: one DX_HULL_K-slot block per cell (x, y, z, vertex index; index -1 pads) -- one
+// 128-B line, read by a lane group in one memory round trip of one or two 16-B loads per
+// lane.  A cell with more than K candidates (the faces of a hull with many coplanar
+// vertices: all of them tie along the face normal) keeps candidates 0..K-2 in its block
+// and a header in slot K-1 = (overflow offset in float4s from the hull's first cell,
+// candidate count, 0, index -2); candidates K-1.. follow in the hull's overflow run,
+// padded to a multiple of K.  n is the smallest of 1, 2, 3, 4, 6, 8, 10, 12 with at most
+// 2 % of the cells overflowing.  (Round 6: 8-slot cells on finer maps instead of 16-slot
+// cells -- half the loads and candidate tests per support, one line per cell.)
 static void cell_corners(int face, int n, int iu, int iv, double eps, double c[4][3]) {
   int ax = face >> 1;
   double sgn = (face & 1) ? -1.0 : 1.0;
@@ -183,12 +184,13 @@ static void build_hull_bins(dx_model* m) {
   int nmesh = (int)num.size();
   std::vector<int> bn(std::max(nmesh, 1), 0), bcap(std::max(nmesh, 1), 0), badr(std::max(nmesh, 1), 0);
   std::vector<float> b4;
-  static const int kN[] = {1, 2, 3, 4, 6, 8};
+  static const int kN[] = {1, 2, 3, 4, 6, 8, 10, 12};
+  constexpr int K = DX_HULL_K;
   const char* env_minn = getenv("DX_HULL_BIN_MINN");  // (experiments: finer cube maps)
   const int minn = env_minn ? atoi(env_minn) : 1;
   for (int i = 0; i < nmesh; i++) {
     int nv = num[i];
-    if (nv <= 16) continue;
+    if (nv <= K) continue;
     std::vector<double> V(3 * nv);
     double R = 0;
     for (int j = 0; j < nv; j++) {
@@ -198,7 +200,7 @@ static void build_hull_bins(dx_model* m) {
     std::vector<std::vector<int>> cells;
     int n = 0;
     for (int nn : kN) {
-      if (nn < minn && nn != kN[5]) continue;
+      if (nn < minn && nn != kN[7]) continue;
       cells.assign(6 * nn * nn, {});
       int over = 0;
       for (int f = 0; f < 6; f++)
@@ -208,14 +210,14 @@ static void build_hull_bins(dx_model* m) {
             cell_corners(f, nn, iu, iv, 1e-3, c);
             auto& L = cells[(f * nn + iu) * nn + iv];
             hull_cell_candidates(V, nv, R, c, L);
-            over += L.size() > 16;
+            over += L.size() > K;
           }
       n = nn;
       if (over <= 0.02 * (double)cells.size()) break;
     }
     const size_t base = b4.size() / 4;  // this hull's first cell, in float4s
     const size_t ncell = cells.size();
-    b4.resize(4 * (base + 16 * ncell), 0.f);
+    b4.resize(4 * (base + K * ncell), 0.f);
     auto put = [&](size_t slot, int idx) {
       float* e = b4.data() + 4 * slot;
       for (int k = 0; k < 3; k++) e[k] = idx >= 0 ? mv[3 * (adr[i] + idx) + k] : 0.f;
@@ -223,17 +225,17 @@ static void build_hull_bins(dx_model* m) {
     };
     for (size_t cidx = 0; cidx < ncell; cidx++) {
       const auto& L = cells[cidx];
-      const size_t blk = base + 16 * cidx;
-      if (L.size() <= 16) {
-        for (int s = 0; s < 16; s++) put(blk + s, s < (int)L.size() ? L[s] : -1);
+      const size_t blk = base + K * cidx;
+      if (L.size() <= (size_t)K) {
+        for (int s = 0; s < K; s++) put(blk + s, s < (int)L.size() ? L[s] : -1);
         continue;
       }
-      for (int s = 0; s < 15; s++) put(blk + s, L[s]);
-      const size_t ov = b4.size() / 4;  // overflow run: candidates 15.., padded to 16
-      const int nov = (int)L.size() - 15;
-      b4.resize(4 * (ov + (size_t)(nov + 15) / 16 * 16), 0.f);
-      for (int s = 0; s < (nov + 15) / 16 * 16; s++) put(ov + s, s < nov ? L[15 + s] : -1);
-      float* h = b4.data() + 4 * (blk + 15);
+      for (int s = 0; s < K - 1; s++) put(blk + s, L[s]);
+      const size_t ov = b4.size() / 4;  // overflow run: candidates K-1.., padded to K
+      const int nov = (int)L.size() - (K - 1);
+      b4.resize(4 * (ov + (size_t)(nov + K - 1) / K * K), 0.f);
+      for (int s = 0; s < (nov + K - 1) / K * K; s++) put(ov + s, s < nov ? L[K - 1 + s] : -1);
+      float* h = b4.data() + 4 * (blk + K - 1);
       const int off = (int)(ov - base), cnt = (int)L.size(), tag = -2;
       memcpy(h, &off, 4);
       memcpy(h + 1, &cnt, 4);
@@ -241,7 +243,7 @@ static void build_hull_bins(dx_model* m) {
       memcpy(h + 3, &tag, 4);
     }
     bn[i] = n;
-    bcap[i] = 16;
+    bcap[i] = K;
     badr[i] = (int)base;
   }
   if (b4.empty()) b4.assign(4, 0.f);
@@ -789,14 +791,15 @@ extern "C" int dx_hull_support(const dx_model* m, int32_t mesh, const float dir[
     }
   }
   if (cell >= 0) {
-    // the cell's block, then its overflow run when slot 15 is a header
-    const float* blk = b4 + 4 * (size_t)cell * 16;
+    // the cell's block, then its overflow run when slot K - 1 is a header
+    const int K = cap;
+    const float* blk = b4 + 4 * (size_t)cell * K;
     int hdr;
-    memcpy(&hdr, blk + 4 * 15 + 3, 4);
-    int off = 0, cnt = 16;
-    if (hdr == -2) { memcpy(&off, blk + 4 * 15, 4); memcpy(&cnt, blk + 4 * 15 + 1, 4); }
+    memcpy(&hdr, blk + 4 * (K - 1) + 3, 4);
+    int off = 0, cnt = K;
+    if (hdr == -2) { memcpy(&off, blk + 4 * (K - 1), 4); memcpy(&cnt, blk + 4 * (K - 1) + 1, 4); }
     for (int s = 0; s < cnt; s++) {
-      const float* e = hdr == -2 && s >= 15 ? b4 + 4 * ((size_t)off + s - 15) : blk + 4 * s;
+      const float* e = hdr == -2 && s >= K - 1 ? b4 + 4 * ((size_t)off + s - (K - 1)) : blk + 4 * s;
       int idx;
       memcpy(&idx, e + 3, 4);
       if (idx < 0) continue;

@@ -258,7 +258,11 @@ enum {
   CNT_PLANE_BOX = 20, CNT_PLANE_CONVEX, CNT_CAPSULE, CNT_MPR, CNT_SUPPORT, CNT_MPR_HIT,
   CNT_MPR_MAXIT, CNT_NEWTON_IT, CNT_LS_IT, CNT_SOLVE, CNT_NEFC, CNT_NP_TRIPS, CNT_BROAD_KEEP, CNT_MID_PAIRS,
   CNT_MID_KEEP,  // event counters, not cycles
-  CNT_QWAIT      // substep queue: cycles a claimed task waited for the env's previous physics step
+  CNT_QWAIT,     // substep queue: cycles a claimed task waited for the env's previous physics step
+  // the narrowphase loop's trips split (DX_NP_MARKS builds only, dx_step.hip NpClock): loop
+  // bookkeeping and contact writes, new pairs' set-up, a support's cell load up to its
+  // first use, the support's reductions and world transform, the portal arithmetic
+  ST_NP_LOOP = 36, ST_NP_FRESH, ST_NP_SUPLOAD, ST_NP_SUPRED, ST_NP_PORTAL
 };
 // The accumulators are this env's own global slots, updated by no-return atomics: a
 // read-modify-write would put a memory round trip on the wave's path at every mark
@@ -276,6 +280,9 @@ __device__ __forceinline__ void stage_mark(const Ctx& c, int k) {
     *last = t;
   }
 }
+#ifndef DX_NP_MARKS
+#define DX_NP_MARKS 0
+#endif
 template <class Ctx>
 __device__ __forceinline__ void stage_count(const Ctx& c, int k, int n = 1) {
   if (c.stage_acc && LANE == 0) stage_add(c.stage_acc + k, (unsigned long long)n);

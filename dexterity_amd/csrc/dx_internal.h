@@ -98,7 +98,7 @@ struct DevModel {
   const DXG int *mesh_vertadr, *mesh_vertnum;
   const DXG float4* mesh_vert4;  // hull vertices padded to (x, y, z, 0)
   // direction-binned hulls (dx_api.hip build_hull_bins): cube map of binn x binn cells
-  // per face, bincap float4 (x, y, z, vertex index bits; -1 = padding) per cell
+  // per face, bincap = DX_HULL_K float4 (x, y, z, vertex index bits; -1 = padding) per cell
   const DXG int *mesh_binn, *mesh_bincap, *mesh_binadr;
   const DXG float4* mesh_bin4;
   // narrowphase setup records: geom_rec [ngeom][8] float4 = {type, body, nvert, bin_n,
@@ -223,7 +223,10 @@ struct DevBatch {
 #define DX_HEALTH_WORDS 16
 #define DX_NCON_HIST 65   // bins 0..63, and >= 64
 #define DX_MAXVAL 1e10f   // mjMAXVAL: |qacc| beyond this is a diverged state (mj_checkAcc)
-#define DX_NSTAGE 40
+#define DX_NSTAGE 48
+// slots of a hull's support block: a cube-map cell (one 128-B line), or the first
+// vertices of a hull scanned whole; a hull with more vertices is binned
+#define DX_HULL_K 8
 
 // Offsets (in 4-byte words) of every per-env LDS array.
 struct Lds {

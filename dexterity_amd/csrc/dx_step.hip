@@ -312,10 +312,10 @@ __device__ __forceinline__ int hull_cell(const float* ld, int n) {
   int face = 2 * ax + (a < 0 ? 1 : 0);
   return (face * n + iu) * n + iv;
 }
-// One hull's support scan by a lane group.  First a 16-slot block -- the direction's
-// cube-map cell (dx_api.hip build_hull_bins), or the first 16 vertices of a hull that
-// is not binned / a zero direction -- two 16-B loads per lane, one memory round trip;
-// then, rarely, an overflow run: the rest of a cell whose slot 15 is a header, or the
+// One hull's support scan by a lane group.  First a DX_HULL_K-slot block -- the
+// direction's cube-map cell (dx_api.hip build_hull_bins), or the first K vertices of a
+// hull that is not binned / a zero direction -- one 128-B line, one memory round trip;
+// then, rarely, an overflow run: the rest of a cell whose slot K - 1 is a header, or the
 // rest of a whole-hull scan.
 struct HullScan {
   HullBest h;
@@ -325,28 +325,28 @@ struct HullScan {
 };
 __device__ __forceinline__ void hull_block(const Shape& s, const float* ld, const DXG float4*& blk, int& n1, bool& cell) {
   blk = s.vert4;
-  n1 = min(s.nvert, 16);
+  n1 = min(s.nvert, DX_HULL_K);
   cell = false;
   if (s.bin_n > 0) {
     int c = hull_cell(ld, s.bin_n);
     if (c >= 0) {
-      blk = s.bin4 + 16 * c;
-      n1 = 16;
+      blk = s.bin4 + DX_HULL_K * c;
+      n1 = DX_HULL_K;
       cell = true;
     }
   }
 }
 template <int NPG>
-__device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[16 / NPG],
+__device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[DX_HULL_K / NPG],
                                                 const DXG float4* blk, int n1, bool cell, HullScan& H) {
-  constexpr int DX_SLK = 16 / NPG;  // block slots per lane
+  constexpr int DX_SLK = DX_HULL_K / NPG;  // block slots per lane
 #pragma unroll
   for (int u = 0; u < DX_SLK; u++) {
     const int sl = u * NPG + SL;
     const int idx = cell ? __float_as_int(v[u].w) : sl;
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < n1 && idx >= 0);
   }
-  // slot 15 (the group's last lane, last load) of a cell: a header (index -2) names
+  // slot K - 1 (the group's last lane, last load) of a cell: a header (index -2) names
   // the overflow run.  The header is rare: the lanes that hold one are found by ballot
   // and only then is it broadcast to its group.
   H.cell = cell;
@@ -360,42 +360,56 @@ __device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld,
     const int cnt = __shfl(__float_as_int(v[DX_SLK - 1].y), src, 64);
     if (cell && tag == -2) {
       H.ov = s.bin4 + off;
-      H.nov = cnt - 15;
+      H.nov = cnt - (DX_HULL_K - 1);
     }
   }
-  if (!cell && s.nvert > 16) {
-    H.ov = s.vert4 + 16;
-    H.nov = s.nvert - 16;
+  if (!cell && s.nvert > DX_HULL_K) {
+    H.ov = s.vert4 + DX_HULL_K;
+    H.nov = s.nvert - DX_HULL_K;
   }
 }
 template <int NPG>
-__device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)[16 / NPG], int base, HullScan& H) {
+__device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)[DX_HULL_K / NPG], int base, HullScan& H) {
 #pragma unroll
-  for (int u = 0; u < 16 / NPG; u++) {
+  for (int u = 0; u < DX_HULL_K / NPG; u++) {
     const int sl = base + u * NPG + SL;
-    const int idx = H.cell ? __float_as_int(v[u].w) : 16 + sl;
+    const int idx = H.cell ? __float_as_int(v[u].w) : DX_HULL_K + sl;
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < H.nov && idx >= 0);
   }
 }
 
 // Support points of A along dir and of B along -dir, by one lane group split in halves:
 // lanes 0-3 of a group hold A (the pair's first geom) in their Shape and scan its hull
-// block along dir, lanes 4-7 hold B and scan along -dir, four slots each; the halves swap
+// block along dir, lanes 4-7 hold B and scan along -dir, two slots each; the halves swap
 // their world points at the end (DPP row_half_mirror: lane i <-> 7 - i).  Every lane
 // computes one cube-map cell, one local direction, one reduction (over its quad: two DPP
 // steps) and one world transform, and keeps one Shape.  The vertex arithmetic and the
 // first-maximiser rule are those of the oracle's serial scan.
-// (NPG = 4: two lanes per half, eight slots each, halves swapped by quad_perm [2,3,0,1])
+// (NPG = 4: two lanes per half, four slots each, halves swapped by quad_perm [2,3,0,1])
 template <int NPG> __device__ __forceinline__ bool half_b() { return (SL & (NPG / 2)) != 0; }  // this lane holds B
 // the other half's value: lane i <-> 7 - i (NPG 8) or i ^ 2 (NPG 4)
 template <int NPG> __device__ __forceinline__ float half_swap(float v) {
   static_assert(NPG == 8 || NPG == 4, "groups of 8 or 4 lanes");
   return NPG == 8 ? dpp_f<0x141, 0xF>(v) : dpp_f<0x4E, 0xF>(v);
 }
+// the narrowphase trip's clock (DX_NP_MARKS builds): stage_mark from divergent code, the first active lane keeping the time
+struct NpClock {
+  unsigned long long* acc;
+  int* I;
+  __device__ void mark(int k) const {
+    if (DX_NP_MARKS && acc && LANE == __builtin_amdgcn_readfirstlane(LANE)) {
+      unsigned long long t = __builtin_amdgcn_s_memtime();
+      unsigned long long* last = (unsigned long long*)(I + 10);
+      stage_add(acc + k, t - *last);
+      *last = t;
+    }
+  }
+};
 template <int NPG>
-__device__ __forceinline__ void support_pair(const Shape& S, const float* dir, float* outA, float* outB) {
+__device__ __forceinline__ void support_pair(const Shape& S, const float* dir, float* outA, float* outB,
+                                             const NpClock& ck = NpClock{nullptr, nullptr}) {
   constexpr int H = NPG / 2;          // lanes per half
-  constexpr int DX_SLH = 16 / H;      // block slots per lane of a half group
+  constexpr int DX_SLH = DX_HULL_K / H;  // block slots per lane of a half group
   const bool hb = half_b<NPG>();
   const int q = SL & (H - 1);
   const float sg = hb ? -1.f : 1.f;
@@ -418,13 +432,39 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
       const int sl = H * u + q;
       v[u] = blk[sl < n1 ? sl : 0];
     }
+    // the lane's first maximiser among its slots (a lane's slots are in vertex-index
+    // order): every dot at once, a max tree, then the selects from the last slot down --
+    // not a chain of DX_SLH dependent compare-and-keep steps
+    {
+      float dd[DX_SLH];
+      int ix[DX_SLH];
 #pragma unroll
-    for (int u = 0; u < DX_SLH; u++) {
-      const int sl = H * u + q;
-      const int idx = cell ? __float_as_int(v[u].w) : sl;
-      hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, mesh && sl < n1 && idx >= 0);
+      for (int u = 0; u < DX_SLH; u++) {
+        const int sl = H * u + q;
+        const int idx = cell ? __float_as_int(v[u].w) : sl;
+        const bool ok = mesh && sl < n1 && idx >= 0;
+        dd[u] = ok ? v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2] : -3.0e38f;
+        ix[u] = ok ? idx : 0x7fffffff;
+      }
+      float m = dd[0];
+#pragma unroll
+      for (int u = 1; u < DX_SLH; u++) m = fmaxf(m, dd[u]);
+      h.d = m;
+      h.i = ix[DX_SLH - 1];
+      h.x = v[DX_SLH - 1].x;
+      h.y = v[DX_SLH - 1].y;
+      h.z = v[DX_SLH - 1].z;
+#pragma unroll
+      for (int u = DX_SLH - 2; u >= 0; u--) {
+        const bool t = dd[u] == m;
+        h.i = t ? ix[u] : h.i;
+        h.x = t ? v[u].x : h.x;
+        h.y = t ? v[u].y : h.y;
+        h.z = t ? v[u].z : h.z;
+      }
     }
-    // overflow run: slot 15 of a cell (its quad's last lane, last load) may be a header
+    ck.mark(ST_NP_SUPLOAD);
+    // overflow run: slot K - 1 of a cell (its half's last lane, last load) may be a header
     const DXG float4* ov = blk;
     int nov = 0;
     const bool hdr = mesh && cell && q == H - 1 && __float_as_int(v[DX_SLH - 1].w) == -2;
@@ -435,14 +475,14 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
       const int cnt = __shfl(__float_as_int(v[DX_SLH - 1].y), src, 64);
       if (mesh && cell && tag == -2) {
         ov = s.bin4 + off;
-        nov = cnt - 15;
+        nov = cnt - (DX_HULL_K - 1);
       }
     }
-    if (mesh && !cell && s.nvert > 16) {
-      ov = s.vert4 + 16;
-      nov = s.nvert - 16;
+    if (mesh && !cell && s.nvert > DX_HULL_K) {
+      ov = s.vert4 + DX_HULL_K;
+      nov = s.nvert - DX_HULL_K;
     }
-    for (int base = 0; __any(base < nov); base += 16) {
+    for (int base = 0; __any(base < nov); base += DX_HULL_K) {
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
         const int sl = base + H * u + q;
@@ -451,7 +491,7 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
         const int sl = base + H * u + q;
-        const int idx = cell ? __float_as_int(v[u].w) : 16 + sl;
+        const int idx = cell ? __float_as_int(v[u].w) : DX_HULL_K + sl;
         hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < nov && idx >= 0);
       }
     }
@@ -489,7 +529,7 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
 // Support of one shape along dir (group-cooperative for hulls).
 template <int NPG>
 __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, float* out) {
-  constexpr int DX_SLK = 16 / NPG;
+  constexpr int DX_SLK = DX_HULL_K / NPG;
   float ld[3], lp[3];
   mattvec3(ld, s.mat, dir);
   if (s.type == DXG_MESH) {
@@ -506,7 +546,7 @@ __device__ __forceinline__ void support_grp(const Shape& s, const float* dir, fl
       v[u] = blk[sl < n1 ? sl : 0];
     }
     hull_take_block<NPG>(s, ld, v, blk, n1, cell, S);
-    for (int base = 0; __any(base < S.nov); base += 16) {
+    for (int base = 0; __any(base < S.nov); base += DX_HULL_K) {
 #pragma unroll
       for (int u = 0; u < DX_SLK; u++) {
         const int sl = base + u * NPG + SL;
@@ -599,7 +639,7 @@ __device__ __forceinline__ void mpr_init(const Shape& G, MprState& S, const floa
 // degenerate and final exits branch.
 template <int NPG>
 __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& depth, float* normal,
-                                        float* pos, NpStats& st) {
+                                        float* pos, NpStats& st, const NpClock& ck = NpClock{nullptr, nullptr}) {
   const float tol = 1e-6f;
   const int maxit = 50;
   float* P = S.P;
@@ -607,7 +647,8 @@ __device__ __forceinline__ int mpr_step(const Shape& G, MprState& S, float& dept
   for (int k = 0; k < 3; k++) { v0[k] = P[k]; v1[k] = P[9 + k]; v2[k] = P[18 + k]; v3[k] = P[27 + k]; }
   MPoint p;
   float* dir = S.dir;
-  support_pair<NPG>(G, dir, p.a, p.b);
+  support_pair<NPG>(G, dir, p.a, p.b, ck);
+  ck.mark(ST_NP_SUPRED);
   sub3(p.v, p.a, p.b);
   st.support++;
   const int ph = S.phase;
@@ -945,10 +986,12 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
     bool cached = false;
     int trips = 0;
     M.P = c.f(c.L.cand + c.L.cand_max) + MP_WORDS * grp;  // free during collision (dx_api.hip layout)
+    const NpClock ck{c.stage_acc, c.I};
     for (;;) {
       bool act = q < ng;
       if (__ballot(act) == 0) break;
       trips++;
+      ck.mark(ST_NP_LOOP);
 
       NpOut o;
       o.wr = false;
@@ -975,9 +1018,11 @@ __device__ __forceinline__ int narrow_pass(const Ctx& c, int ng, const int* gcan
             stepping = true;
           }
         }
+        ck.mark(ST_NP_FRESH);
         if (stepping) {
           float depth, nrm[3], pos[3];
-          int r = mpr_step<NPG>(G, M, depth, nrm, pos, st);
+          int r = mpr_step<NPG>(G, M, depth, nrm, pos, st, ck);
+          ck.mark(ST_NP_PORTAL);
           if (r && c.sep && SL == 0) {
             // remember a separating direction (unless it is the cached one, still
             // separating: phase -1); forget it once the pair touches.  Plain stores: an

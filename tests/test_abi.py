@@ -98,7 +98,7 @@ def test_binned_hull_support_matches_full_scan(lib, asset):
     d = (ctypes.c_float * 3)()
     rng = np.random.RandomState(7)
     checked = binned = 0
-    for mesh in np.nonzero(nvert > 64)[0]:
+    for mesh in np.nonzero(nvert > 8)[0]:
         vv = V[adr[mesh]: adr[mesh] + nvert[mesh]]
         R = np.linalg.norm(vv, axis=1).max()
         dirs = rng.randn(400, 3).astype(np.float32)
@@ -107,9 +107,8 @@ def test_binned_hull_support_matches_full_scan(lib, asset):
         for dv in dirs:
             d[:] = dv
             assert lib.dx_hull_support(model.ptr, int(mesh), d, info) == 0
-            # not binned (a hull whose cells need > 64 slots, e.g. a face with > 64
-            # coplanar vertices): the device scans the whole hull
-            assert (info[1] > 0 and 0 < info[2] <= 64 and info[2] % 16 == 0) or info[1] == info[2] == 0
+            # every hull with more than DX_HULL_K = 8 vertices is binned, 8 slots per cell
+            assert info[1] > 0 and info[2] == 8
             binned += info[1] > 0
             dots = vv @ dv.astype(np.float64)
             ref = int(np.argmax(dots))
@@ -117,5 +116,4 @@ def test_binned_hull_support_matches_full_scan(lib, asset):
             assert info[0] == ref or tie, (mesh, dv)
             checked += 1
     assert checked > 0
-    if asset == "shadow_reorient":
-        assert binned == checked  # every large Shadow hull is binned
+    assert binned == checked

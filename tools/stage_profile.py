@@ -45,6 +45,11 @@ print(f"B={B} steps={steps}: {dt/steps*1e3:.2f} ms/step; total cycles per env-su
 for k, name in enumerate(_lib.STAGES):
     print(f"  {name:20s} {100*cyc[k]/tot:6.2f}%  {per[k]:12.0f} cyc/env-substep")
     out[name] = per[k]
+np_parts = {name: per_env[:, k].sum() / (B * steps * 5) for k, name in _lib.NP_STAGES.items()}
+if sum(np_parts.values()) > 0:  # a DX_NP_MARKS build: the narrowphase trip split
+    trips = cnt["np_trips"]
+    print("narrowphase trip split (cycles per env-substep, per trip):",
+          ", ".join(f"{n} {v:.0f} ({v / max(trips, 1e-9):.0f})" for n, v in np_parts.items()))
 print("narrowphase calls per env-substep", {k: round(v, 3) for k, v in cnt.items()})
 # the heaviest environments bound the launch (longest-first dispatch): their stages
 stage_cols = [k for k in range(len(_lib.STAGES))]
