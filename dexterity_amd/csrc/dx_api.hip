@@ -364,10 +364,16 @@ extern "C" dx_model* dx_model_load(const void* blob, size_t nbytes) {
   mats("geom_quat", "geom_mat", d.ngeom);
   mats("site_quat", "site_mat", d.nsite);
   {
+    // (x, y, z, the vertex's index in its mesh as int bits): a whole-hull scan reads the
+    // index from the slot as a cell scan does, so every support load is one 16-B load
     auto& mv = m->hf["mesh_vert"];
     std::vector<float> v4(4 * std::max<size_t>(mv.size() / 3, 1), 0.f);
     for (size_t i = 0; i < mv.size() / 3; i++)
       for (int k = 0; k < 3; k++) v4[4 * i + k] = mv[3 * i + k];
+    auto& vadr = m->hi["mesh_vertadr"];
+    auto& vnum = m->hi["mesh_vertnum"];
+    for (size_t g = 0; g < vnum.size(); g++)
+      for (int j = 0; j < vnum[g]; j++) memcpy(&v4[4 * ((size_t)vadr[g] + j) + 3], &j, 4);
     m->hf["mesh_vert4"] = v4;
   }
   build_hull_bins(m);

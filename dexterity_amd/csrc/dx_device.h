@@ -26,15 +26,29 @@ __device__ __forceinline__ int lane_id() {
 // wave helpers
 // ------------------------------------------------------------------------ //
 // DPP row reductions (gfx9 family): quad_perm, row_half_mirror, row_mirror, then
-// row_bcast15 / row_bcast31 carry the partial results up to lane 63.
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_f(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK, 0xF, false));
-}
+// row_bcast15 / row_bcast31 carry the partial results up to lane 63.  With every row
+// enabled (the in-row patterns, where each lane's source exists) the move has no "old"
+// operand (mov_dpp, bound_ctrl): the compiler then folds it into the consuming add /
+// integer min / max / or as one v_*_dpp instruction -- with update_dpp(old = x) every
+// step was a copy, the DPP move and the operation.  The masked broadcasts keep x in the
+// rows they skip.
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ int dpp_i(int x) {
+  if (ROWMASK == 0xF) return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);
   return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xF, false);
 }
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(dpp_i<CTRL, ROWMASK>(__float_as_int(x)));
+}
+// fp32 <-> a signed integer of the same order (for max / min reductions on the integer
+// DPP path: fmaxf on a DPP operand also re-canonicalises it, two more instructions per
+// step).  Finite values and infinities only; an involution.
+__device__ __forceinline__ int f2ord(float f) {
+  const int b = __float_as_int(f + 0.0f);  // (-0 -> +0: the two compare equal as floats)
+  return b ^ ((b >> 31) & 0x7fffffff);
+}
+__device__ __forceinline__ float ord2f(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
 // Sums: quad, half-row, row sums by DPP, then rows carried up to lane 63 (each lane
 // contributes exactly once), broadcast with readlane.
 __device__ __forceinline__ float wave_sum(float v) {
@@ -55,15 +69,16 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   v += dpp_i<0x143, 0xC>(v);
   return __builtin_amdgcn_readlane(v, 63);
 }
-__device__ __forceinline__ float wave_max_f(float m) {
-  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));
-  m = fmaxf(m, dpp_f<0x4E, 0xF>(m));
-  m = fmaxf(m, dpp_f<0x141, 0xF>(m));
-  m = fmaxf(m, dpp_f<0x140, 0xF>(m));
-  m = fmaxf(m, dpp_f<0x142, 0xA>(m));
-  m = fmaxf(m, dpp_f<0x143, 0xC>(m));
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 63));
+__device__ __forceinline__ int wave_max_i(int m) {
+  m = max(m, dpp_i<0xB1, 0xF>(m));
+  m = max(m, dpp_i<0x4E, 0xF>(m));
+  m = max(m, dpp_i<0x141, 0xF>(m));
+  m = max(m, dpp_i<0x140, 0xF>(m));
+  m = max(m, dpp_i<0x142, 0xA>(m));
+  m = max(m, dpp_i<0x143, 0xC>(m));
+  return __builtin_amdgcn_readlane(m, 63);
 }
+__device__ __forceinline__ float wave_max_f(float m) { return ord2f(wave_max_i(f2ord(m))); }
 __device__ __forceinline__ int wave_min_i(int m) {
   m = min(m, dpp_i<0xB1, 0xF>(m));
   m = min(m, dpp_i<0x4E, 0xF>(m));
@@ -84,6 +99,7 @@ __device__ __forceinline__ int wave_argmax_first(float best, int bi) {
 // row totals upwards.  No LDS round trip.
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ int dpp_i0(int x) {  // lanes without a source read 0
+  if (ROWMASK == 0xF) return __builtin_amdgcn_mov_dpp(x, CTRL, 0xF, 0xF, true);  // (bound_ctrl: 0)
   return __builtin_amdgcn_update_dpp(0, x, CTRL, ROWMASK, 0xF, false);
 }
 __device__ __forceinline__ int wave_incl_scan(int x) {

@@ -96,7 +96,7 @@ struct DevModel {
   const DXG int *geom_type, *geom_bodyid, *geom_dataid;
   const DXG float *geom_size, *geom_pos, *geom_mat, *geom_center, *geom_bsphere, *geom_bsphere_b, *geom_obb_b;
   const DXG int *mesh_vertadr, *mesh_vertnum;
-  const DXG float4* mesh_vert4;  // hull vertices padded to (x, y, z, 0)
+  const DXG float4* mesh_vert4;  // hull vertices (x, y, z, index in the mesh as int bits)
   // direction-binned hulls (dx_api.hip build_hull_bins): cube map of binn x binn cells
   // per face, bincap = DX_HULL_K float4 (x, y, z, vertex index bits; -1 = padding) per cell
   const DXG int *mesh_binn, *mesh_bincap, *mesh_binadr;

@@ -38,7 +38,7 @@ struct Shape {
   int type, nvert;
   int bin_n, bin_cap;  // direction-binned hull (bin_n > 0), see dx_api.hip build_hull_bins
   float pos[3], mat[9], size[3], center[3], margin;
-  const DXG float4* vert4;  // hull vertices (x, y, z, 0) in global memory (L2-resident)
+  const DXG float4* vert4;  // hull vertices (x, y, z, index) in global memory (L2-resident)
   const DXG float4* bin4;   // this hull's cells
 };
 
@@ -227,11 +227,19 @@ template <int NPG> __device__ __forceinline__ int gbase_() { return LANE & (DX_W
 #define SL sl_<NPG>()
 #define GBASE gbase_<NPG>()
 template <int NPG>
-__device__ __forceinline__ float row_max_f(float m) {
-  m = fmaxf(m, dpp_f<0xB1, 0xF>(m));                      // quad_perm [1,0,3,2]
-  if (NPG >= 4) m = fmaxf(m, dpp_f<0x4E, 0xF>(m));        // quad_perm [2,3,0,1]
-  if (NPG >= 8) m = fmaxf(m, dpp_f<0x141, 0xF>(m));       // row_half_mirror (8 lanes)
-  if (NPG == 16) m = fmaxf(m, dpp_f<0x140, 0xF>(m));      // row_mirror (16 lanes)
+__device__ __forceinline__ int row_max_i(int m) {
+  m = max(m, dpp_i<0xB1, 0xF>(m));                      // quad_perm [1,0,3,2]
+  if (NPG >= 4) m = max(m, dpp_i<0x4E, 0xF>(m));        // quad_perm [2,3,0,1]
+  if (NPG >= 8) m = max(m, dpp_i<0x141, 0xF>(m));       // row_half_mirror (8 lanes)
+  if (NPG == 16) m = max(m, dpp_i<0x140, 0xF>(m));      // row_mirror (16 lanes)
+  return m;
+}
+template <int NPG>
+__device__ __forceinline__ int row_or_i(int m) {
+  m |= dpp_i<0xB1, 0xF>(m);
+  if (NPG >= 4) m |= dpp_i<0x4E, 0xF>(m);
+  if (NPG >= 8) m |= dpp_i<0x141, 0xF>(m);
+  if (NPG == 16) m |= dpp_i<0x140, 0xF>(m);
   return m;
 }
 template <int NPG>
@@ -282,35 +290,38 @@ __device__ __forceinline__ void hull_take(HullBest& h, float4 v, float d, int i,
 // Group reduction: the lowest vertex index among the lanes holding the maximum (a
 // cell's list is sorted by vertex index, a whole hull is scanned in index order, so
 // this is the vertex the oracle's serial scan returns); its coordinates reach the group
-// by a DPP max over the group in which every other lane offers -3e38 (one lane holds
-// the winning slot: the indices of a group's slots are distinct) -- no ballot and no
-// ds_bpermute round trip.
+// by a DPP or over the group in which every other lane offers 0 (one lane holds the
+// winning slot: the indices of a group's slots are distinct) -- no ballot and no
+// ds_bpermute round trip.  The maximum runs on order-preserving integers (f2ord), every
+// step one v_*_dpp instruction.
 template <int NPG>
 __device__ __forceinline__ void hull_reduce(const HullBest& h, float* lp) {
-  float vmax = row_max_f<NPG>(h.d);
-  int bi = row_min_i<NPG>(h.d == vmax ? h.i : 0x7fffffff);
-  const bool win = h.d == vmax && h.i == bi;
-  lp[0] = row_max_f<NPG>(win ? h.x : -3.0e38f);
-  lp[1] = row_max_f<NPG>(win ? h.y : -3.0e38f);
-  lp[2] = row_max_f<NPG>(win ? h.z : -3.0e38f);
+  const int kd = f2ord(h.d);
+  const int kmax = row_max_i<NPG>(kd);
+  const int bi = row_min_i<NPG>(kd == kmax ? h.i : 0x7fffffff);
+  const bool win = kd == kmax && h.i == bi;
+  lp[0] = __int_as_float(row_or_i<NPG>(win ? __float_as_int(h.x) : 0));
+  lp[1] = __int_as_float(row_or_i<NPG>(win ? __float_as_int(h.y) : 0));
+  lp[2] = __int_as_float(row_or_i<NPG>(win ? __float_as_int(h.z) : 0));
 }
 // Cube-map cell of local direction ld (host twin: dx_api.hip cell_corners).  Returns
-// -1 for a zero direction (then the whole hull is scanned, as the oracle does).
+// -1 for a zero direction (then the whole hull is scanned, as the oracle does).  No
+// branch: every lane computes a cell and selects -1 after.
 __device__ __forceinline__ int hull_cell(const float* ld, int n) {
   float ax0 = fabsf(ld[0]), ax1 = fabsf(ld[1]), ax2 = fabsf(ld[2]);
   int ax = (ax0 >= ax1 && ax0 >= ax2) ? 0 : (ax1 >= ax2 ? 1 : 2);
   float a = ax == 0 ? ld[0] : (ax == 1 ? ld[1] : ld[2]);
   float u = ax == 0 ? ld[1] : (ax == 1 ? ld[2] : ld[0]);
   float v = ax == 0 ? ld[2] : (ax == 1 ? ld[0] : ld[1]);
-  float aa = fabsf(a);
-  if (!(aa > 1e-30f)) return -1;
-  float inv = 1.0f / aa;
+  const float aa = fabsf(a);
+  const bool nz = aa > 1e-30f;
+  const float inv = 1.0f / (nz ? aa : 1.f);
   int iu = (int)((u * inv + 1.0f) * 0.5f * (float)n);
   int iv = (int)((v * inv + 1.0f) * 0.5f * (float)n);
   iu = min(max(iu, 0), n - 1);
   iv = min(max(iv, 0), n - 1);
   int face = 2 * ax + (a < 0 ? 1 : 0);
-  return (face * n + iu) * n + iv;
+  return nz ? (face * n + iu) * n + iv : -1;
 }
 // One hull's support scan by a lane group.  First a DX_HULL_K-slot block -- the
 // direction's cube-map cell (dx_api.hip build_hull_bins), or the first K vertices of a
@@ -324,17 +335,10 @@ struct HullScan {
   bool cell;             // cell scan: the vertex index is the slot's w; else the slot number
 };
 __device__ __forceinline__ void hull_block(const Shape& s, const float* ld, const DXG float4*& blk, int& n1, bool& cell) {
-  blk = s.vert4;
-  n1 = min(s.nvert, DX_HULL_K);
-  cell = false;
-  if (s.bin_n > 0) {
-    int c = hull_cell(ld, s.bin_n);
-    if (c >= 0) {
-      blk = s.bin4 + DX_HULL_K * c;
-      n1 = DX_HULL_K;
-      cell = true;
-    }
-  }
+  const int c = s.bin_n > 0 ? hull_cell(ld, max(s.bin_n, 1)) : -1;  // (selects, no branch)
+  cell = c >= 0;
+  blk = cell ? s.bin4 + DX_HULL_K * c : s.vert4;
+  n1 = cell ? DX_HULL_K : min(s.nvert, DX_HULL_K);
 }
 template <int NPG>
 __device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld, const float4 (&v)[DX_HULL_K / NPG],
@@ -343,7 +347,7 @@ __device__ __forceinline__ void hull_take_block(const Shape& s, const float* ld,
 #pragma unroll
   for (int u = 0; u < DX_SLK; u++) {
     const int sl = u * NPG + SL;
-    const int idx = cell ? __float_as_int(v[u].w) : sl;
+    const int idx = __float_as_int(v[u].w);  // (cells and whole-hull slots alike)
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < n1 && idx >= 0);
   }
   // slot K - 1 (the group's last lane, last load) of a cell: a header (index -2) names
@@ -373,7 +377,7 @@ __device__ __forceinline__ void hull_take_run(const float* ld, const float4 (&v)
 #pragma unroll
   for (int u = 0; u < DX_HULL_K / NPG; u++) {
     const int sl = base + u * NPG + SL;
-    const int idx = H.cell ? __float_as_int(v[u].w) : DX_HULL_K + sl;
+    const int idx = __float_as_int(v[u].w);  // (cells and whole-hull slots alike)
     hull_take(H.h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < H.nov && idx >= 0);
   }
 }
@@ -422,10 +426,12 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
     const Shape& s = S;
     const bool mesh = type == DXG_MESH;
     HullBest h = {-3.0e38f, 0.f, 0.f, 0.f, 0x7fffffff};
-    const DXG float4* blk = s.vert4;
-    int n1 = 0;
-    bool cell = false;
-    if (mesh) hull_block(s, ld, blk, n1, cell);
+    const DXG float4* blk;
+    int n1;
+    bool cell;
+    hull_block(s, ld, blk, n1, cell);  // (every lane: a primitive's record has no cells)
+    n1 = mesh ? n1 : 0;
+    cell = mesh && cell;
     float4 v[DX_SLH];
 #pragma unroll
     for (int u = 0; u < DX_SLH; u++) {
@@ -441,7 +447,7 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
         const int sl = H * u + q;
-        const int idx = cell ? __float_as_int(v[u].w) : sl;
+        const int idx = __float_as_int(v[u].w);  // (cells and whole-hull slots alike)
         const bool ok = mesh && sl < n1 && idx >= 0;
         dd[u] = ok ? v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2] : -3.0e38f;
         ix[u] = ok ? idx : 0x7fffffff;
@@ -491,28 +497,29 @@ __device__ __forceinline__ void support_pair(const Shape& S, const float* dir, f
 #pragma unroll
       for (int u = 0; u < DX_SLH; u++) {
         const int sl = base + H * u + q;
-        const int idx = cell ? __float_as_int(v[u].w) : DX_HULL_K + sl;
+        const int idx = __float_as_int(v[u].w);  // (cells and whole-hull slots alike)
         hull_take(h, v[u], v[u].x * ld[0] + v[u].y * ld[1] + v[u].z * ld[2], idx, sl < nov && idx >= 0);
       }
     }
     // half reduction: the lowest vertex index among the maxima, its coordinates by a DPP
-    // max in which only the winning lane offers its own (hull_reduce)
-    float vmax = fmaxf(h.d, dpp_f<0xB1, 0xF>(h.d));
-    if (H == 4) vmax = fmaxf(vmax, dpp_f<0x4E, 0xF>(vmax));
-    int bi = h.d == vmax ? h.i : 0x7fffffff;
+    // or in which only the winning lane offers its own (hull_reduce)
+    const int kd = f2ord(h.d);
+    int kmax = max(kd, dpp_i<0xB1, 0xF>(kd));
+    if (H == 4) kmax = max(kmax, dpp_i<0x4E, 0xF>(kmax));
+    int bi = kd == kmax ? h.i : 0x7fffffff;
     bi = min(bi, dpp_i<0xB1, 0xF>(bi));
     if (H == 4) bi = min(bi, dpp_i<0x4E, 0xF>(bi));
-    const bool win = h.d == vmax && h.i == bi;
-    float hx = win ? h.x : -3.0e38f, hy = win ? h.y : -3.0e38f, hz = win ? h.z : -3.0e38f;
-    hx = fmaxf(hx, dpp_f<0xB1, 0xF>(hx));
-    hy = fmaxf(hy, dpp_f<0xB1, 0xF>(hy));
-    hz = fmaxf(hz, dpp_f<0xB1, 0xF>(hz));
+    const bool win = kd == kmax && h.i == bi;
+    int hx = win ? __float_as_int(h.x) : 0, hy = win ? __float_as_int(h.y) : 0, hz = win ? __float_as_int(h.z) : 0;
+    hx |= dpp_i<0xB1, 0xF>(hx);
+    hy |= dpp_i<0xB1, 0xF>(hy);
+    hz |= dpp_i<0xB1, 0xF>(hz);
     if (H == 4) {
-      hx = fmaxf(hx, dpp_f<0x4E, 0xF>(hx));
-      hy = fmaxf(hy, dpp_f<0x4E, 0xF>(hy));
-      hz = fmaxf(hz, dpp_f<0x4E, 0xF>(hz));
+      hx |= dpp_i<0x4E, 0xF>(hx);
+      hy |= dpp_i<0x4E, 0xF>(hy);
+      hz |= dpp_i<0x4E, 0xF>(hz);
     }
-    if (mesh) { lp[0] = hx; lp[1] = hy; lp[2] = hz; }
+    if (mesh) { lp[0] = __int_as_float(hx); lp[1] = __int_as_float(hy); lp[2] = __int_as_float(hz); }
   }
   if (type != DXG_MESH) support_prim(S, ld, lp);
   // world point (+ the half margin along this half's direction), then the halves swap
