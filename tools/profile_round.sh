@@ -6,6 +6,8 @@ set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/prof
 rm -rf "$O"; mkdir -p "$O"
+# the library the passes measure (bench.py uses the recorded HBM bytes only for this build)
+python3 -c "import sys; sys.path.insert(0, '$R'); from dexterity_amd import _lib; print(_lib.load().dx_build_key().decode())" > "$O/build_key.txt"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/trace" -o run --output-format csv -- \
   python3 "$R/bench.py" --steps 40 --warmup 5 --no-cpu-baseline --host-api-steps 0 > "$O/bench_under_rocprof.log" 2>&1

@@ -76,6 +76,10 @@ json.dump({
     "write_size_kb_median": w_kb,
     "correction": "read bytes = 2 x FETCH_SIZE (gfx950), write bytes = WRITE_SIZE; separate PMC passes",
     "source": f"profiles/{tag}_pmc_hbm.csv",
+    # the measured library's source hash (dx_build_key): bench.py reports these bytes as
+    # roofline.traffic only when it runs that same build, else traffic is null
+    "build_key": open(os.path.join(SRC, "build_key.txt")).read().strip()
+    if os.path.exists(os.path.join(SRC, "build_key.txt")) else None,
 }, open(os.path.join(DST, "pmc_step_kernel.json"), "w"), indent=1)
 for ext in ("json", "log"):
     p = os.path.join(SRC, f"stages.{ext}")
