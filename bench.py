@@ -296,7 +296,8 @@ def main():
                 p = json.load(f)
             # only the build the PMC passes measured (profiles/pmc_step_kernel.json
             # build_key = this library's dx_build_key); otherwise unmeasured
-            key = _lib.load().dx_build_key().decode() if hasattr(_lib.load(), "dx_build_key") else None
+            lib = _lib.load()
+            key = lib.dx_build_key().decode() if hasattr(lib, "dx_build_key") else None
             if p.get("envs") == B and p.get("build_key") and p.get("build_key") == key:
                 traffic = p.get("hbm_bytes_per_launch")
         host_api = host_api_line(env, args.host_api_steps, 5) if world == 1 and args.host_api_steps > 0 else None

@@ -86,8 +86,9 @@ def load(path: str = LIB_PATH):
             f"{path} not found: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
         )
     L = ctypes.CDLL(path)
-    if path == os.path.join(_HERE, "libdx.so") and os.path.isdir(os.path.join(_HERE, "csrc")):
+    if hasattr(L, "dx_build_key"):
         L.dx_build_key.restype = ctypes.c_char_p
+    if path == os.path.join(_HERE, "libdx.so") and os.path.isdir(os.path.join(_HERE, "csrc")):
         # the in-tree library must have been built from the sources beside it (a GPU box
         # runs the library that travelled with the tree, without rebuilding)
         from dexterity_amd import build as _build

@@ -68,7 +68,9 @@ def _units() -> list:
     # take ~430 VGPRs (dx_step.hip solve_pgs_ar), which two waves per SIMD would spill
     # (CG too: its launch is bound by its slowest envs' chains, which run faster alone on a
     # SIMD -- config 3' 0.872 -> 0.900 M env-steps/s same-box, round 6)
-    waves = {"_pgs": os.environ.get("DX_PGS_WAVES", "1"), "_cg": os.environ.get("DX_CG_WAVES", "1")}
+    # (reach: DX_REACH_WAVES, an experiment -- config 2's 1024 envs fill half the slots)
+    waves = {"_pgs": os.environ.get("DX_PGS_WAVES", "1"), "_cg": os.environ.get("DX_CG_WAVES", "1"),
+             "_reach": os.environ.get("DX_REACH_WAVES", "")}
 
     def spec_flags(n):
         w = next((v for k, v in waves.items() if n.endswith(k) and v), None)

@@ -791,9 +791,9 @@ __device__ __forceinline__ void mfma_chol_solve32(const float* A, int n, float d
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // C[k][j], C[k+1][j]
-    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
-    const float l21 = rl(rk1, k) * i11;
-    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(C[vk], k + (up ? 32 : 0)), 1e-30f));
+    const float l21 = rl(C[vk + 1], k + (up ? 32 : 0)) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(C[vk + 1], k + 1 + (up ? 32 : 0)) - l21 * l21, 1e-30f));
     dinv = wl(dinv, i11, k);
     dinv = wl(dinv, i22, k + 1);
     const float lk = rk * i11;                  // L[j][k]   (j > k)
@@ -911,9 +911,9 @@ __device__ __forceinline__ void mfma_chol_solve64(const float* A, int n, float d
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C22[vk], up), rk1 = half_dup(C22[vk + 1], up);
-    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
-    const float l21 = rl(rk1, k) * i11;
-    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(C22[vk], k + (up ? 32 : 0)), 1e-30f));
+    const float l21 = rl(C22[vk + 1], k + (up ? 32 : 0)) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(C22[vk + 1], k + 1 + (up ? 32 : 0)) - l21 * l21, 1e-30f));
     dinv = wl(dinv, i11, 32 + k);
     dinv = wl(dinv, i22, 32 + k + 1);
     const float lk = rk * i11, lk1 = (rk1 - lk * l21) * i22;  // L[32+j][32+k], L[32+j][32+k+1]
@@ -1019,7 +1019,10 @@ __device__ __forceinline__ void mfma_sweep_solve30(const float* A, int n, float 
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // S[k][j], S[k+1][j]
-    const float p00 = rl(rk, k), p10 = rl(rk1, k), p11 = rl(rk1, k + 1);
+    // the pivot block straight from the accumulator (lane k + 32 up holds column k of rows
+    // k, k + 1): the readlanes and the 2 x 2 inverse do not wait for the half swaps
+    const int kl = k + (up ? 32 : 0);
+    const float p00 = rl(C[vk], kl), p10 = rl(C[vk + 1], kl), p11 = rl(C[vk + 1], kl + 1);
     const float id = 1.0f / (p00 * p11 - p10 * p10);
     const float w00 = p11 * id, w01 = -p10 * id, w11 = p00 * id;
     const bool pc = j == k || j == k + 1;  // a pivot column
@@ -1094,7 +1097,10 @@ __device__ __forceinline__ void mfma_sweep_inverse30(const float* A, int n, floa
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // S[k][j], S[k+1][j]
-    const float p00 = rl(rk, k), p10 = rl(rk1, k), p11 = rl(rk1, k + 1);
+    // the pivot block straight from the accumulator (lane k + 32 up holds column k of rows
+    // k, k + 1): the readlanes and the 2 x 2 inverse do not wait for the half swaps
+    const int kl = k + (up ? 32 : 0);
+    const float p00 = rl(C[vk], kl), p10 = rl(C[vk + 1], kl), p11 = rl(C[vk + 1], kl + 1);
     const float id = 1.0f / (p00 * p11 - p10 * p10);
     const float w00 = p11 * id, w01 = -p10 * id, w11 = p00 * id;
     const bool pc = j == k || j == k + 1;  // a pivot column
@@ -1172,9 +1178,9 @@ __device__ __forceinline__ void mfma_chol_factor30(float* A, int n) {
     const int vk = 4 * (k >> 3) + (k & 3);
     const bool up = (k & 7) >= 4;
     const float rk = half_dup(C[vk], up), rk1 = half_dup(C[vk + 1], up);  // C[k][j], C[k+1][j]
-    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(rk, k), 1e-30f));
-    const float l21 = rl(rk1, k) * i11;
-    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(rk1, k + 1) - l21 * l21, 1e-30f));
+    const float i11 = __builtin_amdgcn_rsqf(fmaxf(rl(C[vk], k + (up ? 32 : 0)), 1e-30f));
+    const float l21 = rl(C[vk + 1], k + (up ? 32 : 0)) * i11;
+    const float i22 = __builtin_amdgcn_rsqf(fmaxf(rl(C[vk + 1], k + 1 + (up ? 32 : 0)) - l21 * l21, 1e-30f));
     const float lk = rk * i11;                 // G[j][k]   (j >= k; the diagonal at j = k)
     const float lk1 = (rk1 - lk * l21) * i22;  // G[j][k+1] (j >= k + 1)
     if (hi == 0 && j >= k && j < n) A[ti(j) + k] = lk;

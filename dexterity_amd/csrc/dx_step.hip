@@ -1871,16 +1871,23 @@ __device__ __forceinline__ void velocity_stage(const Ctx& c, const float* xfrc) 
 // ------------------------------------------------------------------------ //
 // Newton solver
 // ------------------------------------------------------------------------ //
+// The force and Hessian weight of row_cost by selects (the line searches' inner loops:
+// the lanes hold rows of every type and zone at once, so row_cost's early returns were
+// exec-mask branches taken both ways).  The same zones and values.
+__device__ __forceinline__ void row_force(int type, float D, float fl, float Rf, float jar, float& force, float& hw) {
+  const bool fr = type == DXR_FRIC;
+  const bool lo = fr && jar <= -Rf, hi = fr && jar >= Rf;  // friction's linear zones
+  const bool quad = fr ? !(lo || hi) : jar < 0;             // the quadratic zone
+  force = lo ? fl : hi ? -fl : quad ? -D * jar : 0.f;
+  hw = quad ? D : 0.f;
+}
 // row cost at jar -> (cost, force, hessian weight)
 __device__ __forceinline__ float row_cost(int type, float D, float fl, float Rf, float jar, float& force, float& hw) {
-  if (type == DXR_FRIC) {
-    if (jar <= -Rf) { force = fl; hw = 0; return -fl * jar - 0.5f * Rf * fl; }
-    if (jar >= Rf) { force = -fl; hw = 0; return fl * jar - 0.5f * Rf * fl; }
-  } else if (jar >= 0) {
-    force = 0; hw = 0; return 0;
-  }
-  force = -D * jar; hw = D;
-  return 0.5f * D * jar * jar;
+  row_force(type, D, fl, Rf, jar, force, hw);
+  const bool fr = type == DXR_FRIC;
+  const bool lo = fr && jar <= -Rf, hi = fr && jar >= Rf;
+  const bool quad = fr ? !(lo || hi) : jar < 0;
+  return lo ? -fl * jar - 0.5f * Rf * fl : hi ? fl * jar - 0.5f * Rf * fl : quad ? 0.5f * D * jar * jar : 0.f;
 }
 
 // y = M x (lanes over rows).  For n <= 32 the row is gathered with 32 independent
@@ -2075,13 +2082,13 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     float fc[3] = {0, 0, 0};
     if ((__float_as_int(r[14]) >> 8) == 1) {
       float f, hw;
-      if (row0 < nefc) { row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); fc[0] = f; }
+      if (row0 < nefc) { row_force(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw); fc[0] = f; }
     } else {
       for (int e = 0; e < 4; e++) {
         int row = row0 + e;
         if (row >= nefc) break;
         float f, hw;
-        row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+        row_force(DXR_CON, D[row], 0, 0, jar[row], f, hw);
         int k = 1 + (e >> 1);
         float mu = r[15 + k] * ((e & 1) ? -1.f : 1.f);
         fc[0] += f;
@@ -2097,19 +2104,19 @@ __device__ __forceinline__ void jac_t_force(const Ctx& c, float* out) {
     float s = 0;
     // friction row of this dof
     int fr = m.dof_fricrow[d];
-    if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += f; }
+    if (fr >= 0) { float f, hw; row_force(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += f; }
     for (int r = c.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, aux = (mt >> 4) & 15, id = mt >> 8;
       if (type == DXR_LIMJ) {
         if (id != d) continue;
         float f, hw;
-        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        row_force(type, D[r], 0, 0, jar[r], f, hw);
         s += aux ? -f : f;
       } else if (type == DXR_LIMT) {
         float tj = m.tendon_J[id * nv + d];
         if (tj == 0) continue;
         float f, hw;
-        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        row_force(type, D[r], 0, 0, jar[r], f, hw);
         s += (aux ? -tj : tj) * f;
       } else {
         break;  // contact rows are last
@@ -2158,13 +2165,13 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
   for (int d = LANE; d < nv; d += DX_WAVE) {
     float s = 0;
     int fr = m.dof_fricrow[d];
-    if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
+    if (fr >= 0) { float f, hw; row_force(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
     for (int r = c.nfric; r < nefc; r++) {
       int mt = meta[r], type = mt & 15, id = mt >> 8;
       if (type != DXR_LIMJ) { if (type == DXR_LIMT) continue; break; }
       if (id != d) continue;
       float f, hw;
-      row_cost(type, D[r], 0, 0, jar[r], f, hw);
+      row_force(type, D[r], 0, 0, jar[r], f, hw);
       s += hw;
     }
     H[ti(d) + d] += s;
@@ -2176,7 +2183,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
     if (type == DXR_CON || type == DXR_CONFL) break;
     if (type != DXR_LIMT) continue;
     float f, hw;
-    row_cost(type, D[r], 0, 0, jar[r], f, hw);
+    row_force(type, D[r], 0, 0, jar[r], f, hw);
     if (hw == 0) continue;
     const float* tj = m.tendon_J + id * nv;
     for (int i = LANE; i < nv; i += DX_WAVE)
@@ -2206,7 +2213,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
       if ((__float_as_int(r[14]) >> 8) == 1) {
         if (row0 < nefc) {
           float f, hw;
-          row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+          row_force(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
           w00 = hw;
         }
       } else {
@@ -2214,7 +2221,7 @@ __device__ __forceinline__ void build_hessian(const Ctx& c) {
           const int row = row0 + e;
           if (row >= nefc) break;
           float f, hw;
-          row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+          row_force(DXR_CON, D[row], 0, 0, jar[row], f, hw);
           const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
           w00 += hw;
           if (e < 2) { w01 += hw * mu; w11 += hw * mu * mu; }
@@ -2284,13 +2291,13 @@ __device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, flo
     const int d = LANE & 31;
     if (d < nv) {
       const int fr = m.dof_fricrow[d];
-      if (fr >= 0) { float f, hw; row_cost(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
+      if (fr >= 0) { float f, hw; row_force(DXR_FRIC, D[fr], fl[fr], Rf[fr], jar[fr], f, hw); s += hw; }
       for (int r = c.nfric; r < nefc; r++) {
         const int mt = meta[r], type = mt & 15, id = mt >> 8;
         if (type != DXR_LIMJ) break;  // (no tendon-limit rows on this path)
         if (id != d) continue;
         float f, hw;
-        row_cost(type, D[r], 0, 0, jar[r], f, hw);
+        row_force(type, D[r], 0, 0, jar[r], f, hw);
         s += hw;
       }
     }
@@ -2313,7 +2320,7 @@ __device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, flo
       if ((__float_as_int(r[14]) >> 8) == 1) {
         if (row0 < nefc) {
           float f, hw;
-          row_cost(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
+          row_force(DXR_CONFL, D[row0], 0, 0, jar[row0], f, hw);
           w[0] = hw;
         }
       } else {
@@ -2321,7 +2328,7 @@ __device__ __forceinline__ float build_hessian_inc(const Ctx& c, bool first, flo
           const int row = row0 + e;
           if (row >= nefc) break;
           float f, hw;
-          row_cost(DXR_CON, D[row], 0, 0, jar[row], f, hw);
+          row_force(DXR_CON, D[row], 0, 0, jar[row], f, hw);
           const float mu = r[16 + (e >> 1)] * ((e & 1) ? -1.f : 1.f);
           w[0] += hw;
           if (e < 2) { w[1] += hw * mu; w[3] += hw * mu * mu; }
@@ -2462,7 +2469,7 @@ __device__ __forceinline__ float line_search(const Ctx& c, const float* qacc, co
     for (int k = 0; k < DX_LS_SLOTS; k++) {
       if (k < ns) {
         float f, hw;
-        row_cost(ty[k], D[k], fl[k], Rf[k], ja[k] + alpha * jj[k], f, hw);
+        row_force(ty[k], D[k], fl[k], Rf[k], ja[k] + alpha * jj[k], f, hw);
         g -= f * jj[k];
         h += hw * jj[k] * jj[k];
       }
@@ -2575,7 +2582,7 @@ __device__ __forceinline__ void solve_cg_reg(const Ctx& c, float scale, float to
     for (int h = 0; h < 2; h++) {
       if (DX_WAVE * h < nefc) {
         float f, hw;
-        row_cost(ty[h], D[h], fl[h], Rf[h], ja[h], f, hw);
+        row_force(ty[h], D[h], fl[h], Rf[h], ja[h], f, hw);
 #pragma unroll
         for (int d = 0; d < 30; d++) t[d] = fmaf(f, Jd[h][d], t[d]);
       }
@@ -2620,7 +2627,7 @@ __device__ __forceinline__ void solve_cg_reg(const Ctx& c, float scale, float to
       for (int h = 0; h < 2; h++) {
         if (DX_WAVE * h < nefc) {
           float f, hw;
-          row_cost(ty[h], D[h], fl[h], Rf[h], ja[h] + alpha * jj[h], f, hw);
+          row_force(ty[h], D[h], fl[h], Rf[h], ja[h] + alpha * jj[h], f, hw);
           g -= f * jj[h];
           hh += hw * jj[h] * jj[h];
         }
@@ -2769,7 +2776,7 @@ __device__ __forceinline__ void solve_cg(const Ctx& c, float scale, float tol) {
         const int r = lane + DX_WAVE * h, rc = min(r, nefc - 1);
         const bool fr = r < c.nfric;
         float f, hw;
-        row_cost(meta[rc] & 15, Dp[rc], fr ? flp[rc] : 0.f, fr ? Rfp[rc] : 0.f, jar[rc], f, hw);
+        row_force(meta[rc] & 15, Dp[rc], fr ? flp[rc] : 0.f, fr ? Rfp[rc] : 0.f, jar[rc], f, hw);
         f = r < nefc ? f : 0.f;
 #pragma unroll
         for (int d = 0; d < 30; d++) t[d] = fmaf(f, Jd[h][d], t[d]);
@@ -3256,7 +3263,7 @@ __device__ __forceinline__ void solve_pgs(const Ctx& c, float scale, float tol) 
   for (int r = LANE; r < nefc; r += DX_WAVE) {
     const bool fr = r < c.nfric;
     float fo, hw;
-    row_cost(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r], fo, hw);
+    row_force(meta[r] & 15, D[r], fr ? fl[r] : 0.f, fr ? Rf[r] : 0.f, jar[r], fo, hw);
     f[r] = fo;
     dc += 0.5f * fo * fo / D[r] - fo * aref[r];
   }
