@@ -50,14 +50,17 @@ __device__ __forceinline__ int f2ord(float f) {
 }
 __device__ __forceinline__ float ord2f(int k) { return __int_as_float(k ^ ((k >> 31) & 0x7fffffff)); }
 // Sums: quad, half-row, row sums by DPP, then rows carried up to lane 63 (each lane
-// contributes exactly once), broadcast with readlane.
+// contributes exactly once), broadcast with readlane.  The two row broadcasts run with
+// every row enabled, so they fold into their operation too: rows 0-2 may read a source
+// that does not exist, but lane 63 reads only lane 47 (row 2's sum) and then lane 31
+// (rows 0 + 1), whatever the other rows hold -- and only lane 63 is read.
 __device__ __forceinline__ float wave_sum(float v) {
   v += dpp_f<0xB1, 0xF>(v);
   v += dpp_f<0x4E, 0xF>(v);
   v += dpp_f<0x141, 0xF>(v);
   v += dpp_f<0x140, 0xF>(v);
-  v += dpp_f<0x142, 0xA>(v);
-  v += dpp_f<0x143, 0xC>(v);
+  v += dpp_f<0x142, 0xF>(v);
+  v += dpp_f<0x143, 0xF>(v);
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 __device__ __forceinline__ int wave_sum_i(int v) {
@@ -65,8 +68,8 @@ __device__ __forceinline__ int wave_sum_i(int v) {
   v += dpp_i<0x4E, 0xF>(v);
   v += dpp_i<0x141, 0xF>(v);
   v += dpp_i<0x140, 0xF>(v);
-  v += dpp_i<0x142, 0xA>(v);
-  v += dpp_i<0x143, 0xC>(v);
+  v += dpp_i<0x142, 0xF>(v);
+  v += dpp_i<0x143, 0xF>(v);
   return __builtin_amdgcn_readlane(v, 63);
 }
 __device__ __forceinline__ int wave_max_i(int m) {
@@ -74,8 +77,8 @@ __device__ __forceinline__ int wave_max_i(int m) {
   m = max(m, dpp_i<0x4E, 0xF>(m));
   m = max(m, dpp_i<0x141, 0xF>(m));
   m = max(m, dpp_i<0x140, 0xF>(m));
-  m = max(m, dpp_i<0x142, 0xA>(m));
-  m = max(m, dpp_i<0x143, 0xC>(m));
+  m = max(m, dpp_i<0x142, 0xF>(m));
+  m = max(m, dpp_i<0x143, 0xF>(m));
   return __builtin_amdgcn_readlane(m, 63);
 }
 __device__ __forceinline__ float wave_max_f(float m) { return ord2f(wave_max_i(f2ord(m))); }
@@ -84,8 +87,8 @@ __device__ __forceinline__ int wave_min_i(int m) {
   m = min(m, dpp_i<0x4E, 0xF>(m));
   m = min(m, dpp_i<0x141, 0xF>(m));
   m = min(m, dpp_i<0x140, 0xF>(m));
-  m = min(m, dpp_i<0x142, 0xA>(m));
-  m = min(m, dpp_i<0x143, 0xC>(m));
+  m = min(m, dpp_i<0x142, 0xF>(m));
+  m = min(m, dpp_i<0x143, 0xF>(m));
   return __builtin_amdgcn_readlane(m, 63);
 }
 // index of the first (lowest-index) maximum over lanes' (best, index) pairs
